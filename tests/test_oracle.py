@@ -1,0 +1,72 @@
+"""Pin the CPU oracle against the reference's own outputs (golden fixtures)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import unproject_ref as ref
+
+
+def _bits_equal(a, b):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
+
+
+@pytest.mark.parametrize("loop", [True, False])
+def test_oracle_matches_reference_fixtures(unproject_cases, loop):
+    for c in unproject_cases:
+        pts, cols = ref.depth_to_point_cloud(c["image"], c["depth"], density=c["density"],
+                                             invert=c["invert"], depth_scale=c["scale"], loop=loop)
+        assert _bits_equal(pts, c["points"]), c["name"]
+        assert _bits_equal(cols, c["colors"]), c["name"]
+        b = ref.gis_bounds(pts)
+        got = np.array([b[k] for k in ("minX", "maxX", "minY", "maxY", "minZ", "maxZ")])
+        assert _bits_equal(got, c["bounds"]), c["name"]
+        assert len(pts) == ref.point_count(c["h"], c["w"], c["density"])
+
+
+def test_percentile_restatement_matches_numpy():
+    rng = np.random.Generator(np.random.PCG64(11))
+    for n in (1, 2, 3, 50, 147_456, 268_324):
+        d = rng.normal(size=n).astype(np.float32)
+        if n > 100:
+            d[:n // 10] = d[0]          # ties
+        p2, p98 = ref.percentile_2_98(d)
+        e2, e98 = np.percentile(d, [2, 98])
+        assert (p2, p98) == (float(e2), float(e98)), n
+
+
+def test_nanmedian_restatement_matches_numpy():
+    rng = np.random.Generator(np.random.PCG64(12))
+    for n in (1, 2, 7, 8, 1001):
+        d = rng.normal(size=n).astype(np.float32)
+        d[rng.choice(n, max(0, n // 5), replace=False)] = np.nan
+        if n > 5:
+            d[0] = np.inf
+        got = ref.nanmedian_f32(d)
+        exp = np.nanmedian(d)
+        assert np.float32(exp).tobytes() == np.float32(got).tobytes(), n
+
+
+def test_pipeline_preview_and_bounds(pipeline_case):
+    s = pipeline_case["summary"]
+    pts, cols = ref.depth_to_point_cloud(pipeline_case["image"], pipeline_case["depth"],
+                                         density=s["gisData"]["pointDensity"], loop=False)
+    assert len(pts) == s["pointCloud"]["points"]
+    assert ref.gis_bounds(pts) == s["gisData"]["bounds"]
+    pp, pc = ref.preview(pts, cols)
+    assert len(pp) == s["preview_len"]
+    assert hashlib.sha256(np.asarray(pp, np.float64).tobytes()).hexdigest() == s["preview_points_sha256"]
+    assert hashlib.sha256(np.asarray(pc, np.float64).tobytes()).hexdigest() == s["preview_colors_sha256"]
+
+
+def test_resize_linear_matches_torch_bilinear():
+    torch = pytest.importorskip("torch")
+    rng = np.random.Generator(np.random.PCG64(13))
+    for (h, w, H, W) in ((384, 384, 1024, 1024), (37, 53, 100, 90), (518, 686, 768, 1024)):
+        d = rng.random((h, w), dtype=np.float32)
+        got = ref.resize_linear_cv2(d, W, H)
+        t = torch.nn.functional.interpolate(torch.from_numpy(d)[None, None], size=(H, W),
+                                            mode="bilinear", align_corners=False)[0, 0].numpy()
+        assert np.max(np.abs(got - t)) < 2e-4   # torch rounds the source coordinate in fp32, cv2 in fp64
