@@ -1,0 +1,797 @@
+// Batched depth -> (x, y, z, rgb) back-projection for gfx950 (MI355X).
+//
+// Replaces backend/app.py:174-250 (depth_to_point_cloud) and the bounds of
+// generate_gis_metadata (app.py:393-400) for a whole batch of images.
+//
+// Pipeline per call (all stream-ordered, graph-capturable, fixed launch list):
+//   k_init            per-image selection state + cv2 INTER_LINEAR tap tables
+//   k_sel_hist/resolve x3 levels (pass 0)   exact order statistics of the
+//                     full-resolution depth (recomputed on the fly from the
+//                     model-resolution map, which stays L2-resident): the
+//                     p2/p98 ranks of np.percentile (app.py:197) -- or, if the
+//                     map holds NaN/Inf, the ranks of np.nanmedian (app.py:195)
+//   k_sel_hist/resolve x3 levels (pass 1)   only when a nanmedian fill was
+//                     needed: p2/p98 of the sanitised map (no-op launches otherwise)
+//   [k_norm_field, k_blur_rows, k_blur_cols]  only when smooth=True (app.py:209-214)
+//   k_unproject       normalise (fp64 / fp32 / constant branch exactly as
+//                     numpy evaluates app.py:198-206), pinhole back-projection in
+//                     Python-double semantics (app.py:219-238), RGB gather
+//                     (app.py:239-244), per-image bbox via wave reductions
+//   k_finalize        bbox / stats to float64
+//
+// Selection: 3-level radix select on order-preserving 32-bit float keys
+// (11 + 11 + 10 bits) with LDS histograms and wave-aggregated LDS atomics
+// (a smooth depth field puts most lanes of a wave in the same bin).
+// Arithmetic is bit-faithful: no FMA contraction in this file.
+#include "common.h"
+
+#include <algorithm>
+#include <cmath>
+
+#pragma clang fp contract(off)
+
+namespace i2pc {
+namespace unproj {
+
+constexpr int kSlots = 4;
+constexpr int kBins = 2048;
+constexpr int kBlock = 256;
+
+enum Phase : uint32_t { PH_INIT = 0, PH_PCT = 1, PH_MED = 2, PH_PCT2_INIT = 3, PH_PCT2 = 4, PH_DONE = 5 };
+
+struct Tap {
+  int i0, i1;     // i1 < 0: single tap (cv2 HResizeLinear right border copies S[sx])
+  float w0, w1;
+};
+
+struct alignas(16) SelState {
+  uint32_t phase;
+  uint32_t n;            // pixels per image
+  uint32_t nan_count;
+  uint32_t nonfinite_count;
+  uint32_t kmin, kmax;   // ordered keys of the non-NaN values of the current pass
+  uint32_t ntgt, nslot;
+  uint32_t rank[4];      // remaining rank of each target inside its prefix range
+  uint32_t prefix[4];
+  uint32_t slot[4];
+  uint32_t slot_prefix[4];
+  uint32_t med_ranks;    // 1 = odd count (one rank), 2 = even
+  uint32_t has_med;
+  float med;
+  int32_t mode;          // 0: float64 branch, 1: float32 min/max branch, 2: constant
+  uint32_t err;
+  uint32_t pad0;
+  double p2, p98, den64;
+  float lo32, hi32, den32, pad1;
+  uint32_t bbox_key[6];
+  uint32_t pad2[2];
+};
+
+struct Geo {
+  const float* depth;
+  int dh, dw, H, W;
+  const Tap* xt;
+  const Tap* yt;
+  int same;  // depth already at image resolution: app.py:187 skips cv2.resize
+};
+
+struct Layout {
+  size_t state, hist, xtab, ytab, field, tmp, total;
+};
+
+static Layout layout(int B, int H, int W, int smooth) {
+  Layout L{};
+  size_t off = 0;
+  L.state = off; off = align_up(off + sizeof(SelState) * (size_t)B, 256);
+  L.hist = off;  off = align_up(off + sizeof(uint32_t) * kSlots * kBins * (size_t)B, 256);
+  L.xtab = off;  off = align_up(off + sizeof(Tap) * (size_t)W, 256);
+  L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
+  L.field = off;
+  if (smooth) {
+    off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
+    L.tmp = off;
+    off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
+  } else {
+    L.tmp = off;
+  }
+  L.total = off;
+  return L;
+}
+
+// ---------------------------------------------------------------- device utils
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+// Blocks b and b+8 share an XCD (round-robin dispatch): when the batch is a
+// multiple of 8, give every image's blocks to one XCD so its model-resolution
+// depth map is read from one L2.
+__device__ __forceinline__ void map_block(int bid, int B, int G, int& b, int& chunk) {
+  if ((B & 7) == 0) {
+    int xcd = bid & 7, slot = bid >> 3, per = B >> 3;
+    b = xcd + 8 * (slot % per);
+    chunk = slot / per;
+  } else {
+    b = bid % B;
+    chunk = bid / B;
+  }
+}
+
+__device__ __forceinline__ float sample(const Geo& g, int b, int v, int u) {
+  const float* D = g.depth + (size_t)b * g.dh * g.dw;
+  if (g.same) return D[(size_t)v * g.dw + u];
+  const Tap ty = g.yt[v];
+  const Tap tx = g.xt[u];
+  const float* r0 = D + (size_t)ty.i0 * g.dw;
+  const float* r1 = D + (size_t)ty.i1 * g.dw;
+  float h0, h1;
+  if (tx.i1 < 0) {
+    h0 = r0[tx.i0];
+    h1 = r1[tx.i0];
+  } else {
+    h0 = r0[tx.i0] * tx.w0 + r0[tx.i1] * tx.w1;
+    h1 = r1[tx.i0] * tx.w0 + r1[tx.i1] * tx.w1;
+  }
+  return h0 * ty.w0 + h1 * ty.w1;
+}
+
+// Wave-aggregated LDS histogram add: lanes with equal bins are merged (up to 4
+// distinct bins per wave-instruction), the rest fall back to per-lane atomics.
+__device__ __forceinline__ void agg_add(uint32_t* h, int bin, bool active) {
+  const int lane = threadIdx.x & 63;
+  uint64_t pending = __ballot(active);
+  for (int it = 0; it < 4 && pending; ++it) {
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const int lbin = __shfl(bin, leader);
+    const uint64_t same = __ballot(active && bin == lbin) & pending;
+    if (lane == leader) atomicAdd(&h[lbin], (uint32_t)__popcll(same));
+    pending &= ~same;
+  }
+  if ((pending >> lane) & 1ull) atomicAdd(&h[bin], 1u);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+  for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
+  return x;
+}
+
+// cv2 resize.cpp INTER_LINEAR tap geometry (fx computed in double, cast to float).
+__device__ Tap make_tap(int dx, int in, int out) {
+  const double scale = 1.0 / ((double)out / (double)in);
+  float fx = (float)(((double)dx + 0.5) * scale - 0.5);
+  int sx = (int)floorf(fx);
+  fx = fx - (float)sx;
+  Tap t;
+  bool right = false;
+  if (sx < 0) { fx = 0.f; sx = 0; }
+  if (sx >= in - 1) { fx = 0.f; sx = in - 1; right = true; }
+  t.i0 = sx;
+  t.i1 = right ? -1 : sx + 1;
+  t.w0 = 1.0f - fx;
+  t.w1 = fx;
+  return t;
+}
+
+// ---------------------------------------------------------------- kernels
+
+__global__ void k_init(SelState* st, int B, int n, Tap* xt, Tap* yt, int dh, int dw, int H, int W) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid < B) {
+    SelState s{};
+    s.phase = PH_INIT;
+    s.n = (uint32_t)n;
+    s.kmin = 0xffffffffu;
+    s.kmax = 0u;
+    for (int i = 0; i < 6; i += 2) { s.bbox_key[i] = 0xffffffffu; s.bbox_key[i + 1] = 0u; }
+    s.med = __uint_as_float(0x7fc00000u);
+    st[tid] = s;
+  }
+  if (tid < W) {
+    Tap t = make_tap(tid, dw, W);
+    if (dw == 1) { t.i0 = 0; t.i1 = -1; t.w0 = 1.f; t.w1 = 0.f; }
+    xt[tid] = t;
+  }
+  if (tid < H) {
+    Tap t = make_tap(tid, dh, H);
+    // vertical pass always uses two rows: the second clamps to the last row
+    if (t.i1 < 0) t.i1 = t.i0;
+    yt[tid] = t;
+  }
+}
+
+template <int PASS>
+__device__ __forceinline__ bool hist_gate(uint32_t phase, int level) {
+  if (PASS == 0) return level == 0 ? phase == PH_INIT : (phase == PH_PCT || phase == PH_MED);
+  return level == 0 ? phase == PH_PCT2_INIT : phase == PH_PCT2;
+}
+
+template <int LEVEL, int PASS>
+__global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32_t* hist, int B, int G) {
+  __shared__ uint32_t sh[kSlots * kBins];
+  __shared__ uint32_t red[4][4];
+  int b, chunk;
+  map_block(blockIdx.x, B, G, b, chunk);
+  SelState* S = st + b;
+  const uint32_t phase = S->phase;
+  if (!hist_gate<PASS>(phase, LEVEL)) return;
+
+  const int nslot = LEVEL == 0 ? 1 : (int)S->nslot;
+  uint32_t sp[kSlots];
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) sp[s] = S->slot_prefix[s];
+  const bool sanitize = PASS == 1;
+  const float med = S->med;
+  constexpr int match_shift = LEVEL == 1 ? 21 : 10;
+  constexpr int bin_shift = LEVEL == 0 ? 21 : (LEVEL == 1 ? 10 : 0);
+  constexpr uint32_t bin_mask = LEVEL == 2 ? 1023u : 2047u;
+
+  for (int i = threadIdx.x; i < nslot * kBins; i += kBlock) sh[i] = 0;
+  __syncthreads();
+
+  const int n = g.H * g.W;
+  const int per = (n + G - 1) / G;
+  const int start = chunk * per;
+  const int end = min(n, start + per);
+  uint32_t nan_c = 0, nonfin_c = 0, kmin = 0xffffffffu, kmax = 0u;
+  for (int base = start; base < end; base += kBlock) {
+    const int p = base + threadIdx.x;
+    bool active = p < end;
+    float val = 0.f;
+    if (active) {
+      const int v = p / g.W;
+      const int u = p - v * g.W;
+      val = sample(g, b, v, u);
+      if (sanitize && !isfinite(val)) val = med;
+    }
+    if (LEVEL == 0 && active && !isfinite(val)) ++nonfin_c;   // NaN and +-Inf
+    if (active && isnan(val)) { ++nan_c; active = false; }
+    const uint32_t key = f2key(val);
+    int bin = 0;
+    if (LEVEL == 0) {
+      if (active) { kmin = min(kmin, key); kmax = max(kmax, key); }
+      bin = (int)((key >> bin_shift) & bin_mask);
+    } else {
+      bool hit = false;
+#pragma unroll
+      for (int s = 0; s < kSlots; ++s) {
+        if (s < nslot && (key >> match_shift) == sp[s]) { hit = true; bin = s * kBins + (int)((key >> bin_shift) & bin_mask); }
+      }
+      active = active && hit;
+    }
+    agg_add(sh, bin, active);
+  }
+  if (LEVEL == 0) {
+    const int wid = threadIdx.x >> 6;
+    nan_c = wave_sum_u32(nan_c);
+    nonfin_c = wave_sum_u32(nonfin_c);
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
+    if ((threadIdx.x & 63) == 0) { red[0][wid] = nan_c; red[1][wid] = nonfin_c; red[2][wid] = kmin; red[3][wid] = kmax; }
+  }
+  __syncthreads();
+  if (LEVEL == 0 && threadIdx.x == 0) {
+    uint32_t a = 0, c = 0, mn = 0xffffffffu, mx = 0;
+    for (int w = 0; w < kBlock / 64; ++w) { a += red[0][w]; c += red[1][w]; mn = min(mn, red[2][w]); mx = max(mx, red[3][w]); }
+    if (a) atomicAdd(&S->nan_count, a);
+    if (c) atomicAdd(&S->nonfinite_count, c);
+    if (mn != 0xffffffffu) atomicMin(&S->kmin, mn);
+    if (mx) atomicMax(&S->kmax, mx);
+  }
+  uint32_t* gh = hist + (size_t)b * kSlots * kBins;
+  for (int i = threadIdx.x; i < nslot * kBins; i += kBlock) {
+    const uint32_t c = sh[i];
+    if (c) atomicAdd(&gh[i], c);
+  }
+}
+
+// Find, for one histogram of `nb` bins, the bin holding 0-based `rank`
+// (all threads call; result left in *out_bin / *out_rem by the owning thread).
+__device__ void find_bin(const uint32_t* h, int nb, uint32_t rank, uint32_t* sc, uint32_t* out_bin, uint32_t* out_rem) {
+  const int per = nb / kBlock;   // 8 or 4
+  const int t = threadIdx.x;
+  uint32_t local = 0;
+  for (int i = 0; i < per; ++i) local += h[t * per + i];
+  sc[t] = local;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 256 entries
+  for (int o = 1; o < kBlock; o <<= 1) {
+    uint32_t x = t >= o ? sc[t - o] : 0u;
+    __syncthreads();
+    sc[t] += x;
+    __syncthreads();
+  }
+  const uint32_t incl = sc[t];
+  const uint32_t excl = incl - local;
+  if (rank >= excl && rank < incl) {
+    uint32_t c = excl;
+    for (int i = 0; i < per; ++i) {
+      const uint32_t hv = h[t * per + i];
+      if (rank < c + hv) { *out_bin = (uint32_t)(t * per + i); *out_rem = rank - c; break; }
+      c += hv;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ void pct_targets(SelState& s) {
+  const uint32_t n = s.n;
+  int k = 0;
+  const double qs[2] = {2.0 / 100.0, 98.0 / 100.0};   // q = [2,98] / float32(100) -> float64
+  for (int j = 0; j < 2; ++j) {
+    const double v = (double)(n - 1) * qs[j];
+    uint32_t i0, i1;
+    if (v >= (double)(n - 1)) { i0 = i1 = n - 1; }
+    else { i0 = (uint32_t)floor(v); i1 = i0 + 1; }
+    s.rank[k++] = i0;
+    s.rank[k++] = i1;
+  }
+  s.ntgt = 4;
+  for (int i = 0; i < 4; ++i) s.prefix[i] = 0;
+}
+
+__device__ void finalize_pct(SelState& s) {
+  const uint32_t n = s.n;
+  const double qs[2] = {2.0 / 100.0, 98.0 / 100.0};
+  double r[2];
+  for (int j = 0; j < 2; ++j) {
+    const double v = (double)(n - 1) * qs[j];
+    const double t = v - floor(v);
+    const float a = key2f(s.prefix[2 * j]);
+    const float bb = key2f(s.prefix[2 * j + 1]);
+    const float diff = bb - a;
+    r[j] = t >= 0.5 ? (double)bb - (double)diff * (1.0 - t) : (double)a + (double)diff * t;
+  }
+  double p2 = r[0], p98 = r[1];
+  int branch = 0;
+  if (p98 <= p2) {                       // app.py:198-199
+    p2 = (double)key2f(s.kmin);
+    p98 = (double)key2f(s.kmax);
+    branch = 1;
+  }
+  if (p98 > p2) {
+    s.mode = branch;
+    s.den64 = (p98 - p2) + 1e-6;
+    s.lo32 = (float)p2;
+    s.hi32 = (float)p98;
+    s.den32 = (float)((p98 - p2) + 1e-6);
+  } else {
+    s.mode = 2;
+  }
+  s.p2 = p2;
+  s.p98 = p98;
+  s.phase = PH_DONE;
+}
+
+template <int LEVEL, int PASS>
+__global__ __launch_bounds__(kBlock) void k_sel_resolve(SelState* st, uint32_t* hist, int B) {
+  __shared__ uint32_t sc[kBlock];
+  __shared__ uint32_t res_bin[4], res_rem[4];
+  __shared__ SelState s;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  if (threadIdx.x == 0) s = st[b];
+  __syncthreads();
+  bool run;
+  if (PASS == 0) run = LEVEL == 0 ? s.phase == PH_INIT : (s.phase == PH_PCT || s.phase == PH_MED);
+  else run = LEVEL == 0 ? s.phase == PH_PCT2_INIT : s.phase == PH_PCT2;
+  if (!run) return;
+  __syncthreads();
+  if (threadIdx.x == 0 && LEVEL == 0) {
+    if (PASS == 0 && s.nonfinite_count != 0) {
+      const uint32_t m = s.n - s.nan_count;
+      if (m == 0) {                      // all-NaN: nanmedian is NaN, every value stays NaN
+        s.has_med = 1;
+        s.mode = 2;
+        s.p2 = s.p98 = (double)__uint_as_float(0x7fc00000u);
+        s.phase = PH_DONE;
+      } else {
+        const uint32_t h = m / 2;
+        if (m & 1u) { s.rank[0] = s.rank[1] = h; s.med_ranks = 1; }
+        else { s.rank[0] = h - 1; s.rank[1] = h; s.med_ranks = 2; }
+        s.ntgt = 2;
+        s.prefix[0] = s.prefix[1] = 0;
+        s.phase = PH_MED;
+      }
+    } else {
+      pct_targets(s);
+      s.phase = PASS == 0 ? PH_PCT : PH_PCT2;
+    }
+    for (int i = 0; i < 4; ++i) s.slot[i] = 0;
+    s.nslot = 1;
+  }
+  __syncthreads();
+  if (s.phase == PH_DONE) {
+    if (threadIdx.x == 0) st[b] = s;
+    return;
+  }
+  uint32_t* gh = hist + (size_t)b * kSlots * kBins;
+  const int nb = LEVEL == 2 ? 1024 : kBins;
+  for (int t = 0; t < (int)s.ntgt; ++t) {
+    if (threadIdx.x == 0) { res_bin[t] = 0; res_rem[t] = 0; }
+    __syncthreads();
+    find_bin(gh + s.slot[t] * kBins, nb, s.rank[t], sc, &res_bin[t], &res_rem[t]);
+  }
+  __syncthreads();
+  // consumed histograms -> zero for the next level
+  for (int i = threadIdx.x; i < (int)s.nslot * kBins; i += kBlock) gh[i] = 0;
+  if (threadIdx.x == 0) {
+    const int bits = LEVEL == 2 ? 10 : 11;
+    for (int t = 0; t < (int)s.ntgt; ++t) {
+      s.prefix[t] = (s.prefix[t] << bits) | res_bin[t];
+      s.rank[t] = res_rem[t];
+    }
+    // distinct prefixes -> histogram slots for the next level
+    s.nslot = 0;
+    for (int t = 0; t < (int)s.ntgt; ++t) {
+      int found = -1;
+      for (int q = 0; q < (int)s.nslot; ++q) if (s.slot_prefix[q] == s.prefix[t]) found = q;
+      if (found < 0) { found = (int)s.nslot; s.slot_prefix[s.nslot++] = s.prefix[t]; }
+      s.slot[t] = (uint32_t)found;
+    }
+    if (LEVEL == 2) {
+      if (s.phase == PH_MED) {
+        const float a = key2f(s.prefix[0]);
+        const float c = key2f(s.prefix[1]);
+        s.med = s.med_ranks == 1 ? a : (a + c) / 2.0f;  // np.mean of the middle pair in float32
+        s.has_med = 1;
+        s.phase = PH_PCT2_INIT;
+        if (isnan(s.med)) {  // e.g. median of {-inf, +inf}: the filled map has NaNs -> np.percentile is NaN
+          s.mode = 2;
+          s.p2 = s.p98 = (double)s.med;
+          s.phase = PH_DONE;
+        }
+        s.kmin = 0xffffffffu;
+        s.kmax = 0u;
+        s.nslot = 1;
+        s.slot_prefix[0] = 0;
+      } else {
+        finalize_pct(s);
+      }
+    }
+    st[b] = s;
+  }
+}
+
+struct Norm {
+  int mode, invert;
+  double p2, p98, den64;
+  float lo32, hi32, den32;
+};
+
+__device__ __forceinline__ Norm load_norm(const SelState* S, int invert) {
+  Norm nm;
+  nm.mode = S->mode;
+  nm.invert = invert;
+  nm.p2 = S->p2;
+  nm.p98 = S->p98;
+  nm.den64 = S->den64;
+  nm.lo32 = S->lo32;
+  nm.hi32 = S->hi32;
+  nm.den32 = S->den32;
+  return nm;
+}
+
+// app.py:200-206 in the dtype numpy uses for the branch taken.
+__device__ __forceinline__ double normalize(float val, const Norm& nm) {
+  if (nm.mode == 0) {
+    double d = (double)val;
+    d = d < nm.p2 ? nm.p2 : d;          // np.clip -> min(max(x, lo), hi)
+    d = d > nm.p98 ? nm.p98 : d;
+    d = (d - nm.p2) / nm.den64;
+    if (nm.invert) d = 1.0 - d;
+    return d;
+  }
+  if (nm.mode == 1) {
+    float f = val < nm.lo32 ? nm.lo32 : val;
+    f = f > nm.hi32 ? nm.hi32 : f;
+    f = (f - nm.lo32) / nm.den32;
+    if (nm.invert) f = 1.0f - f;
+    return (double)f;
+  }
+  return nm.invert ? 1.0 : 0.0;
+}
+
+struct Cam {
+  double cx, cy, f, scale;
+  int step, Wn, N;
+};
+
+__device__ __forceinline__ void project(double d, int v, int u, const Cam& c, float& x, float& y, float& z) {
+  const double zd = d * c.scale;                       // app.py:233
+  const double zz = zd != 0.0 ? zd : 1e-6;             // app.py:234-235
+  x = (float)((((double)u - c.cx) * zz) / c.f);
+  y = (float)((((double)v - c.cy) * zz) / c.f);
+  z = (float)zd;
+}
+
+template <bool kField>
+__global__ __launch_bounds__(kBlock) void k_unproject(Geo g, const SelState* st, const double* field,
+                                                      const uint8_t* img, int C, int B, int G, int invert,
+                                                      Cam cam, float* xyz, uint8_t* rgb, SelState* stw) {
+  __shared__ uint32_t red[6][4];
+  int b, chunk;
+  map_block(blockIdx.x, B, G, b, chunk);
+  const SelState* S = st + b;
+  const Norm nm = load_norm(S, invert);
+  const bool fill = S->has_med != 0;
+  const float med = S->med;
+  const int N = cam.N;
+  const int per = ((N + G - 1) / G + 3) & ~3;
+  const int start = chunk * per;
+  const int end = min(N, start + per);
+  const bool vec_ok = (N & 3) == 0;
+  const size_t img_base = (size_t)b * g.H * g.W;
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  bool any = false;
+  for (int i0 = start + 4 * threadIdx.x; i0 < end; i0 += 4 * kBlock) {
+    float px[4][3];
+    uint8_t pc[4][3];
+    int cnt = min(4, end - i0);
+    for (int j = 0; j < 4; ++j) {
+      if (j >= cnt) break;
+      const int i = i0 + j;
+      const int row = i / cam.Wn;
+      const int col = i - row * cam.Wn;
+      const int v = row * cam.step;
+      const int u = col * cam.step;
+      double d;
+      if (kField) {
+        d = field[img_base + (size_t)v * g.W + u];
+      } else {
+        float val = sample(g, b, v, u);
+        if (fill && !isfinite(val)) val = med;
+        d = normalize(val, nm);
+      }
+      project(d, v, u, cam, px[j][0], px[j][1], px[j][2]);
+      if (C >= 3) {
+        const uint8_t* p = img + ((img_base + (size_t)v * g.W + u) * C);
+        pc[j][0] = p[2];
+        pc[j][1] = p[1];
+        pc[j][2] = p[0];
+      } else {
+        pc[j][0] = pc[j][1] = pc[j][2] = 128;
+      }
+      for (int k = 0; k < 3; ++k) { mn[k] = fminf(mn[k], px[j][k]); mx[k] = fmaxf(mx[k], px[j][k]); }
+      any = true;
+    }
+    const size_t o = (size_t)b * N + i0;
+    if (vec_ok && cnt == 4) {
+      float4* dst = reinterpret_cast<float4*>(xyz + o * 3);
+      dst[0] = make_float4(px[0][0], px[0][1], px[0][2], px[1][0]);
+      dst[1] = make_float4(px[1][1], px[1][2], px[2][0], px[2][1]);
+      dst[2] = make_float4(px[2][2], px[3][0], px[3][1], px[3][2]);
+      uint32_t w0 = pc[0][0] | (pc[0][1] << 8) | (pc[0][2] << 16) | ((uint32_t)pc[1][0] << 24);
+      uint32_t w1 = pc[1][1] | (pc[1][2] << 8) | (pc[2][0] << 16) | ((uint32_t)pc[2][1] << 24);
+      uint32_t w2 = pc[2][2] | (pc[3][0] << 8) | (pc[3][1] << 16) | ((uint32_t)pc[3][2] << 24);
+      uint32_t* cd = reinterpret_cast<uint32_t*>(rgb + o * 3);
+      cd[0] = w0; cd[1] = w1; cd[2] = w2;
+    } else {
+      for (int j = 0; j < cnt; ++j) {
+        for (int k = 0; k < 3; ++k) {
+          xyz[(o + j) * 3 + k] = px[j][k];
+          rgb[(o + j) * 3 + k] = pc[j][k];
+        }
+      }
+    }
+  }
+  // per-image bbox: wave reduce -> LDS -> one atomic per block and component
+  uint32_t kk[6];
+  for (int k = 0; k < 3; ++k) {
+    kk[2 * k] = any ? f2key(mn[k]) : 0xffffffffu;
+    kk[2 * k + 1] = any ? f2key(mx[k]) : 0u;
+  }
+  const int wid = threadIdx.x >> 6;
+  for (int k = 0; k < 6; ++k) {
+    uint32_t x = (k & 1) ? wave_max_u32(kk[k]) : wave_min_u32(kk[k]);
+    if ((threadIdx.x & 63) == 0) red[k][wid] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int k = threadIdx.x;
+    uint32_t x = red[k][0];
+    for (int w = 1; w < kBlock / 64; ++w) x = (k & 1) ? max(x, red[k][w]) : min(x, red[k][w]);
+    uint32_t* dst = &stw[b].bbox_key[k];
+    if (k & 1) { if (x) atomicMax(dst, x); }
+    else { if (x != 0xffffffffu) atomicMin(dst, x); }
+  }
+}
+
+// Smooth path (app.py:209-214): materialise the normalised field, blur, unproject.
+__global__ void k_norm_field(Geo g, const SelState* st, int B, int invert, double* field) {
+  const size_t n = (size_t)g.H * g.W;
+  const size_t total = n * B;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / n);
+    const int p = (int)(i - (size_t)b * n);
+    const int v = p / g.W, u = p - v * g.W;
+    const SelState* S = st + b;
+    float val = sample(g, b, v, u);
+    if (S->has_med && !isfinite(val)) val = S->med;
+    field[i] = normalize(val, load_norm(S, invert));
+  }
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * (n - 1) - i;
+  return i < 0 ? -i : i;
+}
+
+// 5-tap [1,4,6,4,1]/16 (cv2 small-kernel table for ksize 5, sigma 0), BORDER_REFLECT_101,
+// accumulated tap by tap in the branch dtype (float64 for mode 0, float32 otherwise).
+template <bool kRows>
+__global__ void k_blur(const double* src, double* dst, const SelState* st, int B, int H, int W) {
+  const size_t n = (size_t)H * W;
+  const size_t total = n * B;
+  const double k64[5] = {0.0625, 0.25, 0.375, 0.25, 0.0625};
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / n);
+    const int p = (int)(i - (size_t)b * n);
+    const int v = p / W, u = p - v * W;
+    const double* s = src + (size_t)b * n;
+    if (st[b].mode == 0) {
+      double acc = 0.0;
+      for (int t = 0; t < 5; ++t) {
+        const double x = kRows ? s[(size_t)v * W + reflect101(u + t - 2, W)] : s[(size_t)reflect101(v + t - 2, H) * W + u];
+        acc = acc + x * k64[t];
+      }
+      dst[i] = acc;
+    } else {
+      float acc = 0.f;
+      for (int t = 0; t < 5; ++t) {
+        const float x = (float)(kRows ? s[(size_t)v * W + reflect101(u + t - 2, W)] : s[(size_t)reflect101(v + t - 2, H) * W + u]);
+        acc = acc + x * (float)k64[t];
+      }
+      dst[i] = (double)acc;
+    }
+  }
+}
+
+__global__ void k_finalize(const SelState* st, int B, double* bbox, double* stats) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const SelState& s = st[b];
+  if (bbox)
+    for (int k = 0; k < 6; ++k) bbox[b * 6 + k] = (double)key2f(s.bbox_key[k]);
+  if (stats) {
+    stats[b * 4 + 0] = s.p2;
+    stats[b * 4 + 1] = s.p98;
+    stats[b * 4 + 2] = (double)s.mode;
+    stats[b * 4 + 3] = s.has_med ? (double)s.med : (double)__uint_as_float(0x7fc00000u);
+  }
+}
+
+__global__ void k_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,
+                                float* oxyz, float* orgb) {
+  const int64_t cnt = (n + stride - 1) / stride;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = i * stride;
+    for (int k = 0; k < 3; ++k) {
+      oxyz[i * 3 + k] = xyz[s * 3 + k];
+      orgb[i * 3 + k] = (float)rgb[s * 3 + k];
+    }
+  }
+}
+
+template <int PASS>
+static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, int G, hipStream_t s) {
+  hipLaunchKernelGGL((k_sel_hist<0, PASS>), dim3(B * G), dim3(kBlock), 0, s, g, st, hist, B, G);
+  hipLaunchKernelGGL((k_sel_resolve<0, PASS>), dim3(B), dim3(kBlock), 0, s, st, hist, B);
+  hipLaunchKernelGGL((k_sel_hist<1, PASS>), dim3(B * G), dim3(kBlock), 0, s, g, st, hist, B, G);
+  hipLaunchKernelGGL((k_sel_resolve<1, PASS>), dim3(B), dim3(kBlock), 0, s, st, hist, B);
+  hipLaunchKernelGGL((k_sel_hist<2, PASS>), dim3(B * G), dim3(kBlock), 0, s, g, st, hist, B, G);
+  hipLaunchKernelGGL((k_sel_resolve<2, PASS>), dim3(B), dim3(kBlock), 0, s, st, hist, B);
+  return check_launch("select");
+}
+
+}  // namespace unproj
+}  // namespace i2pc
+
+using namespace i2pc;
+using namespace i2pc::unproj;
+
+extern "C" size_t i2pc_unproject_workspace_bytes(int batch, int img_h, int img_w, int smooth) {
+  if (batch <= 0 || img_h <= 0 || img_w <= 0) return 0;
+  return layout(batch, img_h, img_w, smooth).total;
+}
+
+extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const uint8_t* image, int channels,
+                              int batch, int img_h, int img_w, const i2pc_unproject_params* params,
+                              float* xyz, uint8_t* rgb, double* bbox, double* stats,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(params != nullptr, "params is NULL");
+  I2PC_REQUIRE(depth && image && xyz && rgb && workspace, "NULL device pointer");
+  I2PC_REQUIRE(batch > 0 && img_h > 0 && img_w > 0 && dep_h > 0 && dep_w > 0, "empty shape");
+  I2PC_REQUIRE(channels >= 1 && channels <= 4, "channels must be 1..4");
+  const int step = params->step;
+  I2PC_REQUIRE(step == 1 || step == 2 || step == 4, "step must be 1, 2 or 4 (low/medium/high)");
+  I2PC_REQUIRE((int64_t)img_h * img_w < (1ll << 31), "image too large");
+  if (params->smooth) {
+    const int k = params->smooth_ksize < 3 ? 3 : params->smooth_ksize / 2 * 2 + 1;
+    if (k != 5) return set_error(I2PC_EUNSUPPORTED, "smooth_ksize -> kernel %d: only the default 5 is implemented", k);
+  }
+  const Layout L = layout(batch, img_h, img_w, params->smooth);
+  if (workspace_bytes < L.total) return set_error(I2PC_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
+  hipStream_t s = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  SelState* st = reinterpret_cast<SelState*>(ws + L.state);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
+  Tap* xt = reinterpret_cast<Tap*>(ws + L.xtab);
+  Tap* yt = reinterpret_cast<Tap*>(ws + L.ytab);
+
+  if (hipMemsetAsync(hist, 0, sizeof(uint32_t) * kSlots * kBins * (size_t)batch, s) != hipSuccess)
+    return set_error(I2PC_ELAUNCH, "memset failed");
+  const int n = img_h * img_w;
+  const int init_threads = std::max(std::max(batch, img_h), img_w);
+  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, dep_h, dep_w, img_h, img_w);
+
+  Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0};
+  // blocks per image for the selection sweeps: ~8 pixels per thread, >= 1
+  int G = (n + kBlock * 8 - 1) / (kBlock * 8);
+  G = std::max(1, std::min(G, 512));
+  int rc = launch_select<0>(g, st, hist, batch, G, s);
+  if (rc) return rc;
+  rc = launch_select<1>(g, st, hist, batch, G, s);
+  if (rc) return rc;
+
+  Cam cam;
+  cam.cx = img_w / 2.0;
+  cam.cy = img_h / 2.0;
+  const double fov = params->fov_deg;
+  if (fov > 0) {  // app.py:220-221 (NaN compares false -> else branch)
+    cam.f = (img_w / 2.0) / std::tan((fov * (3.141592653589793 / 180.0)) / 2.0);
+  } else {
+    cam.f = (double)std::max(img_w, img_h) * 1.2;     // app.py:223
+  }
+  cam.scale = params->depth_scale;
+  cam.step = step;
+  cam.Wn = (img_w + step - 1) / step;
+  const int Hn = (img_h + step - 1) / step;
+  cam.N = cam.Wn * Hn;
+  int GU = (cam.N + kBlock * 4 * 4 - 1) / (kBlock * 4 * 4);
+  GU = std::max(1, std::min(GU, 1024));
+  const double* field = nullptr;
+  if (params->smooth) {
+    double* f0 = reinterpret_cast<double*>(ws + L.field);
+    double* f1 = reinterpret_cast<double*>(ws + L.tmp);
+    const int nb = 2048;
+    hipLaunchKernelGGL(k_norm_field, dim3(nb), dim3(256), 0, s, g, st, batch, params->invert, f0);
+    hipLaunchKernelGGL((k_blur<true>), dim3(nb), dim3(256), 0, s, f0, f1, st, batch, img_h, img_w);
+    hipLaunchKernelGGL((k_blur<false>), dim3(nb), dim3(256), 0, s, f1, f0, st, batch, img_h, img_w);
+    field = f0;
+    hipLaunchKernelGGL((k_unproject<true>), dim3(batch * GU), dim3(kBlock), 0, s, g, st, field, image, channels,
+                       batch, GU, params->invert, cam, xyz, rgb, st);
+  } else {
+    hipLaunchKernelGGL((k_unproject<false>), dim3(batch * GU), dim3(kBlock), 0, s, g, st, field, image, channels,
+                       batch, GU, params->invert, cam, xyz, rgb, st);
+  }
+  hipLaunchKernelGGL(k_finalize, dim3((batch + 63) / 64), dim3(64), 0, s, st, batch, bbox, stats);
+  return check_launch("unproject");
+}
+
+extern "C" int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,
+                                  float* out_xyz, float* out_rgb, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(xyz && rgb && out_xyz && out_rgb, "NULL device pointer");
+  I2PC_REQUIRE(n > 0 && stride > 0, "n and stride must be positive");
+  const int64_t cnt = (n + stride - 1) / stride;
+  const int blocks = (int)std::min<int64_t>((cnt + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_gather_stride, dim3(blocks), dim3(256), 0, as_stream(stream), xyz, rgb, n, stride, out_xyz, out_rgb);
+  return check_launch("gather_stride");
+}

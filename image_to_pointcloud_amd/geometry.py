@@ -1,0 +1,158 @@
+"""Depth -> point cloud on the GPU: the host-side mirror of the reference interface.
+
+`depth_to_point_cloud` keeps the signature, argument meaning, return types and
+error behaviour of backend/app.py:174-250 (numpy in, numpy out, raises on bad
+input); `generate_gis_bounds` mirrors app.py:393-400.  Both run the HIP
+kernels of libi2pc.so through the C ABI (include/i2pc.h); there is no CPU path.
+
+`unproject_batch` is the batched device API the pipeline uses: torch CUDA
+tensors in, torch CUDA tensors out, stream-ordered on the current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+
+logger = logging.getLogger(__name__)
+
+DENSITY_STEP = {"low": 4, "medium": 2, "high": 1}   # app.py:226
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def require_device():
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise _lib.I2PCError("image_to_pointcloud_amd needs a HIP device (MI355X); no CPU fallback exists")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream_handle():
+    return _torch().cuda.current_stream().cuda_stream
+
+
+_WS = {}
+
+
+def _workspace(nbytes: int, device):
+    torch = _torch()
+    key = (device.index if device.index is not None else torch.cuda.current_device())
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+@dataclass
+class PointBatch:
+    xyz: "object"     # torch.float32 [B, N, 3] on device
+    rgb: "object"     # torch.uint8   [B, N, 3] on device
+    bbox: "object"    # torch.float64 [B, 6]   minX maxX minY maxY minZ maxZ
+    stats: "object"   # torch.float64 [B, 4]   p2 p98 branch median
+
+
+def point_count(h: int, w: int, step: int) -> int:
+    return ((h + step - 1) // step) * ((w + step - 1) // step)
+
+
+def unproject_batch(depth, images, density: str = "medium", invert: bool = True,
+                    depth_scale: float = 10.0, smooth: bool = False, smooth_ksize: int = 5,
+                    fov: Optional[float] = None, out: Optional[PointBatch] = None) -> PointBatch:
+    """Batched GPU depth_to_point_cloud.
+
+    depth : torch.float32 [B, h, w] (model resolution) on the device
+    images: torch.uint8 [B, H, W, C] BGR on the device
+    """
+    torch = _torch()
+    if density not in DENSITY_STEP:
+        raise KeyError(density)            # the reference's dict lookup raises KeyError (app.py:226)
+    step = DENSITY_STEP[density]
+    if depth.dim() == 2:
+        depth = depth.unsqueeze(0)
+    if images.dim() == 3:
+        images = images.unsqueeze(0) if images.shape[-1] in (3, 4) else images.unsqueeze(-1).unsqueeze(0)
+    if images.dim() == 2:
+        images = images.unsqueeze(0).unsqueeze(-1)
+    B, H, W, C = images.shape
+    if depth.shape[0] != B:
+        raise ValueError(f"batch mismatch: depth {tuple(depth.shape)} vs images {tuple(images.shape)}")
+    if not depth.is_cuda or not images.is_cuda:
+        raise _lib.I2PCError("unproject_batch expects device tensors")
+    depth = depth.contiguous().to(torch.float32)
+    images = images.contiguous()
+    if images.dtype != torch.uint8:
+        raise TypeError("images must be uint8")
+    N = point_count(H, W, step)
+    dev = depth.device
+    if out is None:
+        out = PointBatch(
+            xyz=torch.empty((B, N, 3), dtype=torch.float32, device=dev),
+            rgb=torch.empty((B, N, 3), dtype=torch.uint8, device=dev),
+            bbox=torch.empty((B, 6), dtype=torch.float64, device=dev),
+            stats=torch.empty((B, 4), dtype=torch.float64, device=dev),
+        )
+    lib = _lib.load()
+    ws_bytes = lib.i2pc_unproject_workspace_bytes(B, H, W, int(bool(smooth)))
+    ws = _workspace(ws_bytes, dev)
+    p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
+                             fov_deg=float(fov) if fov else 0.0, smooth=int(bool(smooth)),
+                             smooth_ksize=int(smooth_ksize))
+    _lib.call("i2pc_unproject", _ptr(depth), depth.shape[1], depth.shape[2], _ptr(images), C, B, H, W,
+              ctypes.byref(p), _ptr(out.xyz), _ptr(out.rgb), _ptr(out.bbox), _ptr(out.stats),
+              _ptr(ws), ws.numel(), _stream_handle())
+    return out
+
+
+def depth_to_point_cloud(image: np.ndarray, depth: np.ndarray, density: str = "medium",
+                         invert: bool = True, depth_scale: float = 10.0, smooth: bool = False,
+                         smooth_ksize: int = 5, fov: Optional[float] = None) -> tuple:
+    """Drop-in for backend/app.py:174 -- same arguments, (points f32 Nx3, colors f32 Nx3)."""
+    torch = _torch()
+    try:
+        dev = require_device()
+        img = np.ascontiguousarray(image)
+        if img.ndim == 2:
+            img = img[:, :, None]
+        timg = torch.from_numpy(img).to(dev)
+        tdep = torch.from_numpy(np.ascontiguousarray(depth, dtype=np.float32)).to(dev)
+        pb = unproject_batch(tdep.unsqueeze(0), timg.unsqueeze(0), density=density, invert=invert,
+                             depth_scale=depth_scale, smooth=smooth, smooth_ksize=smooth_ksize, fov=fov)
+        pts = pb.xyz[0].cpu().numpy()
+        cols = pb.rgb[0].to(torch.float32).cpu().numpy()
+        return pts, cols
+    except Exception as e:
+        logger.error(f"Error in point cloud generation: {str(e)}")   # app.py:248-250
+        raise
+
+
+def generate_gis_bounds(bbox_row) -> dict:
+    """bounds dict of generate_gis_metadata (app.py:393-400) from a device bbox row."""
+    b = [float(x) for x in (bbox_row.tolist() if hasattr(bbox_row, "tolist") else bbox_row)]
+    return {"minX": b[0], "maxX": b[1], "minY": b[2], "maxY": b[3], "minZ": b[4], "maxZ": b[5]}
+
+
+def preview_subsample(xyz, rgb, max_preview: int = 20000):
+    """Preview stride subsample (app.py:496-506) on device; returns python lists."""
+    torch = _torch()
+    n = xyz.shape[0]
+    stride = max(1, n // max_preview) if n > max_preview else 1
+    cnt = (n + stride - 1) // stride
+    oxyz = torch.empty((cnt, 3), dtype=torch.float32, device=xyz.device)
+    orgb = torch.empty((cnt, 3), dtype=torch.float32, device=xyz.device)
+    _lib.call("i2pc_gather_stride", _ptr(xyz.contiguous()), _ptr(rgb.contiguous()), n, stride,
+              _ptr(oxyz), _ptr(orgb), _stream_handle())
+    return oxyz.cpu().double().tolist(), orgb.cpu().double().tolist()

@@ -106,9 +106,11 @@ def resize_linear_cv2(depth: np.ndarray, out_w: int, out_h: int) -> np.ndarray:
         return src.copy()
     x0, x1, ax0, ax1 = _linear_taps(in_w, out_w)
     y0, y1, by0, by1 = _linear_taps(in_h, out_h)
+    right = x0 >= in_w - 1          # HResizeLinear: dx >= xmax copies S[sx] (one tap)
     with np.errstate(invalid="ignore", over="ignore"):
         hor = src[:, x0] * ax0[None, :] + src[:, x1] * ax1[None, :]          # float32
-        out = hor[y0, :] * by0[:, None] + hor[y1, :] * by1[:, None]          # float32
+        hor[:, right] = src[:, x0[right]]
+        out = hor[y0, :] * by0[:, None] + hor[y1, :] * by1[:, None]          # float32, both taps
     return out.astype(np.float32)
 
 

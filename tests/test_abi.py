@@ -1,0 +1,41 @@
+"""CPU-side checks of the C ABI: the library builds/loads and exports every declared symbol."""
+import ctypes
+import os
+
+import pytest
+
+from image_to_pointcloud_amd import _lib
+
+
+def test_header_declares_core_entry_points():
+    syms = _lib.declared_symbols()
+    for s in ("i2pc_unproject", "i2pc_unproject_workspace_bytes", "i2pc_last_error", "i2pc_abi_version"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libi2pc.so not built (run python -m image_to_pointcloud_amd.build)")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in _lib.declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_no_gpu_calls_needed_for_metadata():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libi2pc.so not built")
+    lib = _lib.load()
+    assert lib.i2pc_abi_version() >= 1
+    assert lib.i2pc_unproject_workspace_bytes(32, 1024, 1024, 0) > 0
+    assert lib.i2pc_unproject_workspace_bytes(0, 1024, 1024, 0) == 0
+    assert lib.i2pc_last_error() is not None
+
+
+def test_missing_device_fails_loudly():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from image_to_pointcloud_amd import geometry
+    import numpy as np
+    with pytest.raises(_lib.I2PCError):
+        geometry.depth_to_point_cloud(np.zeros((4, 4, 3), np.uint8), np.zeros((4, 4), np.float32))

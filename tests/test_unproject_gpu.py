@@ -1,0 +1,166 @@
+"""GPU parity of the HIP unprojection against the reference fixtures and the oracle.
+
+Bar: bit-exact xyz (float32), colours, bounds and percentile stats -- the
+kernels evaluate the reference's arithmetic in the same IEEE order.
+"""
+import numpy as np
+import pytest
+
+from oracle import unproject_ref as ref
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _geom():
+    from image_to_pointcloud_amd import geometry
+    return geometry
+
+
+def _same_bits(a, b):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
+
+
+def _first_diff(a, b):
+    idx = np.argwhere(a != b)
+    if len(idx) == 0:
+        return "shape/dtype"
+    i = tuple(idx[0])
+    return f"first diff at {i}: got {a[i]!r} expected {b[i]!r} ({len(idx)} diffs)"
+
+
+def test_golden_cases_bit_exact(unproject_cases):
+    g = _geom()
+    for c in unproject_cases:
+        pts, cols = g.depth_to_point_cloud(c["image"], c["depth"], density=c["density"],
+                                           invert=c["invert"], depth_scale=c["scale"])
+        assert _same_bits(pts, c["points"]), (c["name"], _first_diff(pts, c["points"]))
+        assert _same_bits(cols, c["colors"]), c["name"]
+
+
+def test_golden_bounds_from_device_bbox(unproject_cases):
+    g = _geom()
+    for c in unproject_cases:
+        dev = torch.device("cuda")
+        pb = g.unproject_batch(torch.from_numpy(c["depth"]).to(dev)[None], torch.from_numpy(c["image"]).to(dev)[None],
+                               density=c["density"], invert=c["invert"], depth_scale=c["scale"])
+        got = pb.bbox[0].cpu().numpy()
+        assert _same_bits(got, c["bounds"]), (c["name"], got, c["bounds"])
+
+
+def _smooth_depth(h, w, seed, noise=0.05):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    base = 0.5 + 4.5 * (0.5 + 0.5 * np.sin(6 * np.pi * u / w) * np.cos(4 * np.pi * v / h))
+    return np.maximum(base + rng.normal(0.0, noise, size=(h, w)), 0.0).astype(np.float32)
+
+
+def _rgb(h, w, seed):
+    return np.random.Generator(np.random.PCG64(seed)).integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("shape", [(384, 384, 1024, 1024), (37, 53, 100, 90), (518, 686, 768, 1024), (96, 96, 95, 97)])
+@pytest.mark.parametrize("density", ["high", "medium", "low"])
+def test_resized_depth_matches_oracle(shape, density):
+    h, w, H, W = shape
+    g = _geom()
+    dep = _smooth_depth(h, w, 21)
+    img = _rgb(H, W, 22)
+    pts, cols = g.depth_to_point_cloud(img, dep, density=density)
+    ep, ec = ref.depth_to_point_cloud(img, dep, density=density, loop=False)
+    assert _same_bits(pts, ep), _first_diff(pts, ep)
+    assert _same_bits(cols, ec)
+
+
+def test_batched_mixed_branches_match_per_image_oracle():
+    g = _geom()
+    B, h, w, H, W = 8, 48, 40, 96, 80
+    deps = np.stack([_smooth_depth(h, w, 100 + i) for i in range(B)])
+    deps[1] = 3.0                                  # constant branch
+    deps[2] = 1.0; deps[2, 0, :5] = 4.0            # min/max float32 branch
+    deps[3, 5, 5] = np.nan; deps[3, 7, 9] = np.inf  # nanmedian fill
+    deps[4, :, :] = np.nan                          # all-NaN
+    imgs = np.stack([_rgb(H, W, 200 + i) for i in range(B)])
+    dev = torch.device("cuda")
+    for density in ("high", "medium"):
+        for invert in (True, False):
+            pb = g.unproject_batch(torch.from_numpy(deps).to(dev), torch.from_numpy(imgs).to(dev),
+                                   density=density, invert=invert, depth_scale=12.5)
+            xyz = pb.xyz.cpu().numpy()
+            rgb = pb.rgb.cpu().numpy()
+            for i in range(B):
+                with np.errstate(all="ignore"):
+                    ep, ec = ref.depth_to_point_cloud(imgs[i], deps[i], density=density, invert=invert,
+                                                      depth_scale=12.5, loop=False)
+                assert _same_bits(xyz[i], ep), (i, density, invert, _first_diff(xyz[i], ep))
+                assert _same_bits(rgb[i].astype(np.float32), ec)
+
+
+def test_percentile_stats_match_numpy():
+    g = _geom()
+    dev = torch.device("cuda")
+    for (h, w) in ((1024, 1024), (384, 384), (1, 1), (1, 7), (3, 2)):
+        d = _smooth_depth(h, w, 31) if h * w > 10 else np.random.default_rng(0).random((h, w), dtype=np.float32)
+        img = _rgb(h, w, 32)
+        pb = g.unproject_batch(torch.from_numpy(d).to(dev)[None], torch.from_numpy(img).to(dev)[None], density="high")
+        st = pb.stats[0].cpu().numpy()
+        p2, p98 = ref.percentile_2_98(d)
+        if p98 > p2:
+            assert st[0] == p2 and st[1] == p98, ((h, w), st, p2, p98)
+
+
+def test_full_size_high_density_properties():
+    """1024^2 x batch 4 from 384^2 depth: bit-exact vs oracle on image 0, shape/size invariants on all."""
+    g = _geom()
+    dev = torch.device("cuda")
+    B = 4
+    deps = np.stack([_smooth_depth(384, 384, 40 + i) for i in range(B)])
+    imgs = np.stack([_rgb(1024, 1024, 50 + i) for i in range(B)])
+    pb = g.unproject_batch(torch.from_numpy(deps).to(dev), torch.from_numpy(imgs).to(dev), density="high")
+    xyz = pb.xyz.cpu().numpy()
+    assert xyz.shape == (B, 1024 * 1024, 3)
+    ep, ec = ref.depth_to_point_cloud(imgs[0], deps[0], density="high", loop=False)
+    assert _same_bits(xyz[0], ep)
+    assert _same_bits(pb.rgb[0].cpu().numpy().astype(np.float32), ec)
+    bb = pb.bbox.cpu().numpy()
+    for i in range(B):
+        x = xyz[i]
+        exp = np.array([x[:, 0].min(), x[:, 0].max(), x[:, 1].min(), x[:, 1].max(), x[:, 2].min(), x[:, 2].max()],
+                       dtype=np.float64)
+        assert _same_bits(bb[i], exp)
+        # invert=True, scale 10: z in [0, 10] and the p98-clipped pixels give z = 10*1e-6/(R+1e-6)
+        assert x[:, 2].min() >= 0.0 and x[:, 2].max() <= 10.0
+
+
+def test_smooth_path_matches_oracle_blur():
+    g = _geom()
+    dep = _smooth_depth(60, 50, 61)
+    img = _rgb(60, 50, 62)
+    pts, _ = g.depth_to_point_cloud(img, dep, density="medium", smooth=True)
+    ep, _ = ref.depth_to_point_cloud(img, dep, density="medium", smooth=True, loop=False)
+    assert _same_bits(pts, ep), _first_diff(pts, ep)
+
+
+def test_preview_subsample_matches_reference(pipeline_case):
+    import hashlib
+    g = _geom()
+    s = pipeline_case["summary"]
+    dev = torch.device("cuda")
+    pb = g.unproject_batch(torch.from_numpy(pipeline_case["depth"]).to(dev)[None],
+                           torch.from_numpy(pipeline_case["image"]).to(dev)[None], density="high")
+    pp, pc = g.preview_subsample(pb.xyz[0], pb.rgb[0])
+    assert len(pp) == s["preview_len"]
+    assert hashlib.sha256(np.asarray(pp, np.float64).tobytes()).hexdigest() == s["preview_points_sha256"]
+    assert hashlib.sha256(np.asarray(pc, np.float64).tobytes()).hexdigest() == s["preview_colors_sha256"]
+    assert g.generate_gis_bounds(pb.bbox[0].cpu()) == s["gisData"]["bounds"]
+
+
+def test_bad_arguments_raise():
+    g = _geom()
+    from image_to_pointcloud_amd._lib import I2PCError
+    with pytest.raises(KeyError):
+        g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), density="ultra")
+    with pytest.raises(I2PCError):
+        g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), smooth=True, smooth_ksize=9)
