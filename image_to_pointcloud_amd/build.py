@@ -26,6 +26,9 @@ ARCH = os.environ.get("I2PC_ARCH", "gfx950")
 SOURCES = [
     "abi.cpp",
     "unproject.hip",
+    "gemm.hip",
+    "misc.hip",
+    "attention.hip",
 ]
 HEADERS = ["common.h", "../../include/i2pc.h"]
 

@@ -1,0 +1,226 @@
+// Fused multi-head self-attention, head_dim 64, bf16 in/out, fp32 softmax (gfx950).
+//
+// Replaces the SDPA / eager attention of DPTSelfAttention
+// (transformers modeling_dpt.py:123-154, eager_attention_forward :73-98):
+//   O = softmax(Q K^T * scale) V, no mask, dropout off (inference).
+//
+// One workgroup = 4 waves = 128 query rows of one (image, head); each wave owns
+// 32 query rows.  K/V tiles of 64 keys are double-buffered in LDS (K by
+// global_load_lds with an XOR-swizzled image, V transposed through registers
+// into a [d][key] image for the P.V operand).  "Swapped" products with
+// v_mfma_f32_32x32x16_bf16 keep each query on one lane:
+//   S^T[key][q] = K . Q^T      (A = K rows from LDS, B = Q fragments in VGPRs)
+//   O^T[d][q]  += V^T . P^T    (A = V^T rows from LDS, B = P straight from the
+//                               S accumulators, converted to bf16 in place)
+// so the online-softmax max/sum are lane-local plus one cross-half exchange.
+#include "common.h"
+
+#include <algorithm>
+
+namespace i2pc {
+namespace attn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint16_t bf16_t;
+
+constexpr int kQ = 128;   // query rows per workgroup
+constexpr int kKV = 64;   // keys per tile
+constexpr int kTileBytes = kKV * 64 * 2;   // 8 KiB (K tile and V^T tile each)
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_base), 16, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+  __bf16 x = (__bf16)a, y = (__bf16)b;
+  return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
+}
+
+// V^T image: row d (128 B = 64 keys), 8-byte units of 4 keys swizzled by (d >> 1) & 15.
+__device__ __forceinline__ int vt_off(int d, int key) {
+  const int unit = (key >> 2) ^ ((d >> 1) & 15);
+  return d * 128 + unit * 8 + (key & 3) * 2;
+}
+
+__global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__ qkv, int B, int T, int NH, float scale_log2,
+                                                      bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * kTileBytes];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int qtiles = (T + kQ - 1) / kQ;
+  int bid = blockIdx.x;
+  const int qt = bid % qtiles;
+  bid /= qtiles;
+  const int h = bid % NH;
+  const int b = bid / NH;
+  const int D = NH * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const bf16_t* Qg = qkv + (int64_t)b * T * ld + h * 64;
+  const bf16_t* Kg = Qg + D;
+  const bf16_t* Vg = Qg + 2 * D;
+
+  const int hh = lane >> 5;     // lane half
+  const int lq = lane & 31;
+  const int q = qt * kQ + wid * 32 + lq;
+  const int qc = min(q, T - 1);
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qg + qc * ld + 16 * s + 8 * hh);
+
+  // K glds: 8 wave-instructions per tile (8 keys x 128 B each), 2 per wave
+  auto stage_k = [&](int buf, int kt) {
+    uint8_t* sK = smem + buf * 2 * kTileBytes;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (wid * 2 + j) * 8 + (lane >> 3);
+      const int pchunk = lane & 7;
+      const int lchunk = pchunk ^ (row & 7);
+      const int key = min(kt * kKV + row, T - 1);
+      glds16(Kg + key * ld + lchunk * 8, sK + (wid * 2 + j) * 8 * 128);
+    }
+  };
+  // V: each thread loads 2 x 16 B (8 d of one key), later scattered transposed
+  uint4 vreg[2];
+  auto load_v = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int piece = threadIdx.x + j * 256;
+      const int key = piece >> 3, ch = piece & 7;
+      const int gk = min(kt * kKV + key, T - 1);
+      vreg[j] = *reinterpret_cast<const uint4*>(Vg + gk * ld + ch * 8);
+    }
+  };
+  auto write_vt = [&](int buf) {
+    uint8_t* sV = smem + buf * 2 * kTileBytes + kTileBytes;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int piece = threadIdx.x + j * 256;
+      const int key = piece >> 3, d0 = (piece & 7) * 8;
+      const uint16_t* e = reinterpret_cast<const uint16_t*>(&vreg[j]);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) *reinterpret_cast<uint16_t*>(sV + vt_off(d0 + t, key)) = e[t];
+    }
+  };
+
+  f32x16 o[2];
+  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int nt = (T + kKV - 1) / kKV;
+  stage_k(0, 0);
+  load_v(0);
+  write_vt(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) {
+      stage_k(cur ^ 1, kt + 1);
+      load_v(kt + 1);
+    }
+    const uint8_t* sK = smem + cur * 2 * kTileBytes;
+    const uint8_t* sV = sK + kTileBytes;
+    // S^T = K Q^T for two 32-key halves
+    f32x16 st[2];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      for (int i = 0; i < 16; ++i) st[k2][i] = 0.f;
+      const int key = 32 * k2 + lq;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int lchunk = 2 * s + hh;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ (key & 7)) << 4));
+        st[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[k2], 0, 0, 0);
+      }
+    }
+    // mask keys beyond T, scale into log2 domain, row max
+    const int kbase = kt * kKV;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + 32 * k2 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        float v = st[k2][r] * scale_log2;
+        if (key >= T) v = -INFINITY;
+        st[k2][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+    uint32_t pk[2][8];
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float p0 = exp2f(st[k2][r] - m_new);
+        const float p1 = exp2f(st[k2][r + 1] - m_new);
+        ls += p0 + p1;
+        pk[k2][r >> 1] = pack_bf16(p0, p1);
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+    // O^T += V^T P^T : 4 key steps of 16 keys
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pf;
+        {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          u32x4 u = {pk[k2][4 * s + 0], pk[k2][4 * s + 1], pk[k2][4 * s + 2], pk[k2][4 * s + 3]};
+          pf = __builtin_bit_cast(bf16x8, u);
+        }
+        const int kb = 32 * k2 + 16 * s + 4 * hh;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int d = 32 * dt + lq;
+          const uint2 lo = *reinterpret_cast<const uint2*>(sV + vt_off(d, kb));
+          const uint2 hi = *reinterpret_cast<const uint2*>(sV + vt_off(d, kb + 8));
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          u32x4 u = {lo.x, lo.y, hi.x, hi.y};
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, u);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+        }
+      }
+    if (kt + 1 < nt) write_vt(cur ^ 1);
+    __syncthreads();
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  const float inv = 1.0f / l_tot;
+  if (q < T) {
+    bf16_t* orow = out + ((int64_t)b * T + q) * D + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * hh;
+        uint2 w;
+        w.x = pack_bf16(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        w.y = pack_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d) = w;
+      }
+  }
+}
+
+}  // namespace attn
+}  // namespace i2pc
+
+using namespace i2pc;
+
+extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scale, void* out, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(qkv && out, "NULL pointer");
+  I2PC_REQUIRE(batch > 0 && tokens > 0 && heads > 0, "attention: empty shape");
+  const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn::k_attention, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+  return check_launch("attention");
+}

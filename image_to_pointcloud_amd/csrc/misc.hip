@@ -1,0 +1,214 @@
+// Memory-bound helpers of the depth network (gfx950): LayerNorm, bilinear 2x
+// upsample (align_corners=True), ViT stem CLS/pos row, fp32->bf16, head output.
+// All are HBM-bound: 16-byte vector loads/stores, one wave per row where a row
+// reduction is needed.
+#include "common.h"
+
+#include <algorithm>
+
+namespace i2pc {
+namespace misc {
+
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float x) {
+  __bf16 b = (__bf16)x;
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+__device__ __forceinline__ float wave_sum(float x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+// one wave per row, D/256 float4 per lane held in registers (two-pass variance)
+template <int V>
+__global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, int64_t ldx,
+                                                   const float* __restrict__ g, const float* __restrict__ b,
+                                                   float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
+  float4 v[V];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    v[i] = xr[i * 64 + lane];
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mean = wave_sum(s) / (float)dim;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const float a = v[i].x - mean, c = v[i].y - mean, d = v[i].z - mean, e = v[i].w - mean;
+    q += (a * a + c * c) + (d * d + e * e);
+  }
+  const float var = wave_sum(q) / (float)dim;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+  uint2* yr = reinterpret_cast<uint2*>(y + row * ldy);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const float4 gg = g4[i * 64 + lane], bb = b4[i * 64 + lane];
+    uint2 o;
+    o.x = pack2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+    o.y = pack2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+    yr[i * 64 + lane] = o;
+  }
+}
+
+// NHWC bf16, 8 channels (16 B) per thread; torch upsample_bilinear2d, align_corners=True.
+__global__ __launch_bounds__(256) void k_upsample2x(const bf16_t* __restrict__ x, int B, int h, int w, int c,
+                                                    const bf16_t* __restrict__ add, bf16_t* __restrict__ y) {
+  const int H = 2 * h, W = 2 * w;
+  const int cv = c / 8;
+  const int64_t total = (int64_t)B * H * W * cv;
+  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cv);
+    int64_t pix = i / cv;
+    const int ox = (int)(pix % W);
+    pix /= W;
+    const int oy = (int)(pix % H);
+    const int b = (int)(pix / H);
+    const float fy = sh * oy, fx = sw * ox;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly1 = fy - y0, lx1 = fx - x0;
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
+    const uint4 a00 = *reinterpret_cast<const uint4*>(base + ((int64_t)y0 * w + x0) * c);
+    const uint4 a01 = *reinterpret_cast<const uint4*>(base + ((int64_t)y0 * w + x1) * c);
+    const uint4 a10 = *reinterpret_cast<const uint4*>(base + ((int64_t)y1 * w + x0) * c);
+    const uint4 a11 = *reinterpret_cast<const uint4*>(base + ((int64_t)y1 * w + x1) * c);
+    const uint32_t* p00 = reinterpret_cast<const uint32_t*>(&a00);
+    const uint32_t* p01 = reinterpret_cast<const uint32_t*>(&a01);
+    const uint32_t* p10 = reinterpret_cast<const uint32_t*>(&a10);
+    const uint32_t* p11 = reinterpret_cast<const uint32_t*>(&a11);
+    uint4 addv = make_uint4(0, 0, 0, 0);
+    if (add) addv = *reinterpret_cast<const uint4*>(add + i * 8);
+    const uint32_t* pa = reinterpret_cast<const uint32_t*>(&addv);
+    uint4 out;
+    uint32_t* po = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float r[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        auto g = [&](uint32_t u) { return hh ? __uint_as_float(u & 0xffff0000u) : __uint_as_float(u << 16); };
+        const float t0 = lx0 * g(p00[k]) + lx1 * g(p01[k]);
+        const float t1 = lx0 * g(p10[k]) + lx1 * g(p11[k]);
+        r[hh] = ly0 * t0 + ly1 * t1;
+        if (add) r[hh] += g(pa[k]);
+      }
+      po[k] = pack2(r[0], r[1]);
+    }
+    *reinterpret_cast<uint4*>(y + i * 8) = out;
+  }
+}
+
+__global__ void k_cls_pos(const float* cls, const float* pos0, int B, int T, int D, float* x) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * D) return;
+  const int b = i / D, d = i - b * D;
+  x[(int64_t)b * T * D + d] = cls[d] + pos0[d];
+}
+
+__global__ void k_f32_to_bf16(const float4* __restrict__ x, int64_t n4, uint2* __restrict__ y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x[i];
+    y[i] = make_uint2(pack2(v.x, v.y), pack2(v.z, v.w));
+  }
+}
+
+// one thread per pixel: C (<= 64, multiple of 8) bf16 channels -> 1 fp32
+__global__ __launch_bounds__(256) void k_head_out(const bf16_t* __restrict__ x, int64_t P, int C,
+                                                  const float* __restrict__ w, float bias, float* __restrict__ d) {
+  __shared__ float sw[64];
+  if (threadIdx.x < C) sw[threadIdx.x] = w[threadIdx.x];
+  __syncthreads();
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint4* src = reinterpret_cast<const uint4*>(x + p * C);
+    float acc = 0.f;
+    for (int k = 0; k < C / 8; ++k) {
+      const uint4 u = src[k];
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(&u);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc += __uint_as_float(q[t] << 16) * sw[k * 8 + 2 * t];
+        acc += __uint_as_float(q[t] & 0xffff0000u) * sw[k * 8 + 2 * t + 1];
+      }
+    }
+    d[p] = fmaxf(acc + bias, 0.f);
+  }
+}
+
+static int grid_for(int64_t work, int per_block = 256) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((work + per_block - 1) / per_block, 256 * 16));
+}
+
+}  // namespace misc
+}  // namespace i2pc
+
+using namespace i2pc;
+using namespace i2pc::misc;
+
+extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
+                              int rows, int dim, void* y, int64_t ldy, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(x && gamma && beta && y, "NULL pointer");
+  I2PC_REQUIRE(rows > 0 && dim > 0 && dim % 256 == 0 && dim <= 2048, "layernorm: dim=%d must be a multiple of 256 <= 2048", dim);
+  I2PC_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "layernorm: row strides must be multiples of 4");
+  hipStream_t s = as_stream(stream);
+  const dim3 grid((rows + 3) / 4), block(256);
+  bf16_t* yy = static_cast<bf16_t*>(y);
+  switch (dim / 256) {
+    case 1: hipLaunchKernelGGL(k_layernorm<1>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 2: hipLaunchKernelGGL(k_layernorm<2>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 3: hipLaunchKernelGGL(k_layernorm<3>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 4: hipLaunchKernelGGL(k_layernorm<4>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 5: hipLaunchKernelGGL(k_layernorm<5>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 6: hipLaunchKernelGGL(k_layernorm<6>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 7: hipLaunchKernelGGL(k_layernorm<7>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 8: hipLaunchKernelGGL(k_layernorm<8>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+  }
+  return check_launch("layernorm");
+}
+
+extern "C" int i2pc_upsample2x(const void* x, int batch, int h, int w, int c, const void* add, void* y, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(x && y, "NULL pointer");
+  I2PC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0, "upsample2x: bad shape (c %% 8 == 0)");
+  const int64_t work = (int64_t)batch * 4 * h * w * (c / 8);
+  hipLaunchKernelGGL(k_upsample2x, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                     static_cast<const bf16_t*>(x), batch, h, w, c, static_cast<const bf16_t*>(add), static_cast<bf16_t*>(y));
+  return check_launch("upsample2x");
+}
+
+extern "C" int i2pc_cls_pos(const float* cls, const float* pos0, int batch, int tokens, int dim, float* x, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(cls && pos0 && x && batch > 0 && tokens > 0 && dim > 0, "cls_pos: bad args");
+  hipLaunchKernelGGL(k_cls_pos, dim3((batch * dim + 255) / 256), dim3(256), 0, as_stream(stream), cls, pos0, batch, tokens, dim, x);
+  return check_launch("cls_pos");
+}
+
+extern "C" int i2pc_f32_to_bf16(const float* x, int64_t n, void* y, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(x && y && n > 0 && n % 4 == 0, "f32_to_bf16: n must be a positive multiple of 4");
+  hipLaunchKernelGGL(k_f32_to_bf16, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(x), n / 4, static_cast<uint2*>(y));
+  return check_launch("f32_to_bf16");
+}
+
+extern "C" int i2pc_head_out(const void* x, int64_t pixels, int c, const float* w, float bias, float* depth, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(x && w && depth && pixels > 0 && c > 0 && c <= 64 && c % 8 == 0, "head_out: bad args");
+  hipLaunchKernelGGL(k_head_out, dim3(grid_for(pixels)), dim3(256), 0, as_stream(stream),
+                     static_cast<const bf16_t*>(x), pixels, c, w, bias, depth);
+  return check_launch("head_out");
+}

@@ -1,0 +1,213 @@
+"""Torch-tensor wrappers over the network entry points of the C ABI (include/i2pc.h).
+
+Every function launches a hand-written gfx950 kernel from libi2pc.so on the
+current stream; nothing here computes on the host, and nothing falls back to
+PyTorch arithmetic.  Tensors must already live on the device.
+Layouts: activations bf16 NHWC / [rows][features]; residual stream fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+from . import _lib
+
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_void_p = ctypes.c_void_p
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("a", c_void_p), ("lda", c_int64), ("m", c_int32), ("n", c_int32), ("k", c_int32),
+        ("a_group", c_int32), ("a_group_stride", c_int32), ("a_offset", c_int32),
+        ("conv", c_int32), ("conv_batch", c_int32), ("conv_h", c_int32), ("conv_w", c_int32),
+        ("conv_c", c_int32), ("conv_oh", c_int32), ("conv_ow", c_int32), ("conv_k", c_int32),
+        ("conv_stride", c_int32), ("conv_pad", c_int32), ("conv_relu_in", c_int32),
+        ("w", c_void_p), ("ldw", c_int64),
+        ("bias", c_void_p),
+        ("row_bias", c_void_p), ("row_bias_group", c_int32),
+        ("table", c_void_p), ("table_rows", c_int32),
+        ("act", c_int32),
+        ("res", c_void_p), ("res_f32", c_int32), ("ldr", c_int64),
+        ("res2", c_void_p), ("ldr2", c_int64),
+        ("c", c_void_p), ("c_f32", c_int32), ("ldc", c_int64),
+        ("out_group", c_int32), ("out_group_stride", c_int32), ("out_offset", c_int32),
+        ("convt_s", c_int32), ("convt_h", c_int32), ("convt_w", c_int32), ("convt_c", c_int32),
+    ]
+
+
+_lib.register("i2pc_gemm", ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p])
+_lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
+                                               ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p])
+_lib.register("i2pc_attention", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_float, c_void_p, c_void_p])
+_lib.register("i2pc_upsample2x", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, c_void_p, c_void_p, c_void_p])
+_lib.register("i2pc_cls_pos", ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             c_void_p, c_void_p])
+_lib.register("i2pc_f32_to_bf16", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p])
+_lib.register("i2pc_head_out", ctypes.c_int, [c_void_p, c_int64, ctypes.c_int, c_void_p, ctypes.c_float,
+                                              c_void_p, c_void_p])
+
+ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _stream():
+    return _torch().cuda.current_stream().cuda_stream
+
+
+def _check(t, dtype, name):
+    torch = _torch()
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise _lib.I2PCError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+def gemm(desc: GemmDesc) -> None:
+    _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
+
+
+def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=False,
+           a_map=(0, 0, 0), out_map=(0, 0, 0), rows=None, row_bias=None, row_bias_group=1,
+           table=None, table_rows=1, ldc=None):
+    """out = act(x @ w.T + bias + row_bias + table) + res + res2.
+
+    x: bf16 [*, K] (row stride x.stride(0)); w: bf16 [N, K]; rows = M (defaults to x rows).
+    a_map / out_map = (group, group_stride, offset) row remaps (see i2pc.h).
+    """
+    torch = _torch()
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.bfloat16, "w")
+    M = rows if rows is not None else x.shape[0]
+    N, K = w.shape
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
+    d = GemmDesc()
+    d.a, d.lda, d.m, d.n, d.k = _p(x), x.stride(0), M, N, K
+    d.a_group, d.a_group_stride, d.a_offset = a_map
+    d.w, d.ldw = _p(w), w.stride(0)
+    d.bias = _p(bias)
+    d.row_bias, d.row_bias_group = _p(row_bias), row_bias_group
+    d.table, d.table_rows = _p(table), table_rows
+    d.act = ACT[act]
+    if res is not None:
+        d.res, d.res_f32, d.ldr = _p(res), int(res.dtype == torch.float32), res.stride(0)
+    if res2 is not None:
+        d.res2, d.ldr2 = _p(res2), res2.stride(0)
+    d.c, d.c_f32 = _p(out), int(out.dtype == torch.float32)
+    d.ldc = ldc if ldc is not None else out.stride(0)
+    d.out_group, d.out_group_stride, d.out_offset = out_map
+    gemm(d)
+    return out
+
+
+def conv2d(x, w, bias=None, k=3, stride=1, pad=1, relu_in=False, act=None, res=None, res2=None, out=None):
+    """NHWC bf16 conv via implicit GEMM.  w: bf16 [Co, k*k*Ci] in (ky, kx, ci) order."""
+    torch = _torch()
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    Co = w.shape[0]
+    OH = (H + 2 * pad - k) // stride + 1
+    OW = (W + 2 * pad - k) // stride + 1
+    if out is None:
+        out = torch.empty((B, OH, OW, Co), dtype=torch.bfloat16, device=x.device)
+    d = GemmDesc()
+    d.a, d.lda, d.m, d.n, d.k = _p(x), C, B * OH * OW, Co, k * k * C
+    if k == 1 and stride == 1 and pad == 0:
+        pass    # a 1x1 conv is a plain GEMM over pixels
+    else:
+        d.conv, d.conv_batch, d.conv_h, d.conv_w, d.conv_c = 1, B, H, W, C
+        d.conv_oh, d.conv_ow, d.conv_k, d.conv_stride, d.conv_pad = OH, OW, k, stride, pad
+    d.conv_relu_in = int(relu_in)
+    d.w, d.ldw = _p(w), w.stride(0)
+    d.bias = _p(bias)
+    d.act = ACT[act]
+    if res is not None:
+        d.res, d.res_f32, d.ldr = _p(res), int(res.dtype == torch.float32), Co
+    if res2 is not None:
+        d.res2, d.ldr2 = _p(res2), Co
+    d.c, d.c_f32, d.ldc = _p(out), int(out.dtype == torch.float32), Co
+    gemm(d)
+    return out
+
+
+def conv_transpose(x, w, bias_tiled, s, out=None):
+    """ConvTranspose2d(kernel = stride = s) on NHWC bf16.  w: bf16 [s*s*Co, Ci] ((dy,dx,co) rows)."""
+    torch = _torch()
+    B, H, W, C = x.shape
+    Co = w.shape[0] // (s * s)
+    if out is None:
+        out = torch.empty((B, H * s, W * s, Co), dtype=torch.bfloat16, device=x.device)
+    d = GemmDesc()
+    d.a, d.lda, d.m, d.n, d.k = _p(x), C, B * H * W, w.shape[0], C
+    d.w, d.ldw = _p(w), w.stride(0)
+    d.bias = _p(bias_tiled)
+    d.c, d.c_f32, d.ldc = _p(out), 0, Co
+    d.convt_s, d.convt_h, d.convt_w, d.convt_c = s, H, W, Co
+    gemm(d)
+    return out
+
+
+def layernorm(x, gamma, beta, eps, out=None):
+    torch = _torch()
+    _check(x, torch.float32, "x")
+    rows, dim = x.shape
+    if out is None:
+        out = torch.empty((rows, dim), dtype=torch.bfloat16, device=x.device)
+    _lib.call("i2pc_layernorm", _p(x), x.stride(0), _p(gamma), _p(beta), float(eps), rows, dim,
+              _p(out), out.stride(0), _stream())
+    return out
+
+
+def attention(qkv, batch, tokens, heads, scale, out=None):
+    torch = _torch()
+    _check(qkv, torch.bfloat16, "qkv")
+    D = heads * 64
+    if out is None:
+        out = torch.empty((batch * tokens, D), dtype=torch.bfloat16, device=qkv.device)
+    _lib.call("i2pc_attention", _p(qkv), batch, tokens, heads, float(scale), _p(out), _stream())
+    return out
+
+
+def upsample2x(x, add=None, out=None):
+    torch = _torch()
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    if out is None:
+        out = torch.empty((B, 2 * H, 2 * W, C), dtype=torch.bfloat16, device=x.device)
+    _lib.call("i2pc_upsample2x", _p(x), B, H, W, C, _p(add), _p(out), _stream())
+    return out
+
+
+def cls_pos(cls, pos0, x, batch, tokens, dim):
+    _lib.call("i2pc_cls_pos", _p(cls), _p(pos0), batch, tokens, dim, _p(x), _stream())
+
+
+def f32_to_bf16(x, out=None):
+    torch = _torch()
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    _lib.call("i2pc_f32_to_bf16", _p(x), x.numel(), _p(out), _stream())
+    return out
+
+
+def head_out(x, w, bias: float, out=None):
+    torch = _torch()
+    B, H, W, C = x.shape
+    if out is None:
+        out = torch.empty((B, H, W), dtype=torch.float32, device=x.device)
+    _lib.call("i2pc_head_out", _p(x), B * H * W, C, _p(w), float(bias), _p(out), _stream())
+    return out

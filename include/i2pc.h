@@ -86,6 +86,69 @@ int i2pc_unproject(const float* depth, int dep_h, int dep_w,
 int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,
                        float* out_xyz, float* out_rgb, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Depth network building blocks (replace the PyTorch CPU conv / linear / SDPA /
+ * LayerNorm arithmetic that process_with_depth_anything reaches through
+ * transformers, backend/app.py:109-113).  bf16 operands, fp32 accumulation.
+ * ------------------------------------------------------------------------ */
+
+/* out[m][n] = epilogue( sum_k A[m][k] * W[n][k] ) on the MFMA cores.
+ * A: bf16 rows (dense, row r(m) = (m / a_group)*a_group_stride + m % a_group + a_offset,
+ *    a_group = 0 means r(m) = m + a_offset), or with conv = 1 the implicit im2col of an
+ *    NHWC bf16 image [conv_batch, conv_h, conv_w, conv_c] for a conv_k x conv_k
+ *    convolution (k order = (ky, kx, ci)), stride conv_stride, zero padding conv_pad,
+ *    optional ReLU applied to the input (conv_relu_in; pre-activation residual units).
+ * W: bf16 [n][k], row stride ldw.
+ * Epilogue in fp32, in this order: + bias[n]; + row_bias[m / row_bias_group][n];
+ *    + table[m % table_rows][n]; act (0 none, 1 GELU-erf, 2 ReLU); + res (fp32 or bf16,
+ *    same indexing as the output); + res2 (bf16); store bf16 (c_f32 = 0) or fp32.
+ * Output row o(m) = (m / out_group)*out_group_stride + m % out_group + out_offset
+ *    (row stride ldc), or, with convt_s > 0, the ConvTranspose(kernel = stride = s)
+ *    pixel shuffle: m = (b, iy, ix) over convt_h x convt_w, n = (dy*s + dx)*convt_c + co
+ *    -> NHWC [b][iy*s+dy][ix*s+dx][co].
+ * Requires k % 64 == 0, n % 32 == 0, conv_c % 64 == 0. */
+typedef struct i2pc_gemm_desc {
+  const void* a; int64_t lda; int32_t m, n, k;
+  int32_t a_group, a_group_stride, a_offset;
+  int32_t conv, conv_batch, conv_h, conv_w, conv_c, conv_oh, conv_ow, conv_k, conv_stride, conv_pad, conv_relu_in;
+  const void* w; int64_t ldw;
+  const float* bias;
+  const float* row_bias; int32_t row_bias_group;
+  const float* table; int32_t table_rows;
+  int32_t act;
+  const void* res; int32_t res_f32; int64_t ldr;
+  const void* res2; int64_t ldr2;
+  void* c; int32_t c_f32; int64_t ldc;
+  int32_t out_group, out_group_stride, out_offset;
+  int32_t convt_s, convt_h, convt_w, convt_c;
+} i2pc_gemm_desc;
+
+int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
+
+/* LayerNorm over the last dim: x fp32 [rows][dim] (row stride ldx) -> y bf16 [rows][dim]
+ * (row stride ldy); gamma/beta fp32 [dim]; two-pass mean/variance in fp32.
+ * (nn.LayerNorm, modeling_dpt.py:233-234). dim % 256 == 0, dim <= 2048. */
+int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
+                   int rows, int dim, void* y, int64_t ldy, void* stream);
+
+/* Fused multi-head self-attention (softmax(Q K^T * scale) V, no mask), head_dim 64.
+ * qkv: bf16 [batch*tokens][3*heads*64] (Q | K | V column blocks, the fused QKV GEMM output);
+ * out: bf16 [batch*tokens][heads*64]. (DPTSelfAttention, modeling_dpt.py:123-154) */
+int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scale, void* out, void* stream);
+
+/* Bilinear 2x upsample, align_corners = True, NHWC bf16 (nn.functional.interpolate,
+ * modeling_dpt.py:504-506, 698), optional + add (bf16, output shape). */
+int i2pc_upsample2x(const void* x, int batch, int h, int w, int c, const void* add, void* y, void* stream);
+
+/* Elementwise helpers of the ViT stem / neck. */
+/* rows [b*tokens + 0] of the fp32 residual stream = cls + pos[0] (modeling_dpt.py:226-231) */
+int i2pc_cls_pos(const float* cls, const float* pos0, int batch, int tokens, int dim, float* x, void* stream);
+/* fp32 -> bf16 copy of a [rows][dim] block */
+int i2pc_f32_to_bf16(const float* x, int64_t n, void* y, void* stream);
+/* depth[b][p] = relu( sum_c x[b][p][c] * w[c] + bias ), x bf16 NHWC with c <= 64
+ * (last 1x1 conv + ReLU of DPTDepthEstimationHead, modeling_dpt.py:701-702) */
+int i2pc_head_out(const void* x, int64_t pixels, int c, const float* w, float bias, float* depth, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,166 @@
+"""Numerics of the network kernels against plain PyTorch fp32 references.
+
+Inputs are rounded to bf16 first, so the only differences are fp32 summation
+order and the bf16 rounding of outputs.  Tolerance (stated per check):
+relative Frobenius error <= 8e-3 and max |err| <= 2e-2 * max |ref|.
+"""
+import math
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+F = torch.nn.functional
+
+
+def _ops():
+    from image_to_pointcloud_amd import ops
+    return ops
+
+
+def _close(got, ref, rel=8e-3, mx=2e-2):
+    got = got.float()
+    ref = ref.float()
+    err = (got - ref)
+    fro = err.norm() / ref.norm().clamp_min(1e-30)
+    m = err.abs().max() / ref.abs().max().clamp_min(1e-30)
+    assert fro <= rel and m <= mx, f"rel fro {fro:.3e}, max {m:.3e}"
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda")
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (18464 // 8, 1024, 1024), (77, 96, 64), (129, 32, 128)])
+def test_linear_bias_gelu_residual(dev, M, N, K):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = _bf(torch.randn(M, K, generator=g)).to(dev)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    r = torch.randn(M, N, generator=g).to(dev)
+    got = ops.linear(x, w, bias=b, act="gelu", res=r, out_f32=True)
+    ref = F.gelu(x.float() @ w.float().T + b) + r
+    _close(got, ref)
+    got2 = ops.linear(x, w, bias=b)
+    _close(got2, x.float() @ w.float().T + b)
+
+
+def test_linear_row_maps_and_tables(dev):
+    """CLS-skipping A remap, per-image row bias, per-row table, output remap (patch embed / readout)."""
+    ops = _ops()
+    B, T, D, N = 3, 17, 128, 64     # tokens = 1 CLS + 16 patches
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = _bf(torch.randn(B * T, D, generator=g)).to(dev)
+    w = _bf(torch.randn(N, D, generator=g) / math.sqrt(D)).to(dev)
+    rb = torch.randn(B, N, generator=g).to(dev)
+    tbl = torch.randn(T - 1, N, generator=g).to(dev)
+    out = torch.zeros(B * T, N, device=dev, dtype=torch.float32)
+    ops.linear(x, w, rows=B * (T - 1), a_map=(T - 1, T, 1), row_bias=rb, row_bias_group=T - 1,
+               table=tbl, table_rows=T - 1, out=out, out_map=(T - 1, T, 1))
+    xs = x.float().view(B, T, D)[:, 1:]
+    ref = xs @ w.float().T + rb[:, None, :] + tbl[None]
+    _close(out.view(B, T, N)[:, 1:], ref)
+    assert torch.all(out.view(B, T, N)[:, 0] == 0)
+
+
+def _pack_conv(w):      # [Co, Ci, k, k] -> [Co, k*k*Ci] (ky, kx, ci)
+    return _bf(w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)).contiguous()
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,stride", [(2, 24, 24, 256, 256, 1), (2, 24, 24, 1024, 256, 2),
+                                                (1, 13, 17, 64, 32, 1), (2, 12, 12, 128, 128, 1)])
+def test_conv3x3(dev, B, H, W, C, Co, stride):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(B * H + C)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    w = (torch.randn(Co, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    b = torch.randn(Co, generator=g).to(dev)
+    wp = _pack_conv(w)
+    got = ops.conv2d(x, wp, bias=b, stride=stride)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), _bf(w).float(), b, stride=stride, padding=1).permute(0, 2, 3, 1)
+    _close(got, ref)
+
+
+def test_conv_preact_residual_unit(dev):
+    """ReLU-on-input conv + ReLU epilogue, then conv + bias + two residuals (DPT fusion unit)."""
+    ops = _ops()
+    B, H, W, C = 2, 24, 24, 256
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    hid = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    w1 = (torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    w2 = (torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    b1 = torch.randn(C, generator=g).to(dev) * 0.1
+    b2 = torch.randn(C, generator=g).to(dev) * 0.1
+    y1 = ops.conv2d(x, _pack_conv(w1), bias=b1, relu_in=True, act="relu")
+    y2 = ops.conv2d(y1, _pack_conv(w2), bias=b2, res=x, res2=hid)
+    xc = x.float().permute(0, 3, 1, 2)
+    r1 = F.relu(F.conv2d(F.relu(xc), _bf(w1).float(), b1, padding=1))
+    r2 = F.conv2d(_bf(r1).float(), _bf(w2).float(), b2, padding=1) + xc + hid.float().permute(0, 3, 1, 2)
+    _close(y2, r2.permute(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("s,C", [(4, 256), (2, 512)])
+def test_conv_transpose(dev, s, C):
+    ops = _ops()
+    B, H, W = 2, 24, 24
+    g = torch.Generator(device="cpu").manual_seed(s)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    w = (torch.randn(C, C, s, s, generator=g) / math.sqrt(C)).to(dev)   # [Ci, Co, s, s]
+    b = torch.randn(C, generator=g).to(dev)
+    wp = _bf(w.permute(2, 3, 1, 0).reshape(s * s * C, C)).contiguous()
+    bt = b.repeat(s * s).contiguous()
+    got = ops.conv_transpose(x, wp, bt, s)
+    ref = F.conv_transpose2d(x.float().permute(0, 3, 1, 2), _bf(w).float(), b, stride=s).permute(0, 2, 3, 1)
+    _close(got, ref)
+
+
+@pytest.mark.parametrize("rows,dim", [(1000, 1024), (37, 768), (5, 384 * 2)])
+def test_layernorm(dev, rows, dim):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(rows)
+    x = (torch.randn(rows, dim, generator=g) * 3 + 1).to(dev)
+    ga = torch.randn(dim, generator=g).to(dev)
+    be = torch.randn(dim, generator=g).to(dev)
+    got = ops.layernorm(x, ga, be, 1e-12)
+    _close(got, F.layer_norm(x, (dim,), ga, be, 1e-12))
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 577, 16), (1, 37, 6), (3, 1, 4), (2, 130, 12), (1, 1370, 6)])
+def test_attention(dev, B, T, H):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(T)
+    qkv = _bf(torch.randn(B * T, 3 * H * 64, generator=g) * 1.5).to(dev)
+    got = ops.attention(qkv, B, T, H, 0.125)
+    q, k, v = qkv.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    _close(got, ref, rel=1.2e-2, mx=3e-2)
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 12, 12, 256), (1, 5, 7, 64), (1, 192, 192, 128)])
+def test_upsample2x_align_corners(dev, B, H, W, C):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(H)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    add = _bf(torch.randn(B, 2 * H, 2 * W, C, generator=g)).to(dev)
+    got = ops.upsample2x(x, add=add)
+    ref = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
+                        align_corners=True).permute(0, 2, 3, 1) + add.float()
+    _close(got, ref)
+
+
+def test_head_out(dev):
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = _bf(torch.randn(2, 40, 30, 32, generator=g)).to(dev)
+    w = torch.randn(32, generator=g).to(dev)
+    got = ops.head_out(x, w, 0.25)
+    ref = F.relu(x.float() @ w + 0.25)
+    _close(got, ref, rel=1e-5, mx=1e-5)
