@@ -29,6 +29,7 @@ SOURCES = [
     "gemm.hip",
     "misc.hip",
     "attention.hip",
+    "preprocess.hip",
 ]
 HEADERS = ["common.h", "../../include/i2pc.h"]
 

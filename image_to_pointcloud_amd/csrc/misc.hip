@@ -61,6 +61,34 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
   }
 }
 
+// generic row width (dim % 64 == 0, dim <= 2048): E scalars per lane, stride 64 (coalesced)
+__global__ __launch_bounds__(256) void k_layernorm_any(const float* __restrict__ x, int64_t ldx,
+                                                       const float* __restrict__ g, const float* __restrict__ b,
+                                                       float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int E = dim / 64;
+  const float* xr = x + row * ldx;
+  float v[32];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    v[i] = i < E ? xr[i * 64 + lane] : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / (float)dim;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i)
+    if (i < E) { const float a = v[i] - mean; q += a * a; }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)dim + eps);
+  bf16_t* yr = y + row * ldy;
+#pragma unroll
+  for (int i = 0; i < 32; ++i)
+    if (i < E) yr[i * 64 + lane] = f2bf((v[i] - mean) * rstd * g[i * 64 + lane] + b[i * 64 + lane]);
+}
+
 // NHWC bf16, 8 channels (16 B) per thread; torch upsample_bilinear2d, align_corners=True.
 __global__ __launch_bounds__(256) void k_upsample2x(const bf16_t* __restrict__ x, int B, int h, int w, int c,
                                                     const bf16_t* __restrict__ add, bf16_t* __restrict__ y) {
@@ -162,11 +190,15 @@ extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, c
                               int rows, int dim, void* y, int64_t ldy, void* stream) {
   clear_error();
   I2PC_REQUIRE(x && gamma && beta && y, "NULL pointer");
-  I2PC_REQUIRE(rows > 0 && dim > 0 && dim % 256 == 0 && dim <= 2048, "layernorm: dim=%d must be a multiple of 256 <= 2048", dim);
+  I2PC_REQUIRE(rows > 0 && dim > 0 && dim % 64 == 0 && dim <= 2048, "layernorm: dim=%d must be a multiple of 64 <= 2048", dim);
   I2PC_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "layernorm: row strides must be multiples of 4");
   hipStream_t s = as_stream(stream);
   const dim3 grid((rows + 3) / 4), block(256);
   bf16_t* yy = static_cast<bf16_t*>(y);
+  if (dim % 256 != 0) {
+    hipLaunchKernelGGL(k_layernorm_any, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy);
+    return check_launch("layernorm");
+  }
   switch (dim / 256) {
     case 1: hipLaunchKernelGGL(k_layernorm<1>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
     case 2: hipLaunchKernelGGL(k_layernorm<2>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;

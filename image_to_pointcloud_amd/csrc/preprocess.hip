@@ -1,0 +1,266 @@
+// Network input pipeline on the GPU (gfx950): BGR uint8 -> RGB -> Pillow-exact
+// separable bicubic resample (8-bit fixed point, uint8 intermediate) -> rescale
+// 1/255 (float64 -> float32) -> (x - mean) / std (float32), written either as
+// float32 NCHW pixel_values or directly as bf16 patch rows for the patch-embed GEMM.
+//
+// Replaces backend/app.py:103 (cvtColor) + :109 (DPTImageProcessorPil:
+// transformers image_processing_pil_dpt.py:192-267, image_transforms.py:89-122,
+// 313-440) and the patchify of DPTViTPatchEmbeddings (modeling_dpt.py:60-69).
+// Coefficients follow Pillow's libImaging/Resample.c (precompute_coeffs /
+// normalize_coeffs_8bpc, PRECISION_BITS = 22) and are computed once per size on
+// the host (i2pc_preprocess_plan_create), so the device path is pure integer
+// arithmetic and bit-exact.
+//
+// One workgroup = one image x a band of R output rows: the horizontal pass
+// resamples exactly the input rows that band needs into LDS (uint8), the
+// vertical pass reads them back; nothing but the input and the output touch HBM.
+#include "common.h"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+namespace i2pc {
+namespace pre {
+
+constexpr int PB = 32 - 8 - 2;     // PRECISION_BITS
+constexpr int kLdsBudget = 60 * 1024;
+
+struct Axis {
+  int out, ksize;
+  std::vector<int> xmin, cnt;
+  std::vector<int> k;   // [out][ksize] fixed point
+};
+
+static double bicubic(double x) {
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+
+// Pillow precompute_coeffs + normalize_coeffs_8bpc (box = [0, in_size)).
+static Axis coeffs(int in_size, int out_size) {
+  Axis ax;
+  ax.out = out_size;
+  const float in0 = 0.f, in1 = (float)in_size;
+  double scale = (double)(in1 - in0) / out_size;
+  double filterscale = scale;
+  if (filterscale < 1.0) filterscale = 1.0;
+  const double support = 2.0 * filterscale;
+  ax.ksize = (int)std::ceil(support) * 2 + 1;
+  ax.xmin.resize(out_size);
+  ax.cnt.resize(out_size);
+  ax.k.assign((size_t)out_size * ax.ksize, 0);
+  std::vector<double> kk(ax.ksize);
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = in0 + (xx + 0.5) * scale;
+    double ww = 0.0;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    for (int x = 0; x < xmax; ++x) {
+      const double w = bicubic((x + xmin - center + 0.5) * ss);
+      kk[x] = w;
+      ww += w;
+    }
+    for (int x = 0; x < xmax; ++x)
+      if (ww != 0.0) kk[x] /= ww;
+    for (int x = 0; x < xmax; ++x) {
+      const double v = kk[x] * (1 << PB);
+      ax.k[(size_t)xx * ax.ksize + x] = kk[x] < 0 ? (int)(-0.5 + v) : (int)(0.5 + v);
+    }
+    ax.xmin[xx] = xmin;
+    ax.cnt[xx] = xmax;
+  }
+  return ax;
+}
+
+static Axis identity(int n) {
+  Axis ax;
+  ax.out = n;
+  ax.ksize = 1;
+  ax.xmin.resize(n);
+  ax.cnt.assign(n, 1);
+  ax.k.assign(n, 1 << PB);
+  for (int i = 0; i < n; ++i) ax.xmin[i] = i;
+  return ax;
+}
+
+struct DevPlan {
+  int in_h, in_w, out_h, out_w, kx, ky, R, tiles, patch, lds_bytes;
+  float mean[3], stdv[3];
+  const int* hx_min; const int* hx_cnt; const int* hx_k;
+  const int* vy_min; const int* vy_cnt; const int* vy_k;
+  const int* tile_lo; const int* tile_n;
+};
+
+}  // namespace pre
+}  // namespace i2pc
+
+struct i2pc_preprocess_plan {
+  i2pc::pre::DevPlan p;
+  void* dev;
+};
+
+namespace i2pc {
+namespace pre {
+
+__device__ __forceinline__ uint8_t clip8(int ss) {
+  if (ss >= (1 << PB << 8)) return 255;
+  if (ss <= 0) return 0;
+  return (uint8_t)(ss >> PB);
+}
+
+__global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __restrict__ bgr, int layout, void* out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t tmp[];   // [rows][out_w][3] uint8 (BGR order)
+  const int b = blockIdx.x / P.tiles;
+  const int tile = blockIdx.x - b * P.tiles;
+  const int ylo = P.tile_lo[tile];
+  const int nrows = P.tile_n[tile];
+  const uint8_t* img = bgr + (int64_t)b * P.in_h * P.in_w * 3;
+  const int OW = P.out_w;
+  // horizontal pass: input rows [ylo, ylo + nrows) -> LDS
+  const int hwork = nrows * OW;
+  for (int i = threadIdx.x; i < hwork; i += blockDim.x) {
+    const int r = i / OW;
+    const int xx = i - r * OW;
+    const uint8_t* row = img + (int64_t)(ylo + r) * P.in_w * 3;
+    const int xmin = P.hx_min[xx], cnt = P.hx_cnt[xx];
+    const int* k = P.hx_k + xx * P.kx;
+    int s0 = 1 << (PB - 1), s1 = s0, s2 = s0;
+    for (int x = 0; x < cnt; ++x) {
+      const uint8_t* px = row + (xmin + x) * 3;
+      const int kv = k[x];
+      s0 += px[0] * kv;
+      s1 += px[1] * kv;
+      s2 += px[2] * kv;
+    }
+    uint8_t* t = tmp + (r * OW + xx) * 3;
+    t[0] = clip8(s0);
+    t[1] = clip8(s1);
+    t[2] = clip8(s2);
+  }
+  __syncthreads();
+  // vertical pass + rescale/normalise + layout
+  const int y0 = tile * P.R;
+  const int rows_out = min(P.R, P.out_h - y0);
+  const int vwork = rows_out * OW;
+  const int np_x = OW / max(P.patch, 1);
+  const int npatch = (P.out_h / max(P.patch, 1)) * np_x;
+  for (int i = threadIdx.x; i < vwork; i += blockDim.x) {
+    const int ry = i / OW;
+    const int xx = i - ry * OW;
+    const int yy = y0 + ry;
+    const int ymin = P.vy_min[yy] - ylo, cnt = P.vy_cnt[yy];
+    const int* k = P.vy_k + yy * P.ky;
+    int s[3] = {1 << (PB - 1), 1 << (PB - 1), 1 << (PB - 1)};
+    for (int y = 0; y < cnt; ++y) {
+      const uint8_t* t = tmp + ((ymin + y) * OW + xx) * 3;
+      const int kv = k[y];
+      s[0] += t[0] * kv;
+      s[1] += t[1] * kv;
+      s[2] += t[2] * kv;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {       // c = RGB channel; BGR source index 2 - c
+      const uint8_t u = clip8(s[2 - c]);
+      const float f = (float)((double)u * (1.0 / 255.0));
+      const float v = (f - P.mean[c]) / P.stdv[c];
+      if (layout == 0) {
+        static_cast<float*>(out)[(((int64_t)b * 3 + c) * P.out_h + yy) * OW + xx] = v;
+      } else {
+        const int p = P.patch;
+        const int prow = b * npatch + (yy / p) * np_x + xx / p;
+        const int col = c * p * p + (yy % p) * p + (xx % p);
+        __bf16 h = (__bf16)v;
+        static_cast<uint16_t*>(out)[(int64_t)prow * 3 * p * p + col] = *reinterpret_cast<uint16_t*>(&h);
+      }
+    }
+  }
+}
+
+}  // namespace pre
+}  // namespace i2pc
+
+using namespace i2pc;
+using namespace i2pc::pre;
+
+extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int out_w, const float* mean,
+                                           const float* stdv, int patch, i2pc_preprocess_plan** plan) {
+  clear_error();
+  I2PC_REQUIRE(plan && mean && stdv, "NULL argument");
+  I2PC_REQUIRE(in_h > 0 && in_w > 0 && out_h > 0 && out_w > 0, "empty size");
+  I2PC_REQUIRE(patch >= 0, "patch must be >= 0");
+  if (patch > 0) I2PC_REQUIRE(out_h % patch == 0 && out_w % patch == 0, "output %dx%d not a multiple of patch %d", out_h, out_w, patch);
+  Axis hx = out_w != in_w ? coeffs(in_w, out_w) : identity(in_w);
+  Axis vy = out_h != in_h ? coeffs(in_h, out_h) : identity(in_h);
+  // rows per workgroup so that the uint8 intermediate fits the LDS budget
+  const double scale = (double)in_h / out_h;
+  const int row_bytes = out_w * 3;
+  I2PC_REQUIRE(row_bytes * (vy.ksize + 2) <= kLdsBudget, "output width %d too large for one LDS band", out_w);
+  int R = 1;
+  for (int r = 64; r >= 1; r /= 2) {
+    // rows needed by r output rows <= (r - 1) * scale + ksize + 2
+    const double need = (r - 1) * scale + vy.ksize + 2;
+    if (need * row_bytes <= kLdsBudget) { R = r; break; }
+  }
+  const int tiles = (out_h + R - 1) / R;
+  std::vector<int> tlo(tiles), tn(tiles);
+  int max_rows = 0;
+  for (int t = 0; t < tiles; ++t) {
+    const int y0 = t * R, y1 = std::min(out_h, y0 + R);
+    int lo = 1 << 30, hi = 0;
+    for (int y = y0; y < y1; ++y) { lo = std::min(lo, vy.xmin[y]); hi = std::max(hi, vy.xmin[y] + vy.cnt[y]); }
+    tlo[t] = lo;
+    tn[t] = hi - lo;
+    max_rows = std::max(max_rows, hi - lo);
+  }
+  I2PC_REQUIRE(max_rows * row_bytes <= 64 * 1024, "LDS band too large (%d rows)", max_rows);
+  // one device buffer: hx_min | hx_cnt | hx_k | vy_min | vy_cnt | vy_k | tile_lo | tile_n
+  std::vector<int> blob;
+  auto put = [&](const std::vector<int>& v) { size_t off = blob.size(); blob.insert(blob.end(), v.begin(), v.end()); return off; };
+  const size_t o0 = put(hx.xmin), o1 = put(hx.cnt), o2 = put(hx.k), o3 = put(vy.xmin), o4 = put(vy.cnt), o5 = put(vy.k),
+               o6 = put(tlo), o7 = put(tn);
+  void* dev = nullptr;
+  if (hipMalloc(&dev, blob.size() * sizeof(int)) != hipSuccess) return set_error(I2PC_ELAUNCH, "hipMalloc failed");
+  if (hipMemcpy(dev, blob.data(), blob.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(dev);
+    return set_error(I2PC_ELAUNCH, "hipMemcpy failed");
+  }
+  auto* pl = new i2pc_preprocess_plan();
+  pl->dev = dev;
+  DevPlan& P = pl->p;
+  P.in_h = in_h; P.in_w = in_w; P.out_h = out_h; P.out_w = out_w;
+  P.kx = hx.ksize; P.ky = vy.ksize; P.R = R; P.tiles = tiles; P.patch = patch;
+  P.lds_bytes = (int)align_up((size_t)max_rows * row_bytes, 16);
+  for (int c = 0; c < 3; ++c) { P.mean[c] = mean[c]; P.stdv[c] = stdv[c]; }
+  const int* base = static_cast<const int*>(dev);
+  P.hx_min = base + o0; P.hx_cnt = base + o1; P.hx_k = base + o2;
+  P.vy_min = base + o3; P.vy_cnt = base + o4; P.vy_k = base + o5;
+  P.tile_lo = base + o6; P.tile_n = base + o7;
+  *plan = pl;
+  return I2PC_OK;
+}
+
+extern "C" void i2pc_preprocess_plan_destroy(i2pc_preprocess_plan* plan) {
+  if (!plan) return;
+  (void)hipFree(plan->dev);
+  delete plan;
+}
+
+extern "C" int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* bgr, int batch, int layout,
+                               void* out, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(plan && bgr && out && batch > 0, "bad arguments");
+  I2PC_REQUIRE(layout == 0 || (layout == 1 && plan->p.patch > 0), "layout must be 0 (fp32 NCHW) or 1 (bf16 patch rows, plan with patch > 0)");
+  const DevPlan& P = plan->p;
+  hipLaunchKernelGGL(k_preprocess, dim3(batch * P.tiles), dim3(256), P.lds_bytes, as_stream(stream), P, bgr, layout, out);
+  return check_launch("preprocess");
+}

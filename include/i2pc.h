@@ -127,7 +127,7 @@ int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
 
 /* LayerNorm over the last dim: x fp32 [rows][dim] (row stride ldx) -> y bf16 [rows][dim]
  * (row stride ldy); gamma/beta fp32 [dim]; two-pass mean/variance in fp32.
- * (nn.LayerNorm, modeling_dpt.py:233-234). dim % 256 == 0, dim <= 2048. */
+ * (nn.LayerNorm, modeling_dpt.py:233-234). dim % 64 == 0, dim <= 2048. */
 int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
                    int rows, int dim, void* y, int64_t ldy, void* stream);
 
@@ -148,6 +148,21 @@ int i2pc_f32_to_bf16(const float* x, int64_t n, void* y, void* stream);
 /* depth[b][p] = relu( sum_c x[b][p][c] * w[c] + bias ), x bf16 NHWC with c <= 64
  * (last 1x1 conv + ReLU of DPTDepthEstimationHead, modeling_dpt.py:701-702) */
 int i2pc_head_out(const void* x, int64_t pixels, int c, const float* w, float bias, float* depth, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Network input (app.py:103 cvtColor BGR->RGB + app.py:109 DPTImageProcessorPil):
+ * Pillow-exact bicubic resample, rescale 1/255, normalise, optional patchify.
+ * A plan holds the per-size Pillow coefficient tables (computed on the host and
+ * uploaded once: create/destroy are NOT stream-ordered; i2pc_preprocess is).
+ * ------------------------------------------------------------------------ */
+typedef struct i2pc_preprocess_plan i2pc_preprocess_plan;
+int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int out_w, const float* mean3, const float* std3,
+                                int patch, i2pc_preprocess_plan** plan);
+void i2pc_preprocess_plan_destroy(i2pc_preprocess_plan* plan);
+/* bgr: uint8 [batch, in_h, in_w, 3]; layout 0 -> float32 [batch, 3, out_h, out_w] (pixel_values);
+ * layout 1 -> bf16 [batch * (out_h/patch)*(out_w/patch)][3*patch*patch], column order (c, py, px)
+ * (the im2col of the patch-embedding conv, modeling_dpt.py:60-69). */
+int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* bgr, int batch, int layout, void* out, void* stream);
 
 #ifdef __cplusplus
 }

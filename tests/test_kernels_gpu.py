@@ -122,7 +122,7 @@ def test_conv_transpose(dev, s, C):
     _close(got, ref)
 
 
-@pytest.mark.parametrize("rows,dim", [(1000, 1024), (37, 768), (5, 384 * 2)])
+@pytest.mark.parametrize("rows,dim", [(1000, 1024), (37, 768), (5, 384 * 2), (70, 384), (9, 128)])
 def test_layernorm(dev, rows, dim):
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(rows)
