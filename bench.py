@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Mpoints/sec end-to-end (depth + unproject) on synthetic 1024x1024 RGB batches.
+
+BASELINE.json metric / configs[1]: DPT-Large bf16, batch 32 x 1024^2, one
+MI355X per rank.  A step = preprocess + DPT-Large forward + depth resize +
+exact p2/p98 + normalise + unproject (density "high", 1,048,576 points/image)
++ RGB gather + bbox, for the rank's batch, inputs already resident in HBM,
+replayed as one HIP graph.  Ranks shard images (weak scaling, no data-path
+collective: each rank owns its images' point buffers).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+  roofline      -- the dominant kernel (by time in one eager, event-timed step):
+                   achieved = algorithmic FLOPs / average launch duration
+                   (HIP events on the launch stream), peak = 2.5 PF bf16 dense;
+  roofline_unproject -- the geometry stage against HBM (8 TB/s), algorithmic
+                   bytes 4*h'*w' + 18*N per image;
+  cpu_baseline  -- the reference CPU path restated (oracle/: Pillow-exact
+                   preprocessing, transformers fp32 DPT-Large forward on all
+                   host threads, the reference's per-point Python loop) on ONE
+                   1024^2 image, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (AMD's 5 PF headline is 2:1 sparse)
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--density", default="high", choices=["low", "medium", "high"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-profile", action="store_true")
+    return ap.parse_args()
+
+
+def _images(batch, size, rank, device):
+    import numpy as np
+    import torch
+    out = torch.empty((batch, size, size, 3), dtype=torch.uint8, device=device)
+    for i in range(batch):
+        rng = np.random.Generator(np.random.PCG64(1000 + rank * batch + i))   # image i seeded 1000+i
+        out[i] = torch.from_numpy(rng.integers(0, 256, (size, size, 3), dtype=np.uint8)).to(device)
+    return out
+
+
+def _kernel_profile(pipe, images):
+    """One eager step with HIP events around every network launch + the geometry stage."""
+    import torch
+    from image_to_pointcloud_amd import geometry, ops
+    ops.profile = []
+    stream = torch.cuda.current_stream()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    pipe.pre(images, layout="patches", out=pipe._patches)
+    depth = pipe.model(pipe._patches, pipe.batch)
+    e0.record(stream)
+    geometry.unproject_batch(depth, images, density=pipe.density, invert=pipe.invert,
+                             depth_scale=pipe.depth_scale, out=pipe._out)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    recs = ops.profile
+    ops.profile = None
+    per = {}
+    for label, flops, nbytes, a, b in recs:
+        t = a.elapsed_time(b) * 1e-3
+        d = per.setdefault(label, {"n": 0, "t": 0.0, "flops": 0.0, "bytes": 0.0})
+        d["n"] += 1
+        d["t"] += t
+        d["flops"] += flops
+        d["bytes"] += nbytes
+    geo_t = e0.elapsed_time(e1) * 1e-3
+    return per, geo_t
+
+
+def _cpu_baseline():
+    """Reference CPU path (restated) on one 1024^2 image, density high."""
+    import numpy as np
+    import torch
+    from transformers import DPTConfig, DPTForDepthEstimation
+
+    from image_to_pointcloud_amd.dpt import DPT_LARGE, synthetic_state_dict
+    from oracle import preprocess_ref, unproject_ref
+
+    threads = os.cpu_count() or 1
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    model = DPTForDepthEstimation(DPTConfig(**DPT_LARGE.hf_config_kwargs()))
+    model.load_state_dict(synthetic_state_dict(DPT_LARGE, 0), strict=False)
+    model.eval()
+    rng = np.random.Generator(np.random.PCG64(1000))
+    img = rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8)
+    t0 = time.perf_counter()
+    pix = preprocess_ref.dpt_preprocess(img)                            # app.py:103,109
+    with torch.no_grad():                                               # app.py:111-116
+        depth = model(pixel_values=torch.from_numpy(pix)[None]).predicted_depth[0].numpy().astype(np.float32)
+    t1 = time.perf_counter()
+    pts, _ = unproject_ref.depth_to_point_cloud(img, depth, density="high", loop=True)   # app.py:174-250
+    unproject_ref.gis_bounds(pts)
+    t2 = time.perf_counter()
+    n = len(pts)
+    return {"value": n / (t2 - t0) / 1e6, "unit": "Mpoints/s", "cores": threads, "kind": "port",
+            "sample": f"1 image 1024x1024, density high ({n} points): Pillow-exact preprocessing + transformers "
+                      f"fp32 DPT-Large forward on {threads} threads ({t1 - t0:.2f} s) + the reference per-point "
+                      f"Python loop, single-threaded ({t2 - t1:.2f} s)",
+            "seconds": t2 - t0}
+
+
+def main():
+    a = _args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from image_to_pointcloud_amd.dpt import DPT_LARGE
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+
+    B, S = a.batch, a.size
+    pipe = PointCloudPipeline(B, S, S, spec=DPT_LARGE, density=a.density, device=device, seed=0)
+    images = _images(B, S, rank, device)
+    if a.no_graph:
+        step = lambda: pipe.run(images)     # noqa: E731
+        step()
+    else:
+        pipe.capture(images)
+        step = pipe.replay
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    points_step = world * B * pipe.points_per_image
+    value = points_step * a.steps / elapsed / 1e6
+    ms = elapsed / a.steps * 1e3
+
+    roofline = roof_geo = None
+    kernels = None
+    if rank == 0 and not a.no_kernel_profile:
+        per, geo_t = _kernel_profile(pipe, images)
+        dom = max(per.items(), key=lambda kv: kv[1]["t"])
+        name, d = dom
+        if d["flops"] > 0:
+            ach = d["flops"] / d["n"] / (d["t"] / d["n"]) / 1e12
+            roofline = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": BF16_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                        "launches": d["n"], "avg_us": round(d["t"] / d["n"] * 1e6, 2),
+                        "flops_per_launch": d["flops"] / d["n"],
+                        "share_of_step": round(d["t"] / (ms * 1e-3), 3)}
+        else:
+            ach = d["bytes"] / (d["t"]) / 1e9
+            roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+        g = DPT_LARGE.grid * DPT_LARGE.patch
+        geo_bytes = B * (4.0 * g * g + 18.0 * pipe.points_per_image)
+        roof_geo = {"kernel": "i2pc_unproject (select + unproject + bbox launches)", "bound": "hbm",
+                    "achieved": round(geo_bytes / geo_t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(geo_bytes / geo_t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                    "ms": round(geo_t * 1e3, 3), "bytes_per_step": geo_bytes}
+        kernels = {k: {"launches": v["n"], "ms": round(v["t"] * 1e3, 3),
+                       "tflops": round(v["flops"] / v["t"] / 1e12, 1) if v["flops"] else None}
+                   for k, v in sorted(per.items(), key=lambda kv: -kv[1]["t"])}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            cpu = _cpu_baseline()
+        except Exception as e:   # the GPU figure stands on its own; say why the baseline is missing
+            cpu = {"value": None, "unit": "Mpoints/s", "cores": os.cpu_count(), "kind": "port",
+                   "sample": f"failed: {type(e).__name__}: {e}"}
+
+    if rank == 0:
+        flops_img = DPT_LARGE.flops_per_image()
+        out = {
+            "metric": "Mpoints/sec end-to-end (depth+unproject), 1024² batch",
+            "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic (uint8 RGB uniform, PCG64 seeds 1000+i; seeded random DPT-Large weights)",
+            "config": {"workload": f"DPT-Large bf16 depth + unproject, batch {B} x {S}x{S} per GPU, density {a.density}",
+                       "model": "DPT-Large (ViT-L/16, 384x384 network input)", "global_batch": B * world,
+                       "image": [S, S], "points_per_image": pipe.points_per_image, "parallelism": f"dp{world}",
+                       "hip_graph": not a.no_graph},
+            "network_tflops": round(flops_img * B * world / (elapsed / a.steps) / 1e12, 1),
+            "roofline": roofline,
+            "roofline_unproject": roof_geo,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

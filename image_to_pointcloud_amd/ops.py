@@ -76,8 +76,54 @@ def _check(t, dtype, name):
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
 
 
+# ---------------------------------------------------------------- launch timing
+# When `profile` is a list, every wrapped launch appends (kernel label, flops,
+# bytes, start event, end event) recorded on the launch stream; bench.py turns
+# that into per-kernel durations and roofline fractions.
+profile = None
+
+
+class _Timed:
+    def __init__(self, label, flops=0.0, nbytes=0.0):
+        self.label, self.flops, self.nbytes = label, flops, nbytes
+
+    def __enter__(self):
+        if profile is not None:
+            torch = _torch()
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record(torch.cuda.current_stream())
+        return self
+
+    def __exit__(self, *exc):
+        if profile is not None:
+            torch = _torch()
+            self.e1.record(torch.cuda.current_stream())
+            profile.append((self.label, self.flops, self.nbytes, self.e0, self.e1))
+        return False
+
+
+def gemm_kernel_label(desc: GemmDesc) -> str:
+    """Name of the k_gemm instance i2pc_gemm dispatches to (mirrors gemm.hip `dispatch`)."""
+    M, N = desc.m, desc.n
+    t128 = ((M + 127) // 128) * (N // 128)
+    if N % 128 == 0 and t128 >= 512:
+        bm, bn = 128, 128
+    elif N % 64 == 0:
+        bm, bn = 128, 64
+    else:
+        bm, bn = 128, 32
+    conv = "true" if desc.conv else "false"
+    relu = "true" if desc.conv_relu_in else "false"
+    return f"k_gemm<{bm}, {bn}, {conv}, {relu}>"
+
+
 def gemm(desc: GemmDesc) -> None:
-    _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
+    if profile is None:
+        _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
+        return
+    with _Timed(gemm_kernel_label(desc), 2.0 * desc.m * desc.n * desc.k):
+        _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
 
 
 def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=False,
@@ -167,8 +213,9 @@ def layernorm(x, gamma, beta, eps, out=None):
     rows, dim = x.shape
     if out is None:
         out = torch.empty((rows, dim), dtype=torch.bfloat16, device=x.device)
-    _lib.call("i2pc_layernorm", _p(x), x.stride(0), _p(gamma), _p(beta), float(eps), rows, dim,
-              _p(out), out.stride(0), _stream())
+    with _Timed("k_layernorm", 0.0, rows * dim * 6.0):
+        _lib.call("i2pc_layernorm", _p(x), x.stride(0), _p(gamma), _p(beta), float(eps), rows, dim,
+                  _p(out), out.stride(0), _stream())
     return out
 
 
@@ -178,7 +225,8 @@ def attention(qkv, batch, tokens, heads, scale, out=None):
     D = heads * 64
     if out is None:
         out = torch.empty((batch * tokens, D), dtype=torch.bfloat16, device=qkv.device)
-    _lib.call("i2pc_attention", _p(qkv), batch, tokens, heads, float(scale), _p(out), _stream())
+    with _Timed("k_attention", 4.0 * batch * heads * tokens * tokens * 64):
+        _lib.call("i2pc_attention", _p(qkv), batch, tokens, heads, float(scale), _p(out), _stream())
     return out
 
 
@@ -188,7 +236,8 @@ def upsample2x(x, add=None, out=None):
     B, H, W, C = x.shape
     if out is None:
         out = torch.empty((B, 2 * H, 2 * W, C), dtype=torch.bfloat16, device=x.device)
-    _lib.call("i2pc_upsample2x", _p(x), B, H, W, C, _p(add), _p(out), _stream())
+    with _Timed("k_upsample2x", 0.0, 2.0 * B * H * W * C * (1 + 4 + (4 if add is not None else 0))):
+        _lib.call("i2pc_upsample2x", _p(x), B, H, W, C, _p(add), _p(out), _stream())
     return out
 
 
@@ -209,5 +258,6 @@ def head_out(x, w, bias: float, out=None):
     B, H, W, C = x.shape
     if out is None:
         out = torch.empty((B, H, W), dtype=torch.float32, device=x.device)
-    _lib.call("i2pc_head_out", _p(x), B * H * W, C, _p(w), float(bias), _p(out), _stream())
+    with _Timed("k_head_out", 2.0 * B * H * W * C, B * H * W * (2.0 * C + 4)):
+        _lib.call("i2pc_head_out", _p(x), B * H * W, C, _p(w), float(bias), _p(out), _stream())
     return out
