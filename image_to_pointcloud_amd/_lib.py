@@ -11,7 +11,7 @@ import os
 import re
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libi2pc.so")
+LIB_PATH = os.environ.get("I2PC_LIB") or os.path.join(_PKG, "libi2pc.so")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "i2pc.h")
 
 c_int = ctypes.c_int

@@ -8,6 +8,7 @@ Layouts: activations bf16 NHWC / [rows][features]; residual stream fp32.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 from . import _lib
@@ -106,16 +107,25 @@ class _Timed:
 def gemm_kernel_label(desc: GemmDesc) -> str:
     """Name of the k_gemm instance i2pc_gemm dispatches to (mirrors gemm.hip `dispatch`)."""
     M, N = desc.m, desc.n
+    t256 = ((M + 255) // 256) * (N // 256)
     t128 = ((M + 127) // 128) * (N // 128)
-    if N % 128 == 0 and t128 >= 512:
+    force = int(os.environ.get("I2PC_GEMM_TILE", "0") or 0)
+    if force == 256 and N % 256 == 0:
+        bm, bn = 256, 256
+    elif force == 128 and N % 128 == 0:
+        bm, bn = 128, 128
+    elif N % 256 == 0 and t256 >= 512:
+        bm, bn = 256, 256
+    elif N % 128 == 0 and t128 >= 512:
         bm, bn = 128, 128
     elif N % 64 == 0:
         bm, bn = 128, 64
     else:
         bm, bn = 128, 32
+    wm, wn = {(256, 256): (2, 4), (128, 128): (2, 2), (128, 64): (2, 2), (128, 32): (4, 1)}[(bm, bn)]
     conv = "true" if desc.conv else "false"
     relu = "true" if desc.conv_relu_in else "false"
-    return f"k_gemm<{bm}, {bn}, {conv}, {relu}>"
+    return f"k_gemm<{bm}, {bn}, {wm}, {wn}, {conv}, {relu}>"
 
 
 def gemm(desc: GemmDesc) -> None:

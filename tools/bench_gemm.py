@@ -1,0 +1,36 @@
+"""GEMM/conv microbenchmark on the DPT-Large shapes (batch 32): TFLOP/s per tile config + a numerics check."""
+import math, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from image_to_pointcloud_amd import ops
+
+dev = torch.device("cuda")
+M = 32 * 577
+shapes = [("qkv", M, 3072, 1024), ("o", M, 1024, 1024), ("fc1", M, 4096, 1024), ("fc2", M, 1024, 4096)]
+def timeit(fn, iters=20):
+    fn(); torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters): fn()
+    e1.record(); torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+g = torch.Generator(device="cpu").manual_seed(0)
+for tile in sys.argv[1:] or ["0"]:
+    os.environ["I2PC_GEMM_TILE"] = tile
+    # the C side caches the env var at first dispatch: run each tile in its own process
+for name, m, n, k in shapes:
+    x = (torch.rand(m, k, generator=g) * 2 - 1).to(torch.bfloat16).to(dev)
+    w = ((torch.rand(n, k, generator=g) * 2 - 1) / math.sqrt(k)).to(torch.bfloat16).to(dev)
+    b = torch.randn(n, generator=g).to(dev)
+    out = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
+    t = timeit(lambda: ops.linear(x, w, bias=b, out=out))
+    ref = x[:2048].float() @ w.float().T + b
+    err = ((out[:2048].float() - ref).norm() / ref.norm()).item()
+    print(f"tile={os.environ.get('I2PC_GEMM_TILE')} {name:4s} M={m} N={n} K={k}: {t*1e6:8.1f} us  {2*m*n*k/t/1e12:7.1f} TF  relerr={err:.2e}")
+# conv shapes (neck/fusion at 96x96 and head)
+for (B, H, W, C, Co) in [(32, 96, 96, 256, 256), (32, 48, 48, 256, 256), (32, 192, 192, 256, 128), (32, 384, 384, 128, 32)]:
+    x = (torch.rand(B, H, W, C, generator=g) * 2 - 1).to(torch.bfloat16).to(dev)
+    w = ((torch.rand(Co, 9 * C, generator=g) * 2 - 1) / math.sqrt(9 * C)).to(torch.bfloat16).to(dev)
+    out = torch.empty(B, H, W, Co, dtype=torch.bfloat16, device=dev)
+    t = timeit(lambda: ops.conv2d(x, w, out=out), iters=10)
+    print(f"tile={os.environ.get('I2PC_GEMM_TILE')} conv {B}x{H}x{W}x{C}->{Co}: {t*1e6:8.1f} us  {2*B*H*W*Co*9*C/t/1e12:7.1f} TF")
