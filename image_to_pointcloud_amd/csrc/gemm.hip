@@ -36,13 +36,13 @@ constexpr int BK = 64;
 __device__ __attribute__((aligned(16))) uint8_t g_zero[512];   // conv zero padding source
 #ifdef I2PC_STAMPS
 // diagnostic build only: per-block s_memtime stamps (start, after prologue, after K loop, end)
-__device__ unsigned long long g_stamps[65536 * 4];
+__device__ unsigned long long g_stamps[65536 * 8];
 #define STAMP(k)                                                                      \
   do {                                                                                \
     if (threadIdx.x == 0 && blockIdx.x < 65536) {                                     \
       unsigned long long t;                                                           \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");      \
-      g_stamps[blockIdx.x * 4 + (k)] = t;                                             \
+      g_stamps[blockIdx.x * 8 + (k)] = t;                                             \
     }                                                                                 \
   } while (0)
 #else
@@ -127,6 +127,11 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   const int lane = threadIdx.x & 63;
   const int frow = lane & 15;
   const int fq = lane >> 4;
+  // bias depends on the column only: load it once, all loads in flight together
+  float4 bias4[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j)
+    bias4[j] = p.bias ? *reinterpret_cast<const float4*>(p.bias + ncol0 + j * 16 + fq * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
   // phase 1
 #pragma unroll
   for (int ii = 0; ii < ni; ++ii) {
@@ -137,11 +142,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
       const int n = ncol0 + j * 16 + fq * 4;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.bias) {
-        const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-      }
+      float v[4] = {acc[i][j][0] + bias4[j].x, acc[i][j][1] + bias4[j].y, acc[i][j][2] + bias4[j].z,
+                    acc[i][j][3] + bias4[j].w};
       if (p.rbias) {
         const float4 bb = *reinterpret_cast<const float4*>(p.rbias + (int64_t)(mc / p.rb_g) * p.N + n);
         v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
@@ -164,6 +166,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (i0 == 0) STAMP(4);
   // phase 2: lanes per row = TN/8, rows per pass = 64 / (TN/8)
   constexpr int LPR = TN / 8;
   constexpr int RPP = 64 / LPR;
@@ -232,6 +235,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   }
 }
 
+static int group_m_for(int tiles_m);
+
 // Epilogue for one lane: out[m][n..n+3] = epi(v[0..3]).
 __device__ __forceinline__ void epilogue4(const Args& p, int m, int n, float v[4]) {
   int orow = 0;
@@ -297,21 +302,29 @@ __device__ __forceinline__ void epilogue4(const Args& p, int m, int n, float v[4
   }
 }
 
-// BM x BN x 64 tile, WM x WN waves (64*WM*WN threads), LDS double buffer.
-template <int BM, int BN, int WM, int WN, bool CONV, bool RELU_A>
+// BM x BN x KB tile, WM x WN waves (64*WM*WN threads), LDS double buffer.
+// KB = 64: 128-B LDS rows (swizzle chunk ^ (row & 7)); KB = 32: 64-B rows (swizzle
+// chunk ^ ((row >> 1) & 3)), half the LDS per block so 4-5 blocks share a CU and
+// cover each other's load latency and epilogues.
+template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM;            // activation rows per wave
   constexpr int TN = BN / WN;            // output columns per wave
   constexpr int RM = TM / 16;
   constexpr int RN = TN / 16;
-  constexpr int A_LOADS = BM / (8 * NW); // glds wave-instructions per wave per tile (8 rows each)
-  constexpr int W_LOADS = BN / (8 * NW);
-  constexpr int A_BYTES = BM * BK * 2;
-  constexpr int W_BYTES = BN * BK * 2;
+  constexpr int ROWB = KB * 2;           // LDS bytes per row
+  constexpr int CPR = KB / 8;            // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;          // rows per glds wave-instruction
+  constexpr int A_LOADS = BM / (RPI * NW);
+  constexpr int W_LOADS = BN / (RPI * NW);
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int W_BYTES = BN * ROWB;
   constexpr int STAGE = A_BYTES + W_BYTES;
+  constexpr int SUB = KB / 32;           // MFMA k-substeps per stage
   static_assert(RM >= 1 && RN >= 1, "tile too small");
-  static_assert(A_LOADS >= 1 && W_LOADS >= 1 && A_LOADS * 8 * NW == BM && W_LOADS * 8 * NW == BN, "load split");
+  static_assert(A_LOADS >= 1 && W_LOADS >= 1 && A_LOADS * RPI * NW == BM && W_LOADS * RPI * NW == BN, "load split");
+  static_assert(KB == 32 || KB == 64, "KB");
 
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
@@ -319,6 +332,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   const int wid = threadIdx.x >> 6;
   const int wm = wid / WN;
   const int wn = wid % WN;
+  auto swz = [](int row) { return KB == 64 ? (row & 7) : ((row >> 1) & 3); };
 
   int tm, tn;
   tile_coords(p, blockIdx.x, tm, tn);
@@ -326,35 +340,35 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   const int n0 = tn * BN;
 
   // ---- per-lane source rows for the A and W glds streams
-  const int lrow = lane >> 3;          // row inside an 8-row glds slab
-  const int pchunk = lane & 7;         // physical 16-B chunk this lane fills
+  const int lrow = lane / CPR;         // row inside an RPI-row glds slab
+  const int pchunk = lane % CPR;       // physical 16-B chunk this lane fills
   const bf16_t* a_src[A_LOADS];
-  int cy[A_LOADS], cx[A_LOADS];
+  int cpix[A_LOADS], cyx[A_LOADS];
 #pragma unroll
   for (int j = 0; j < A_LOADS; ++j) {
-    const int row = (wid * A_LOADS + j) * 8 + lrow;
-    const int lchunk = pchunk ^ (row & 7);
+    const int row = (wid * A_LOADS + j) * RPI + lrow;
+    const int lchunk = pchunk ^ swz(row);
     int m = m0 + row;
     if (m > p.M - 1) m = p.M - 1;
     if (!CONV) {
       a_src[j] = p.A + (int64_t)remap(m, p.a_g, p.a_gs, p.a_o) * p.lda + lchunk * 8;
-      cy[j] = cx[j] = 0;
+      cpix[j] = cyx[j] = 0;
     } else {
       const int hw = p.coh * p.cow;
       const int b = m / hw;
       const int rem = m - b * hw;
       const int oy = rem / p.cow;
       const int ox = rem - oy * p.cow;
-      cy[j] = oy * p.cs - p.cp;
-      cx[j] = ox * p.cs - p.cp;
-      a_src[j] = p.A + (int64_t)b * p.ch * p.cw * p.cc + lchunk * 8;
+      cpix[j] = b * p.ch * p.cw;
+      cyx[j] = ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff);
+      a_src[j] = p.A + lchunk * 8;
     }
   }
   const bf16_t* w_src[W_LOADS];
 #pragma unroll
   for (int j = 0; j < W_LOADS; ++j) {
-    const int row = (wid * W_LOADS + j) * 8 + lrow;
-    const int lchunk = pchunk ^ (row & 7);
+    const int row = (wid * W_LOADS + j) * RPI + lrow;
+    const int lchunk = pchunk ^ swz(row);
     w_src[j] = p.W + (int64_t)(n0 + row) * p.ldw + lchunk * 8;
   }
 
@@ -363,7 +377,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
     uint8_t* sW = sA + A_BYTES;
     if (!CONV) {
 #pragma unroll
-      for (int j = 0; j < A_LOADS; ++j) glds16(a_src[j] + k0, sA + (wid * A_LOADS + j) * 8 * 128);
+      for (int j = 0; j < A_LOADS; ++j) glds16(a_src[j] + k0, sA + (wid * A_LOADS + j) * RPI * ROWB);
     } else {
       const int kk = k0 / p.cc;
       const int ky = kk / p.ck;
@@ -371,15 +385,15 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
       const int ci0 = k0 - kk * p.cc;
 #pragma unroll
       for (int j = 0; j < A_LOADS; ++j) {
-        const int yi = cy[j] + ky, xi = cx[j] + kx;
+        const int yi = (cyx[j] >> 16) + ky, xi = ((int)(short)(cyx[j] & 0xffff)) + kx;
         const bool ok = yi >= 0 && yi < p.ch && xi >= 0 && xi < p.cw;
-        const void* src = ok ? (const void*)(a_src[j] + ((int64_t)yi * p.cw + xi) * p.cc + ci0)
+        const void* src = ok ? (const void*)(a_src[j] + ((int64_t)cpix[j] + (int64_t)yi * p.cw + xi) * p.cc + ci0)
                              : (const void*)(g_zero + pchunk * 16);
-        glds16(src, sA + (wid * A_LOADS + j) * 8 * 128);
+        glds16(src, sA + (wid * A_LOADS + j) * RPI * ROWB);
       }
     }
 #pragma unroll
-    for (int j = 0; j < W_LOADS; ++j) glds16(w_src[j] + k0, sW + (wid * W_LOADS + j) * 8 * 128);
+    for (int j = 0; j < W_LOADS; ++j) glds16(w_src[j] + k0, sW + (wid * W_LOADS + j) * RPI * ROWB);
   };
 
   f32x4 acc[RM][RN];
@@ -389,7 +403,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   STAMP(0);
-  const int nk = p.K / BK;
+  const int nk = p.K / KB;
   stage(0, 0);
   __syncthreads();   // waits vmcnt(0): tile 0 landed
   STAMP(1);
@@ -398,22 +412,22 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   const int fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * KB);
     const uint8_t* sA = smem + cur * STAGE;
     const uint8_t* sW = sA + A_BYTES;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < SUB; ++s) {
       bf16x8 wf[RN];
       const int lchunk = 4 * s + fq;
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int row = wn * TN + j * 16 + frow;
-        wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * 128 + ((lchunk ^ (row & 7)) << 4));
+        wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * ROWB + ((lchunk ^ swz(row)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int row = wm * TM + i * 16 + frow;
-        bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + row * 128 + ((lchunk ^ (row & 7)) << 4));
+        bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((lchunk ^ swz(row)) << 4));
         if (RELU_A) af = relu8(af);
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
@@ -434,6 +448,22 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
     __builtin_amdgcn_wave_barrier();
   }
   STAMP(3);
+}
+
+template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>
+static void launch(const Args& p, hipStream_t s) {
+  Args q = p;
+  q.tiles_m = (p.M + BM - 1) / BM;
+  q.tiles_n = p.N / BN;
+  q.group_m = group_m_for(q.tiles_m);
+  const int smem = 2 * (BM + BN) * KB * 2;
+  auto kern = k_gemm<BM, BN, WM, WN, KB, CONV, RELU_A>;
+  static bool attr = false;
+  if (!attr && smem > 64 * 1024) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(q.tiles_m * q.tiles_n), dim3(64 * WM * WN), smem, s, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -818,38 +848,24 @@ static void launch8(const Args& p, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(q.tiles_m * q.tiles_n), dim3(512), smem, s, q);
 }
 
-template <int BM, int BN, int WM, int WN, bool CONV, bool RELU_A>
-static void launch(const Args& p, hipStream_t s) {
-  Args q = p;
-  q.tiles_m = (p.M + BM - 1) / BM;
-  q.tiles_n = p.N / BN;
-  q.group_m = group_m_for(q.tiles_m);
-  const int smem = 2 * (BM + BN) * BK * 2;
-  auto kern = k_gemm<BM, BN, WM, WN, CONV, RELU_A>;
-  static bool attr = false;
-  if (!attr && smem > 64 * 1024) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(q.tiles_m * q.tiles_n), dim3(64 * WM * WN), smem, s, q);
-}
 
 template <bool CONV, bool RELU_A>
 static int dispatch(const Args& p, hipStream_t s) {
-  // 256x256 (8 waves, 128 KiB LDS) when the grid still fills the chip; else 128-row tiles.
   const int64_t t256 = (int64_t)((p.M + 255) / 256) * (p.N / 256);
   const int64_t t128 = (int64_t)((p.M + 127) / 128) * (p.N / 128);
   static const int force = [] { const char* e = getenv("I2PC_GEMM_TILE"); return e ? atoi(e) : 0; }();
   const bool even_k = (p.K / BK) % 2 == 0;
   const bool big_ok = p.N % 256 == 0 && even_k && (CONV || p.a_g == 0);
   if (force == 8 && big_ok) launch8<CONV, RELU_A>(p, s);
-  else if (force == 4 && p.N % 256 == 0 && p.K % 32 == 0) launch_ring<CONV, RELU_A>(p, s);
-  else if (force == 256 && p.N % 256 == 0) launch<256, 256, 2, 4, CONV, RELU_A>(p, s);
-  else if (force == 128 && p.N % 128 == 0) launch<128, 128, 2, 2, CONV, RELU_A>(p, s);
-  else if (p.N % 256 == 0 && t256 >= 512) launch<256, 256, 2, 4, CONV, RELU_A>(p, s);
-  else if (p.N % 128 == 0 && t128 >= 512) launch<128, 128, 2, 2, CONV, RELU_A>(p, s);
-  else if (p.N % 64 == 0) launch<128, 64, 2, 2, CONV, RELU_A>(p, s);
-  else if (p.N % 32 == 0) launch<128, 32, 4, 1, CONV, RELU_A>(p, s);
+  else if (force == 4 && p.N % 256 == 0) launch_ring<CONV, RELU_A>(p, s);
+  else if (force == 256 && p.N % 256 == 0) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
+  else if (force == 25632 && p.N % 256 == 0) launch<256, 256, 2, 4, 32, CONV, RELU_A>(p, s);
+  else if (force == 128 && p.N % 128 == 0) launch<128, 128, 2, 2, 64, CONV, RELU_A>(p, s);
+  else if (force == 12832 && p.N % 128 == 0) launch<128, 128, 2, 2, 32, CONV, RELU_A>(p, s);
+  else if (p.N % 256 == 0 && t256 >= 512) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
+  else if (p.N % 128 == 0 && t128 >= 512) launch<128, 128, 2, 2, 64, CONV, RELU_A>(p, s);
+  else if (p.N % 64 == 0) launch<128, 64, 2, 2, 64, CONV, RELU_A>(p, s);
+  else if (p.N % 32 == 0) launch<128, 32, 4, 1, 64, CONV, RELU_A>(p, s);
   else return set_error(I2PC_EUNSUPPORTED, "gemm: N=%d must be a multiple of 32", p.N);
   return check_launch("gemm");
 }

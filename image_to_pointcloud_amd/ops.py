@@ -110,10 +110,11 @@ def gemm_kernel_label(desc: GemmDesc) -> str:
     t256 = ((M + 255) // 256) * (N // 256)
     t128 = ((M + 127) // 128) * (N // 128)
     force = int(os.environ.get("I2PC_GEMM_TILE", "0") or 0)
-    if force == 256 and N % 256 == 0:
-        bm, bn = 256, 256
-    elif force == 128 and N % 128 == 0:
-        bm, bn = 128, 128
+    kb = 64
+    if force in (256, 25632) and N % 256 == 0:
+        bm, bn, kb = 256, 256, (64 if force == 256 else 32)
+    elif force in (128, 12832) and N % 128 == 0:
+        bm, bn, kb = 128, 128, (64 if force == 128 else 32)
     elif N % 256 == 0 and t256 >= 512:
         bm, bn = 256, 256
     elif N % 128 == 0 and t128 >= 512:
@@ -125,7 +126,7 @@ def gemm_kernel_label(desc: GemmDesc) -> str:
     wm, wn = {(256, 256): (2, 4), (128, 128): (2, 2), (128, 64): (2, 2), (128, 32): (4, 1)}[(bm, bn)]
     conv = "true" if desc.conv else "false"
     relu = "true" if desc.conv_relu_in else "false"
-    return f"k_gemm<{bm}, {bn}, {wm}, {wn}, {conv}, {relu}>"
+    return f"k_gemm<{bm}, {bn}, {wm}, {wn}, {kb}, {conv}, {relu}>"
 
 
 def gemm(desc: GemmDesc) -> None:
