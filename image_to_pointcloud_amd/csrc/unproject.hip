@@ -36,6 +36,7 @@ namespace unproj {
 constexpr int kSlots = 4;
 constexpr int kBins = 2048;
 constexpr int kBlock = 256;
+constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
 
 enum Phase : uint32_t { PH_INIT = 0, PH_PCT = 1, PH_MED = 2, PH_PCT2_INIT = 3, PH_PCT2 = 4, PH_DONE = 5 };
 
@@ -148,7 +149,7 @@ __device__ __forceinline__ void agg_add(uint32_t* h, int bin, bool active) {
   uint64_t pending = __ballot(active);
   for (int it = 0; it < 4 && pending; ++it) {
     const int leader = __ffsll((unsigned long long)pending) - 1;
-    const int lbin = __shfl(bin, leader);
+    const int lbin = __builtin_amdgcn_readlane(bin, leader);   // SALU broadcast, no LDS round trip
     const uint64_t same = __ballot(active && bin == lbin) & pending;
     if (lane == leader) atomicAdd(&h[lbin], (uint32_t)__popcll(same));
     pending &= ~same;
@@ -219,12 +220,54 @@ __device__ __forceinline__ bool hist_gate(uint32_t phase, int level) {
   return level == 0 ? phase == PH_PCT2_INIT : phase == PH_PCT2;
 }
 
+// Row-blocked sweep geometry: a workgroup owns image b and output rows [v0, v1);
+// the model-resolution rows feeding them are staged once into LDS, every thread
+// owns 4 consecutive columns (+1024 per chunk), the row taps are wave-uniform.
+struct Sweep {
+  int R;         // output rows per workgroup
+  int nrb;       // row blocks per image
+  int lds_rows;  // capacity of the LDS row window (0: sample from global)
+};
+
+__device__ __forceinline__ void map_rows(int bid, int B, int nrb, int& b, int& rb) { map_block(bid, B, nrb, b, rb); }
+
+// Stage model rows [yt[v0].i0, yt[v1-1].i1] of image b into LDS; returns the first row.
+__device__ __forceinline__ int stage_rows(const Geo& g, int b, int v0, int v1, float* rows, int cap) {
+  if (g.same || cap == 0) return 0;
+  const int lo = g.yt[v0].i0;
+  const int hi = g.yt[v1 - 1].i1;
+  const int n = (hi - lo + 1) * g.dw;
+  const float* src = g.depth + ((size_t)b * g.dh + lo) * g.dw;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) rows[i] = src[i];
+  return lo;
+}
+
+__device__ __forceinline__ float sample_rows(const Geo& g, const float* rows, int lo, bool use_lds, int b,
+                                             const Tap& ty, int v, int u) {
+  if (g.same) return g.depth[((size_t)b * g.dh + v) * g.dw + u];
+  if (!use_lds) return sample(g, b, v, u);
+  const Tap tx = g.xt[u];
+  const float* r0 = rows + (ty.i0 - lo) * g.dw;
+  const float* r1 = rows + (ty.i1 - lo) * g.dw;
+  float h0, h1;
+  if (tx.i1 < 0) {
+    h0 = r0[tx.i0];
+    h1 = r1[tx.i0];
+  } else {
+    h0 = r0[tx.i0] * tx.w0 + r0[tx.i1] * tx.w1;
+    h1 = r1[tx.i0] * tx.w0 + r1[tx.i1] * tx.w1;
+  }
+  return h0 * ty.w0 + h1 * ty.w1;
+}
+
 template <int LEVEL, int PASS>
-__global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32_t* hist, int B, int G) {
-  __shared__ uint32_t sh[kSlots * kBins];
+__global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32_t* hist, int B, Sweep sw) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
+  uint32_t* sh = smem_u;                                        // [kSlots * kBins]
+  float* rows = reinterpret_cast<float*>(smem_u + kSlots * kBins);
   __shared__ uint32_t red[4][4];
-  int b, chunk;
-  map_block(blockIdx.x, B, G, b, chunk);
+  int b, rb;
+  map_rows(blockIdx.x, B, sw.nrb, b, rb);
   SelState* S = st + b;
   const uint32_t phase = S->phase;
   if (!hist_gate<PASS>(phase, LEVEL)) return;
@@ -232,47 +275,70 @@ __global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32
   const int nslot = LEVEL == 0 ? 1 : (int)S->nslot;
   uint32_t sp[kSlots];
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s) sp[s] = S->slot_prefix[s];
+  for (int q = 0; q < kSlots; ++q) sp[q] = S->slot_prefix[q];
   const bool sanitize = PASS == 1;
   const float med = S->med;
   constexpr int match_shift = LEVEL == 1 ? 21 : 10;
   constexpr int bin_shift = LEVEL == 0 ? 21 : (LEVEL == 1 ? 10 : 0);
   constexpr uint32_t bin_mask = LEVEL == 2 ? 1023u : 2047u;
 
+  const int v0 = rb * sw.R;
+  const int v1 = min(g.H, v0 + sw.R);
   for (int i = threadIdx.x; i < nslot * kBins; i += kBlock) sh[i] = 0;
+  const int lo = stage_rows(g, b, v0, v1, rows, sw.lds_rows);
+  const bool use_lds = sw.lds_rows > 0;
   __syncthreads();
 
-  const int n = g.H * g.W;
-  const int per = (n + G - 1) / G;
-  const int start = chunk * per;
-  const int end = min(n, start + per);
   uint32_t nan_c = 0, nonfin_c = 0, kmin = 0xffffffffu, kmax = 0u;
-  for (int base = start; base < end; base += kBlock) {
-    const int p = base + threadIdx.x;
-    bool active = p < end;
-    float val = 0.f;
-    if (active) {
-      const int v = p / g.W;
-      const int u = p - v * g.W;
-      val = sample(g, b, v, u);
-      if (sanitize && !isfinite(val)) val = med;
-    }
-    if (LEVEL == 0 && active && !isfinite(val)) ++nonfin_c;   // NaN and +-Inf
-    if (active && isnan(val)) { ++nan_c; active = false; }
-    const uint32_t key = f2key(val);
-    int bin = 0;
-    if (LEVEL == 0) {
-      if (active) { kmin = min(kmin, key); kmax = max(kmax, key); }
-      bin = (int)((key >> bin_shift) & bin_mask);
-    } else {
-      bool hit = false;
+  // thread columns u = cb + j*256 + tid: neighbouring lanes read neighbouring LDS words
+  for (int cb = 0; cb < g.W; cb += 4 * kBlock) {
+    Tap tx[4];
+    bool colok[4];
 #pragma unroll
-      for (int s = 0; s < kSlots; ++s) {
-        if (s < nslot && (key >> match_shift) == sp[s]) { hit = true; bin = s * kBins + (int)((key >> bin_shift) & bin_mask); }
-      }
-      active = active && hit;
+    for (int j = 0; j < 4; ++j) {
+      const int u = cb + j * kBlock + threadIdx.x;
+      colok[j] = u < g.W;
+      tx[j] = g.xt[min(u, g.W - 1)];      // unconditional (clamped) load: no divergent waits
     }
-    agg_add(sh, bin, active);
+    for (int v = v0; v < v1; ++v) {
+      const Tap ty = g.same ? Tap{0, 0, 1.f, 0.f} : g.yt[v];
+      const float* r0 = use_lds ? rows + (ty.i0 - lo) * g.dw : g.depth + ((size_t)b * g.dh + ty.i0) * g.dw;
+      const float* r1 = use_lds ? rows + (ty.i1 - lo) * g.dw : g.depth + ((size_t)b * g.dh + ty.i1) * g.dw;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = min(cb + j * kBlock + threadIdx.x, g.W - 1);
+        bool active = colok[j];
+        float val;
+        if (g.same) {
+          val = g.depth[((size_t)b * g.dh + v) * g.dw + u];
+        } else {
+          // single-tap columns (i1 < 0) use weights (1, 0) on a duplicated index: identical
+          // value except for Inf/NaN neighbours, so keep the exact expression via select
+          const int i1 = tx[j].i1 < 0 ? tx[j].i0 : tx[j].i1;
+          const float a0 = r0[tx[j].i0], a1 = r0[i1], c0 = r1[tx[j].i0], c1 = r1[i1];
+          const float h0 = tx[j].i1 < 0 ? a0 : a0 * tx[j].w0 + a1 * tx[j].w1;
+          const float h1 = tx[j].i1 < 0 ? c0 : c0 * tx[j].w0 + c1 * tx[j].w1;
+          val = h0 * ty.w0 + h1 * ty.w1;
+        }
+        if (sanitize && !isfinite(val)) val = med;
+        if (LEVEL == 0 && active && !isfinite(val)) ++nonfin_c;   // NaN and +-Inf
+        if (active && isnan(val)) { ++nan_c; active = false; }
+        const uint32_t key = f2key(val);
+        int bin = 0;
+        if (LEVEL == 0) {
+          if (active) { kmin = min(kmin, key); kmax = max(kmax, key); }
+          bin = (int)((key >> bin_shift) & bin_mask);
+        } else {
+          bool hit = false;
+#pragma unroll
+          for (int q = 0; q < kSlots; ++q) {
+            if (q < nslot && (key >> match_shift) == sp[q]) { hit = true; bin = q * kBins + (int)((key >> bin_shift) & bin_mask); }
+          }
+          active = active && hit;
+        }
+        agg_add(sh, bin, active);
+      }
+    }
   }
   if (LEVEL == 0) {
     const int wid = threadIdx.x >> 6;
@@ -518,79 +584,137 @@ __device__ __forceinline__ void project(double d, int v, int u, const Cam& c, fl
   z = (float)zd;
 }
 
+// Row-blocked unprojection: workgroup = image b x output point rows [r0, r1);
+// thread = 4 consecutive points of a row (+1024 per column chunk).  Model rows
+// staged in LDS (shared with the select sweeps' geometry); RGB of 4 pixels read
+// as 12 contiguous bytes when step == 1; xyz stored as 3 x 16 B and rgb as
+// 3 x 4 B per thread (a wave writes 3 KiB + 768 B contiguous).
 template <bool kField>
 __global__ __launch_bounds__(kBlock) void k_unproject(Geo g, const SelState* st, const double* field,
-                                                      const uint8_t* img, int C, int B, int G, int invert,
+                                                      const uint8_t* img, int C, int B, Sweep sw, int invert,
                                                       Cam cam, float* xyz, uint8_t* rgb, SelState* stw) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
+  float* rows = reinterpret_cast<float*>(smem_u);
   __shared__ uint32_t red[6][4];
-  int b, chunk;
-  map_block(blockIdx.x, B, G, b, chunk);
+  int b, rb;
+  map_rows(blockIdx.x, B, sw.nrb, b, rb);
   const SelState* S = st + b;
   const Norm nm = load_norm(S, invert);
   const bool fill = S->has_med != 0;
   const float med = S->med;
-  const int N = cam.N;
-  const int per = ((N + G - 1) / G + 3) & ~3;
-  const int start = chunk * per;
-  const int end = min(N, start + per);
-  const bool vec_ok = (N & 3) == 0;
+  const int Hn = cam.N / cam.Wn;
+  const int r0 = rb * sw.R;
+  const int r1 = min(Hn, r0 + sw.R);
+  const int step = cam.step;
+  const bool use_lds = !kField && sw.lds_rows > 0;
+  int lo = 0;
+  if (!kField) lo = stage_rows(g, b, r0 * step, (r1 - 1) * step + 1, rows, sw.lds_rows);
+  __syncthreads();
+  const bool vec_ok = (cam.N & 3) == 0 && (cam.Wn & 3) == 0;
+  const bool rgb_vec = step == 1 && C == 3 && (g.W & 3) == 0;
   const size_t img_base = (size_t)b * g.H * g.W;
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  bool any = false;
-  for (int i0 = start + 4 * threadIdx.x; i0 < end; i0 += 4 * kBlock) {
-    float px[4][3];
-    uint8_t pc[4][3];
-    int cnt = min(4, end - i0);
-    for (int j = 0; j < 4; ++j) {
-      if (j >= cnt) break;
-      const int i = i0 + j;
-      const int row = i / cam.Wn;
-      const int col = i - row * cam.Wn;
-      const int v = row * cam.step;
-      const int u = col * cam.step;
-      double d;
-      if (kField) {
-        d = field[img_base + (size_t)v * g.W + u];
-      } else {
-        float val = sample(g, b, v, u);
-        if (fill && !isfinite(val)) val = med;
-        d = normalize(val, nm);
-      }
-      project(d, v, u, cam, px[j][0], px[j][1], px[j][2]);
-      if (C >= 3) {
-        const uint8_t* p = img + ((img_base + (size_t)v * g.W + u) * C);
-        pc[j][0] = p[2];
-        pc[j][1] = p[1];
-        pc[j][2] = p[0];
-      } else {
-        pc[j][0] = pc[j][1] = pc[j][2] = 128;
-      }
-      for (int k = 0; k < 3; ++k) { mn[k] = fminf(mn[k], px[j][k]); mx[k] = fmaxf(mx[k], px[j][k]); }
-      any = true;
-    }
-    const size_t o = (size_t)b * N + i0;
-    if (vec_ok && cnt == 4) {
-      float4* dst = reinterpret_cast<float4*>(xyz + o * 3);
-      dst[0] = make_float4(px[0][0], px[0][1], px[0][2], px[1][0]);
-      dst[1] = make_float4(px[1][1], px[1][2], px[2][0], px[2][1]);
-      dst[2] = make_float4(px[2][2], px[3][0], px[3][1], px[3][2]);
-      uint32_t w0 = pc[0][0] | (pc[0][1] << 8) | (pc[0][2] << 16) | ((uint32_t)pc[1][0] << 24);
-      uint32_t w1 = pc[1][1] | (pc[1][2] << 8) | (pc[2][0] << 16) | ((uint32_t)pc[2][1] << 24);
-      uint32_t w2 = pc[2][2] | (pc[3][0] << 8) | (pc[3][1] << 16) | ((uint32_t)pc[3][2] << 24);
-      uint32_t* cd = reinterpret_cast<uint32_t*>(rgb + o * 3);
-      cd[0] = w0; cd[1] = w1; cd[2] = w2;
-    } else {
-      for (int j = 0; j < cnt; ++j) {
-        for (int k = 0; k < 3; ++k) {
-          xyz[(o + j) * 3 + k] = px[j][k];
-          rgb[(o + j) * 3 + k] = pc[j][k];
+  for (int cb = 0; cb < cam.Wn; cb += 4 * kBlock) {
+    const int ui0 = cb + threadIdx.x * 4;
+    const int cnt = min(4, cam.Wn - ui0);
+    if (cnt <= 0) continue;
+    // column taps once per chunk
+    Tap tx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tx[j] = (!g.same && !kField && j < cnt) ? g.xt[(ui0 + j) * step] : Tap{0, -1, 1.f, 0.f};
+    // prefetch the RGB of every row of the block (HBM latency overlaps the whole row loop)
+    uint32_t q[kMaxRows][3];
+    const bool rgbv = rgb_vec && cnt == 4;
+    if (rgbv) {
+#pragma unroll
+      for (int k = 0; k < kMaxRows; ++k) {
+        if (r0 + k < r1) {
+          const uint32_t* p32 = reinterpret_cast<const uint32_t*>(img + (img_base + (size_t)(r0 + k) * g.W + ui0) * 3);
+          q[k][0] = p32[0]; q[k][1] = p32[1]; q[k][2] = p32[2];
         }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxRows; ++k) {
+      const int ri = r0 + k;
+      if (ri >= r1) break;
+      const int v = ri * step;
+      const Tap ty = g.same ? Tap{0, 0, 1.f, 0.f} : g.yt[v];
+      float px[4][3];
+      uint8_t pc[4][3];
+      if (rgbv) {
+        const uint32_t w0 = q[k][0], w1 = q[k][1], w2 = q[k][2];
+        const uint8_t bytes[12] = {(uint8_t)w0, (uint8_t)(w0 >> 8), (uint8_t)(w0 >> 16), (uint8_t)(w0 >> 24),
+                                   (uint8_t)w1, (uint8_t)(w1 >> 8), (uint8_t)(w1 >> 16), (uint8_t)(w1 >> 24),
+                                   (uint8_t)w2, (uint8_t)(w2 >> 8), (uint8_t)(w2 >> 16), (uint8_t)(w2 >> 24)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { pc[j][0] = bytes[3 * j + 2]; pc[j][1] = bytes[3 * j + 1]; pc[j][2] = bytes[3 * j]; }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int u = (ui0 + (j < cnt ? j : 0)) * step;
+          if (C >= 3) {
+            const uint8_t* qq = img + (img_base + (size_t)v * g.W + u) * C;
+            pc[j][0] = qq[2]; pc[j][1] = qq[1]; pc[j][2] = qq[0];
+          } else {
+            pc[j][0] = pc[j][1] = pc[j][2] = 128;
+          }
+        }
+      }
+      const float* rr0 = use_lds ? rows + (ty.i0 - lo) * g.dw : g.depth + ((size_t)b * g.dh + ty.i0) * g.dw;
+      const float* rr1 = use_lds ? rows + (ty.i1 - lo) * g.dw : g.depth + ((size_t)b * g.dh + ty.i1) * g.dw;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < cnt) {
+          const int u = (ui0 + j) * step;
+          double d;
+          if (kField) {
+            d = field[img_base + (size_t)v * g.W + u];
+          } else {
+            float val;
+            if (g.same) {
+              val = g.depth[((size_t)b * g.dh + v) * g.dw + u];
+            } else if (tx[j].i1 < 0) {
+              val = rr0[tx[j].i0] * ty.w0 + rr1[tx[j].i0] * ty.w1;
+            } else {
+              const float h0 = rr0[tx[j].i0] * tx[j].w0 + rr0[tx[j].i1] * tx[j].w1;
+              const float h1 = rr1[tx[j].i0] * tx[j].w0 + rr1[tx[j].i1] * tx[j].w1;
+              val = h0 * ty.w0 + h1 * ty.w1;
+            }
+            if (fill && !isfinite(val)) val = med;
+            d = normalize(val, nm);
+          }
+          project(d, v, u, cam, px[j][0], px[j][1], px[j][2]);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) { mn[c] = fminf(mn[c], px[j][c]); mx[c] = fmaxf(mx[c], px[j][c]); }
+        }
+      }
+      const size_t o = (size_t)b * cam.N + (size_t)ri * cam.Wn + ui0;
+      if (vec_ok && cnt == 4) {
+        float4* dst = reinterpret_cast<float4*>(xyz + o * 3);
+        dst[0] = make_float4(px[0][0], px[0][1], px[0][2], px[1][0]);
+        dst[1] = make_float4(px[1][1], px[1][2], px[2][0], px[2][1]);
+        dst[2] = make_float4(px[2][2], px[3][0], px[3][1], px[3][2]);
+        uint32_t* cd = reinterpret_cast<uint32_t*>(rgb + o * 3);
+        cd[0] = pc[0][0] | (pc[0][1] << 8) | (pc[0][2] << 16) | (pc[1][0] << 24);
+        cd[1] = pc[1][1] | (pc[1][2] << 8) | (pc[2][0] << 16) | (pc[2][1] << 24);
+        cd[2] = pc[2][2] | (pc[3][0] << 8) | (pc[3][1] << 16) | (pc[3][2] << 24);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < cnt)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              xyz[(o + j) * 3 + c] = px[j][c];
+              rgb[(o + j) * 3 + c] = pc[j][c];
+            }
       }
     }
   }
   // per-image bbox: wave reduce -> LDS -> one atomic per block and component
   uint32_t kk[6];
   for (int k = 0; k < 3; ++k) {
+    const bool any = mn[k] <= mx[k];
     kk[2 * k] = any ? f2key(mn[k]) : 0xffffffffu;
     kk[2 * k + 1] = any ? f2key(mx[k]) : 0u;
   }
@@ -606,6 +730,152 @@ __global__ __launch_bounds__(kBlock) void k_unproject(Geo g, const SelState* st,
     for (int w = 1; w < kBlock / 64; ++w) x = (k & 1) ? max(x, red[k][w]) : min(x, red[k][w]);
     uint32_t* dst = &stw[b].bbox_key[k];
     if (k & 1) { if (x) atomicMax(dst, x); }
+    else { if (x != 0xffffffffu) atomicMin(dst, x); }
+  }
+}
+
+__device__ __forceinline__ Tap xtap(const Geo& g, int u) {
+  Tap t = make_tap(u, g.dw, g.W);
+  if (g.dw == 1) { t.i0 = 0; t.i1 = -1; t.w0 = 1.f; t.w1 = 0.f; }
+  return t;
+}
+__device__ __forceinline__ Tap ytap(const Geo& g, int v) {
+  Tap t = make_tap(v, g.dh, g.H);
+  if (t.i1 < 0) t.i1 = t.i0;
+  return t;
+}
+
+// Fast unprojection (no smoothing, N % 4 == 0, ceil(W/step) % 4 == 0, 3 channels):
+// every load is unconditional (indices clamped, only the stores are predicated) so
+// the compiler never parks a wave on a divergent vmcnt(0); the RGB of both point
+// groups a thread owns is in flight before any arithmetic; cv2 taps are recomputed
+// in registers (no table loads).
+constexpr int kGroupsPerThread = 2;
+template <int STEP>
+__global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState* st, const uint8_t* img, int B,
+                                                           Sweep sw, int invert, Cam cam, float* xyz, uint8_t* rgb,
+                                                           SelState* stw) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
+  float* rows = reinterpret_cast<float*>(smem_u);
+  __shared__ uint32_t red[6][4];
+  int b, rb;
+  map_rows(blockIdx.x, B, sw.nrb, b, rb);
+  const SelState* S = st + b;
+  const Norm nm = load_norm(S, invert);
+  const bool fill = S->has_med != 0;
+  const float med = S->med;
+  const int Hn = cam.N / cam.Wn;
+  const int r0 = rb * sw.R;
+  const int r1 = min(Hn, r0 + sw.R);
+  const bool use_lds = sw.lds_rows > 0 && !g.same;
+  int lo = 0;
+  if (use_lds) {
+    lo = ytap(g, r0 * STEP).i0;
+    const int hi = ytap(g, (r1 - 1) * STEP).i1;
+    const int n = (hi - lo + 1) * g.dw;
+    const float* src = g.depth + ((size_t)b * g.dh + lo) * g.dw;
+    for (int i = threadIdx.x; i < n; i += kBlock) rows[i] = src[i];
+  }
+  __syncthreads();
+  const int Wn4 = cam.Wn >> 2;
+  const int G = (r1 - r0) * Wn4;
+  const size_t img_base = (size_t)b * g.H * g.W;
+  const float* dimg = g.depth + (size_t)b * g.dh * g.dw;
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int base = 0; base < G; base += kGroupsPerThread * kBlock) {
+    int row[kGroupsPerThread], ui0[kGroupsPerThread];
+    uint32_t q[kGroupsPerThread][4][3];
+#pragma unroll
+    for (int k = 0; k < kGroupsPerThread; ++k) {
+      const int gi = min(base + k * kBlock + (int)threadIdx.x, G - 1);
+      row[k] = r0 + gi / Wn4;
+      ui0[k] = (gi - (row[k] - r0) * Wn4) * 4;
+      const int v = row[k] * STEP;
+      if (STEP == 1) {
+        const uint32_t* p32 = reinterpret_cast<const uint32_t*>(img + (img_base + (size_t)v * g.W + ui0[k]) * 3);
+        q[k][0][0] = p32[0]; q[k][0][1] = p32[1]; q[k][0][2] = p32[2];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint8_t* px = img + (img_base + (size_t)v * g.W + (ui0[k] + j) * STEP) * 3;
+          q[k][j][0] = px[0]; q[k][j][1] = px[1]; q[k][j][2] = px[2];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kGroupsPerThread; ++k) {
+      const int gidx = base + k * kBlock + (int)threadIdx.x;
+      const int v = row[k] * STEP;
+      uint32_t pc[4][3];   // [point][r,g,b] (source is BGR)
+      if (STEP == 1) {
+        const uint32_t w[3] = {q[k][0][0], q[k][0][1], q[k][0][2]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int byte = 3 * j + (2 - c);
+            pc[j][c] = (w[byte >> 2] >> (8 * (byte & 3))) & 0xffu;
+          }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { pc[j][0] = q[k][j][2]; pc[j][1] = q[k][j][1]; pc[j][2] = q[k][j][0]; }
+      }
+      const Tap ty = ytap(g, v);
+      const float* rr0 = use_lds ? rows + (ty.i0 - lo) * g.dw : dimg + (size_t)ty.i0 * g.dw;
+      const float* rr1 = use_lds ? rows + (ty.i1 - lo) * g.dw : dimg + (size_t)ty.i1 * g.dw;
+      float px[4][3];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = (ui0[k] + j) * STEP;
+        float val;
+        if (g.same) {
+          val = dimg[(size_t)v * g.dw + u];
+        } else {
+          const Tap tx = xtap(g, u);
+          const int i1 = tx.i1 < 0 ? tx.i0 : tx.i1;
+          const float a0 = rr0[tx.i0], a1 = rr0[i1], c0 = rr1[tx.i0], c1 = rr1[i1];
+          const float h0 = tx.i1 < 0 ? a0 : a0 * tx.w0 + a1 * tx.w1;
+          const float h1 = tx.i1 < 0 ? c0 : c0 * tx.w0 + c1 * tx.w1;
+          val = h0 * ty.w0 + h1 * ty.w1;
+        }
+        if (fill && !isfinite(val)) val = med;
+        project(normalize(val, nm), v, u, cam, px[j][0], px[j][1], px[j][2]);
+      }
+      if (gidx < G) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) { mn[c] = fminf(mn[c], px[j][c]); mx[c] = fmaxf(mx[c], px[j][c]); }
+        const size_t o = (size_t)b * cam.N + (size_t)row[k] * cam.Wn + ui0[k];
+        float4* dst = reinterpret_cast<float4*>(xyz + o * 3);
+        dst[0] = make_float4(px[0][0], px[0][1], px[0][2], px[1][0]);
+        dst[1] = make_float4(px[1][1], px[1][2], px[2][0], px[2][1]);
+        dst[2] = make_float4(px[2][2], px[3][0], px[3][1], px[3][2]);
+        uint32_t* cd = reinterpret_cast<uint32_t*>(rgb + o * 3);
+        cd[0] = pc[0][0] | (pc[0][1] << 8) | (pc[0][2] << 16) | (pc[1][0] << 24);
+        cd[1] = pc[1][1] | (pc[1][2] << 8) | (pc[2][0] << 16) | (pc[2][1] << 24);
+        cd[2] = pc[2][2] | (pc[3][0] << 8) | (pc[3][1] << 16) | (pc[3][2] << 24);
+      }
+    }
+  }
+  uint32_t kk[6];
+  for (int c = 0; c < 3; ++c) {
+    const bool any = mn[c] <= mx[c];
+    kk[2 * c] = any ? f2key(mn[c]) : 0xffffffffu;
+    kk[2 * c + 1] = any ? f2key(mx[c]) : 0u;
+  }
+  const int wid = threadIdx.x >> 6;
+  for (int c = 0; c < 6; ++c) {
+    uint32_t x = (c & 1) ? wave_max_u32(kk[c]) : wave_min_u32(kk[c]);
+    if ((threadIdx.x & 63) == 0) red[c][wid] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int c = threadIdx.x;
+    uint32_t x = red[c][0];
+    for (int w = 1; w < kBlock / 64; ++w) x = (c & 1) ? max(x, red[c][w]) : min(x, red[c][w]);
+    uint32_t* dst = &stw[b].bbox_key[c];
+    if (c & 1) { if (x) atomicMax(dst, x); }
     else { if (x != 0xffffffffu) atomicMin(dst, x); }
   }
 }
@@ -688,14 +958,37 @@ __global__ void k_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n,
   }
 }
 
+constexpr int kRowBudget = 31 * 1024;   // LDS bytes for the staged model-row window (+32 KiB hist < 64 KiB)
+
+// Rows per workgroup so that the model-row window fits the LDS budget.
+static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same, int target_rows) {
+  Sweep sw{};
+  int cap_rows = same ? 0 : kRowBudget / (int)(sizeof(float) * dw);
+  int R = target_rows;
+  if (!same && cap_rows >= 3) {
+    // model rows spanned by R output rows (image rows (R-1)*step apart): <= (R-1)*step*dh/H + 3
+    while (R > 1 && (double)(R - 1) * step * dh / H + 3.0 > cap_rows) R /= 2;
+  } else {
+    cap_rows = 0;
+  }
+  sw.R = std::max(1, R);
+  sw.nrb = (rows_out + sw.R - 1) / sw.R;
+  sw.lds_rows = cap_rows;
+  return sw;
+}
+
+static size_t sweep_lds(const Sweep& sw, int dw) { return sw.lds_rows ? (size_t)sw.lds_rows * dw * sizeof(float) : 0; }
+
 template <int PASS>
-static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, int G, hipStream_t s) {
-  hipLaunchKernelGGL((k_sel_hist<0, PASS>), dim3(B * G), dim3(kBlock), 0, s, g, st, hist, B, G);
-  hipLaunchKernelGGL((k_sel_resolve<0, PASS>), dim3(B), dim3(kBlock), 0, s, st, hist, B);
-  hipLaunchKernelGGL((k_sel_hist<1, PASS>), dim3(B * G), dim3(kBlock), 0, s, g, st, hist, B, G);
-  hipLaunchKernelGGL((k_sel_resolve<1, PASS>), dim3(B), dim3(kBlock), 0, s, st, hist, B);
-  hipLaunchKernelGGL((k_sel_hist<2, PASS>), dim3(B * G), dim3(kBlock), 0, s, g, st, hist, B, G);
-  hipLaunchKernelGGL((k_sel_resolve<2, PASS>), dim3(B), dim3(kBlock), 0, s, st, hist, B);
+static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, const Sweep& sw, hipStream_t s) {
+  const size_t lds = sizeof(uint32_t) * kSlots * kBins + sweep_lds(sw, g.dw);
+  const dim3 grid(B * sw.nrb), block(kBlock);
+  hipLaunchKernelGGL((k_sel_hist<0, PASS>), grid, block, lds, s, g, st, hist, B, sw);
+  hipLaunchKernelGGL((k_sel_resolve<0, PASS>), dim3(B), block, 0, s, st, hist, B);
+  hipLaunchKernelGGL((k_sel_hist<1, PASS>), grid, block, lds, s, g, st, hist, B, sw);
+  hipLaunchKernelGGL((k_sel_resolve<1, PASS>), dim3(B), block, 0, s, st, hist, B);
+  hipLaunchKernelGGL((k_sel_hist<2, PASS>), grid, block, lds, s, g, st, hist, B, sw);
+  hipLaunchKernelGGL((k_sel_resolve<2, PASS>), dim3(B), block, 0, s, st, hist, B);
   return check_launch("select");
 }
 
@@ -742,12 +1035,12 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
   hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, dep_h, dep_w, img_h, img_w);
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0};
-  // blocks per image for the selection sweeps: ~8 pixels per thread, >= 1
-  int G = (n + kBlock * 8 - 1) / (kBlock * 8);
-  G = std::max(1, std::min(G, 512));
-  int rc = launch_select<0>(g, st, hist, batch, G, s);
+  // selection sweeps: ~8 output rows per workgroup for 1024-wide images
+  const int sel_rows = std::max(1, std::min(16, (8 * 1024 + img_w - 1) / img_w));
+  const Sweep ssel = plan_sweep(img_h, 1, dep_h, dep_w, img_h, g.same != 0, sel_rows);
+  int rc = launch_select<0>(g, st, hist, batch, ssel, s);
   if (rc) return rc;
-  rc = launch_select<1>(g, st, hist, batch, G, s);
+  rc = launch_select<1>(g, st, hist, batch, ssel, s);
   if (rc) return rc;
 
   Cam cam;
@@ -764,8 +1057,9 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
   cam.Wn = (img_w + step - 1) / step;
   const int Hn = (img_h + step - 1) / step;
   cam.N = cam.Wn * Hn;
-  int GU = (cam.N + kBlock * 4 * 4 - 1) / (kBlock * 4 * 4);
-  GU = std::max(1, std::min(GU, 1024));
+  const int unp_rows = std::max(1, std::min(kMaxRows, (4 * 1024 + cam.Wn - 1) / cam.Wn));
+  const Sweep sunp = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, unp_rows);
+  const size_t unp_lds = sweep_lds(sunp, dep_w);
   const double* field = nullptr;
   if (params->smooth) {
     double* f0 = reinterpret_cast<double*>(ws + L.field);
@@ -775,11 +1069,23 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
     hipLaunchKernelGGL((k_blur<true>), dim3(nb), dim3(256), 0, s, f0, f1, st, batch, img_h, img_w);
     hipLaunchKernelGGL((k_blur<false>), dim3(nb), dim3(256), 0, s, f1, f0, st, batch, img_h, img_w);
     field = f0;
-    hipLaunchKernelGGL((k_unproject<true>), dim3(batch * GU), dim3(kBlock), 0, s, g, st, field, image, channels,
-                       batch, GU, params->invert, cam, xyz, rgb, st);
+    hipLaunchKernelGGL((k_unproject<true>), dim3(batch * sunp.nrb), dim3(kBlock), 0, s, g, st, field, image,
+                       channels, batch, sunp, params->invert, cam, xyz, rgb, st);
+  } else if (channels == 3 && cam.N % 4 == 0 && cam.Wn % 4 == 0) {
+    // 2 rows of 1024 points (or the equivalent) per workgroup: 2 groups of 4 points per thread
+    const int fast_rows = std::max(1, std::min(kMaxRows, (2 * 1024 + cam.Wn - 1) / cam.Wn));
+    const Sweep sf = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, fast_rows);
+    const size_t lf = sweep_lds(sf, dep_w);
+    const dim3 grid(batch * sf.nrb), block(kBlock);
+    if (step == 1)
+      hipLaunchKernelGGL((k_unproject_fast<1>), grid, block, lf, s, g, st, image, batch, sf, params->invert, cam, xyz, rgb, st);
+    else if (step == 2)
+      hipLaunchKernelGGL((k_unproject_fast<2>), grid, block, lf, s, g, st, image, batch, sf, params->invert, cam, xyz, rgb, st);
+    else
+      hipLaunchKernelGGL((k_unproject_fast<4>), grid, block, lf, s, g, st, image, batch, sf, params->invert, cam, xyz, rgb, st);
   } else {
-    hipLaunchKernelGGL((k_unproject<false>), dim3(batch * GU), dim3(kBlock), 0, s, g, st, field, image, channels,
-                       batch, GU, params->invert, cam, xyz, rgb, st);
+    hipLaunchKernelGGL((k_unproject<false>), dim3(batch * sunp.nrb), dim3(kBlock), unp_lds, s, g, st, field, image,
+                       channels, batch, sunp, params->invert, cam, xyz, rgb, st);
   }
   hipLaunchKernelGGL(k_finalize, dim3((batch + 63) / 64), dim3(64), 0, s, st, batch, bbox, stats);
   return check_launch("unproject");
