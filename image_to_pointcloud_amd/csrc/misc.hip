@@ -90,13 +90,21 @@ __global__ __launch_bounds__(256) void k_layernorm_any(const float* __restrict__
 }
 
 // NHWC bf16, 8 channels (16 B) per thread; torch upsample_bilinear2d, align_corners=True.
-__global__ __launch_bounds__(256) void k_upsample2x(const bf16_t* __restrict__ x, int B, int h, int w, int c,
-                                                    const bf16_t* __restrict__ add, bf16_t* __restrict__ y) {
-  const int H = 2 * h, W = 2 * w;
+// Bilinear resize of an NHWC bf16 map to (H, W) with torch's upsample_bilinear2d
+// source-index rules (float scale; align_corners: s = (in-1)/(out-1) * dst, else
+// s = max(in/out * (dst + 0.5) - 0.5, 0)); 8 channels per lane (16 B loads).
+__global__ __launch_bounds__(256) void k_resize(const bf16_t* __restrict__ x, int B, int h, int w, int c, int H, int W,
+                                                int align, const bf16_t* __restrict__ add, bf16_t* __restrict__ y) {
   const int cv = c / 8;
   const int64_t total = (int64_t)B * H * W * cv;
-  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
-  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  float sh, sw;
+  if (align) {
+    sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+    sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  } else {
+    sh = (float)h / (float)H;
+    sw = (float)w / (float)W;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int ch = (int)(i % cv);
     int64_t pix = i / cv;
@@ -104,12 +112,13 @@ __global__ __launch_bounds__(256) void k_upsample2x(const bf16_t* __restrict__ x
     pix /= W;
     const int oy = (int)(pix % H);
     const int b = (int)(pix / H);
-    const float fy = sh * oy, fx = sw * ox;
+    const float fy = align ? sh * oy : fmaxf(sh * (oy + 0.5f) - 0.5f, 0.f);
+    const float fx = align ? sw * ox : fmaxf(sw * (ox + 0.5f) - 0.5f, 0.f);
     const int y0 = (int)fy, x0 = (int)fx;
     const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
     const float ly1 = fy - y0, lx1 = fx - x0;
     const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-    const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
+const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
     const uint4 a00 = *reinterpret_cast<const uint4*>(base + ((int64_t)y0 * w + x0) * c);
     const uint4 a01 = *reinterpret_cast<const uint4*>(base + ((int64_t)y0 * w + x1) * c);
     const uint4 a10 = *reinterpret_cast<const uint4*>(base + ((int64_t)y1 * w + x0) * c);
@@ -212,14 +221,21 @@ extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, c
   return check_launch("layernorm");
 }
 
-extern "C" int i2pc_upsample2x(const void* x, int batch, int h, int w, int c, const void* add, void* y, void* stream) {
+extern "C" int i2pc_resize_bilinear(const void* x, int batch, int h, int w, int c, int out_h, int out_w,
+                                    int align_corners, const void* add, void* y, void* stream) {
   clear_error();
   I2PC_REQUIRE(x && y, "NULL pointer");
-  I2PC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0, "upsample2x: bad shape (c %% 8 == 0)");
-  const int64_t work = (int64_t)batch * 4 * h * w * (c / 8);
-  hipLaunchKernelGGL(k_upsample2x, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
-                     static_cast<const bf16_t*>(x), batch, h, w, c, static_cast<const bf16_t*>(add), static_cast<bf16_t*>(y));
-  return check_launch("upsample2x");
+  I2PC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && out_h > 0 && out_w > 0,
+               "resize_bilinear: bad shape (c %% 8 == 0)");
+  const int64_t work = (int64_t)batch * out_h * out_w * (c / 8);
+  hipLaunchKernelGGL(k_resize, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), static_cast<const bf16_t*>(x),
+                     batch, h, w, c, out_h, out_w, align_corners ? 1 : 0, static_cast<const bf16_t*>(add),
+                     static_cast<bf16_t*>(y));
+  return check_launch("resize_bilinear");
+}
+
+extern "C" int i2pc_upsample2x(const void* x, int batch, int h, int w, int c, const void* add, void* y, void* stream) {
+  return i2pc_resize_bilinear(x, batch, h, w, c, 2 * h, 2 * w, 1, add, y, stream);
 }
 
 extern "C" int i2pc_cls_pos(const float* cls, const float* pos0, int batch, int tokens, int dim, float* x, void* stream) {

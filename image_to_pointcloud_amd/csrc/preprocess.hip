@@ -94,7 +94,7 @@ static Axis identity(int n) {
 }
 
 struct DevPlan {
-  int in_h, in_w, out_h, out_w, kx, ky, R, tiles, patch, lds_bytes;
+  int in_h, in_w, out_h, out_w, kx, ky, R, tiles, patch, pld, lds_bytes;
   float mean[3], stdv[3];
   const int* hx_min; const int* hx_cnt; const int* hx_k;
   const int* vy_min; const int* vy_cnt; const int* vy_k;
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __
         const int prow = b * npatch + (yy / p) * np_x + xx / p;
         const int col = c * p * p + (yy % p) * p + (xx % p);
         __bf16 h = (__bf16)v;
-        static_cast<uint16_t*>(out)[(int64_t)prow * 3 * p * p + col] = *reinterpret_cast<uint16_t*>(&h);
+        static_cast<uint16_t*>(out)[(int64_t)prow * P.pld + col] = *reinterpret_cast<uint16_t*>(&h);
       }
     }
   }
@@ -239,6 +239,7 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
   DevPlan& P = pl->p;
   P.in_h = in_h; P.in_w = in_w; P.out_h = out_h; P.out_w = out_w;
   P.kx = hx.ksize; P.ky = vy.ksize; P.R = R; P.tiles = tiles; P.patch = patch;
+  P.pld = (3 * patch * patch + 63) / 64 * 64;   // patch-row pitch: the GEMM K axis, padded to 64
   P.lds_bytes = (int)align_up((size_t)max_rows * row_bytes, 16);
   for (int c = 0; c < 3; ++c) { P.mean[c] = mean[c]; P.stdv[c] = stdv[c]; }
   const int* base = static_cast<const int*>(dev);

@@ -45,6 +45,7 @@ class DPTSpec:
     fusion: int
     factors: tuple = (4, 2, 1, 0.5)
     eps: float = 1e-12
+    family: str = "dpt"
 
     @property
     def grid(self) -> int:
@@ -279,8 +280,10 @@ class DPTDepthModel:
         return b
 
     # ------------------------------------------------------------------ forward
-    def forward(self, patches, B: int):
+    def forward(self, patches, B: int, gh: int = None, gw: int = None):
         """patches: bf16 [B * grid^2, 3*patch^2] (preprocess layout 'patches') -> depth fp32 [B, H', W']."""
+        if (gh or self.spec.grid, gw or self.spec.grid) != (self.spec.grid, self.spec.grid):
+            raise NotImplementedError("DPT runs on its square checkpoint grid (the Intel processors resize to 384x384)")
         s = self.spec
         D, g = s.hidden, s.grid
         np_, T = g * g, g * g + 1

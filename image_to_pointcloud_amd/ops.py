@@ -45,6 +45,9 @@ _lib.register("i2pc_attention", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_
                                                ctypes.c_float, c_void_p, c_void_p])
 _lib.register("i2pc_upsample2x", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, c_void_p, c_void_p, c_void_p])
+_lib.register("i2pc_resize_bilinear", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     c_void_p, c_void_p, c_void_p])
 _lib.register("i2pc_cls_pos", ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              c_void_p, c_void_p])
 _lib.register("i2pc_f32_to_bf16", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p])
@@ -247,8 +250,21 @@ def upsample2x(x, add=None, out=None):
     B, H, W, C = x.shape
     if out is None:
         out = torch.empty((B, 2 * H, 2 * W, C), dtype=torch.bfloat16, device=x.device)
-    with _Timed("k_upsample2x", 0.0, 2.0 * B * H * W * C * (1 + 4 + (4 if add is not None else 0))):
+    with _Timed("k_resize", 0.0, 2.0 * B * H * W * C * (1 + 4 + (4 if add is not None else 0))):
         _lib.call("i2pc_upsample2x", _p(x), B, H, W, C, _p(add), _p(out), _stream())
+    return out
+
+
+def resize_bilinear(x, out_h, out_w, align_corners=True, add=None, out=None):
+    """NHWC bf16 bilinear resize (torch upsample_bilinear2d index rules), optional + add."""
+    torch = _torch()
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    if out is None:
+        out = torch.empty((B, out_h, out_w, C), dtype=torch.bfloat16, device=x.device)
+    with _Timed("k_resize", 0.0, 2.0 * B * out_h * out_w * C * (1 + 4 + (1 if add is not None else 0))):
+        _lib.call("i2pc_resize_bilinear", _p(x), B, H, W, C, out_h, out_w, int(bool(align_corners)), _p(add),
+                  _p(out), _stream())
     return out
 
 

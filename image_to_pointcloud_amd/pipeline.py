@@ -18,31 +18,46 @@ from __future__ import annotations
 from typing import Optional
 
 from . import geometry
-from .dpt import DPT_LARGE, DPTDepthModel, DPTSpec, synthetic_state_dict
-from .preprocess import DPT_LARGE_PROCESSOR, Preprocessor, ProcessorSpec
+from .dpt import DPT_LARGE, DPTSpec
+from .preprocess import DEPTH_ANYTHING_PROCESSOR, DPT_LARGE_PROCESSOR, Preprocessor, ProcessorSpec
+
+
+def model_for(spec, state_dict=None, device=None, seed: int = 0):
+    """The network of a spec's family (DPT or Depth-Anything); seeded synthetic weights when none are given."""
+    if getattr(spec, "family", "dpt") == "depth-anything":
+        from .depth_anything import DepthAnythingModel as Model, synthetic_state_dict
+    else:
+        from .dpt import DPTDepthModel as Model, synthetic_state_dict
+    return Model(spec, state_dict if state_dict is not None else synthetic_state_dict(spec, seed), device)
+
+
+def default_processor(spec) -> ProcessorSpec:
+    return DEPTH_ANYTHING_PROCESSOR if getattr(spec, "family", "dpt") == "depth-anything" else DPT_LARGE_PROCESSOR
 
 
 class PointCloudPipeline:
     def __init__(self, batch: int, height: int, width: int, spec: DPTSpec = DPT_LARGE,
-                 state_dict: Optional[dict] = None, processor: ProcessorSpec = DPT_LARGE_PROCESSOR,
+                 state_dict: Optional[dict] = None, processor: Optional[ProcessorSpec] = None,
                  density: str = "high", invert: bool = True, depth_scale: float = 10.0,
-                 smooth: bool = False, fov: Optional[float] = None, device=None, seed: int = 0):
+                 smooth: bool = False, fov: Optional[float] = None, device=None, seed: int = 0, model=None):
         import torch
         self.device = torch.device(device) if device is not None else geometry.require_device()
         self.batch, self.height, self.width = batch, height, width
         self.spec = spec
         self.density, self.invert, self.depth_scale, self.smooth, self.fov = density, invert, depth_scale, smooth, fov
-        sd = state_dict if state_dict is not None else synthetic_state_dict(spec, seed)
-        self.model = DPTDepthModel(spec, sd, self.device)
-        pspec = ProcessorSpec(size=(spec.image, spec.image), mean=processor.mean, std=processor.std,
-                              keep_aspect_ratio=processor.keep_aspect_ratio, multiple=processor.multiple)
-        self.pre = Preprocessor(height, width, pspec, patch=spec.patch)
-        if (self.pre.out_h, self.pre.out_w) != (spec.image, spec.image):
-            raise NotImplementedError("non-square network input needs position-embedding interpolation")
+        if model is None:
+            model = model_for(spec, state_dict, self.device, seed)
+        self.model = model
+        processor = processor or default_processor(spec)
+        if getattr(spec, "family", "dpt") == "dpt":
+            processor = ProcessorSpec(size=(spec.image, spec.image), mean=processor.mean, std=processor.std,
+                                      keep_aspect_ratio=processor.keep_aspect_ratio, multiple=processor.multiple)
+        self.pre = Preprocessor(height, width, processor, patch=spec.patch)
+        self.gh, self.gw = self.pre.out_h // spec.patch, self.pre.out_w // spec.patch
         step = geometry.DENSITY_STEP[density]
         self.points_per_image = geometry.point_count(height, width, step)
-        g = spec.grid
-        self._patches = torch.empty((batch * g * g, 3 * spec.patch ** 2), dtype=torch.bfloat16, device=self.device)
+        self._patches = torch.zeros((batch * self.gh * self.gw, self.pre.patch_pitch), dtype=torch.bfloat16,
+                                    device=self.device)
         self._out = geometry.PointBatch(
             xyz=torch.empty((batch, self.points_per_image, 3), dtype=torch.float32, device=self.device),
             rgb=torch.empty((batch, self.points_per_image, 3), dtype=torch.uint8, device=self.device),
@@ -52,10 +67,15 @@ class PointCloudPipeline:
         self._static_in = None
         self.depth = None
 
+    def infer_depth(self, images):
+        """images: uint8 [B,H,W,3] BGR on the device -> model-resolution depth fp32 [B, h', w']."""
+        self.pre(images, layout="patches", out=self._patches)
+        self.depth = self.model(self._patches, self.batch, self.gh, self.gw)
+        return self.depth
+
     def run(self, images):
         """images: uint8 [B,H,W,3] BGR on the device -> PointBatch (device tensors, reused across calls)."""
-        self.pre(images, layout="patches", out=self._patches)
-        self.depth = self.model(self._patches, self.batch)
+        self.infer_depth(images)
         return geometry.unproject_batch(self.depth, images, density=self.density, invert=self.invert,
                                         depth_scale=self.depth_scale, smooth=self.smooth, fov=self.fov,
                                         out=self._out)

@@ -53,11 +53,17 @@ def output_size(in_h: int, in_w: int, spec: ProcessorSpec):
     return constrain(sh * in_h, spec.multiple), constrain(sw * in_w, spec.multiple)
 
 
+def patch_pitch(patch: int) -> int:
+    """Row pitch of the bf16 patch rows: 3*p*p rounded up to the GEMM K granule (64)."""
+    return (3 * patch * patch + 63) // 64 * 64
+
+
 class Preprocessor:
     def __init__(self, in_h: int, in_w: int, spec: ProcessorSpec = DPT_LARGE_PROCESSOR, patch: int = 0):
         self.in_h, self.in_w = in_h, in_w
         self.out_h, self.out_w = output_size(in_h, in_w, spec)
         self.patch = patch
+        self.patch_pitch = patch_pitch(patch)
         lib = _lib.load()
         mean = (ctypes.c_float * 3)(*spec.mean)
         std = (ctypes.c_float * 3)(*spec.std)
@@ -89,8 +95,10 @@ class Preprocessor:
         elif layout == "patches":
             p = self.patch
             if out is None:
-                out = torch.empty((B * (self.out_h // p) * (self.out_w // p), 3 * p * p), dtype=torch.bfloat16,
+                out = torch.zeros((B * (self.out_h // p) * (self.out_w // p), self.patch_pitch), dtype=torch.bfloat16,
                                   device=bgr.device)
+            if out.shape[-1] != self.patch_pitch or not out.is_contiguous():
+                raise ValueError(f"patch rows need a contiguous [rows, {self.patch_pitch}] buffer")
             code = 1
         else:
             raise ValueError(layout)

@@ -140,6 +140,13 @@ int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scal
  * modeling_dpt.py:504-506, 698), optional + add (bf16, output shape). */
 int i2pc_upsample2x(const void* x, int batch, int h, int w, int c, const void* add, void* y, void* stream);
 
+/* General bilinear resize of an NHWC bf16 map to out_h x out_w with torch's
+ * upsample_bilinear2d index rules (align_corners 1: the DPT/Depth-Anything fusion and
+ * head resizes, modeling_depth_anything.py:169-174, 296-301; 0: the fusion residual
+ * resize, :161-163), optional + add (bf16, output shape). c % 8 == 0. */
+int i2pc_resize_bilinear(const void* x, int batch, int h, int w, int c, int out_h, int out_w,
+                         int align_corners, const void* add, void* y, void* stream);
+
 /* Elementwise helpers of the ViT stem / neck. */
 /* rows [b*tokens + 0] of the fp32 residual stream = cls + pos[0] (modeling_dpt.py:226-231) */
 int i2pc_cls_pos(const float* cls, const float* pos0, int batch, int tokens, int dim, float* x, void* stream);
@@ -160,8 +167,10 @@ int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int out_w, const 
                                 int patch, i2pc_preprocess_plan** plan);
 void i2pc_preprocess_plan_destroy(i2pc_preprocess_plan* plan);
 /* bgr: uint8 [batch, in_h, in_w, 3]; layout 0 -> float32 [batch, 3, out_h, out_w] (pixel_values);
- * layout 1 -> bf16 [batch * (out_h/patch)*(out_w/patch)][3*patch*patch], column order (c, py, px)
- * (the im2col of the patch-embedding conv, modeling_dpt.py:60-69). */
+ * layout 1 -> bf16 [batch * (out_h/patch)*(out_w/patch)][pitch], pitch = 3*patch*patch rounded up
+ * to a multiple of 64 (the GEMM K granule; 768 for patch 16, 640 for patch 14), column order
+ * (c, py, px) (the im2col of the patch-embedding conv, modeling_dpt.py:60-69,
+ * modeling_dinov2.py Dinov2PatchEmbeddings); the pad columns are never written (zero them once). */
 int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* bgr, int batch, int layout, void* out, void* stream);
 
 #ifdef __cplusplus

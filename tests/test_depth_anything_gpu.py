@@ -1,0 +1,81 @@
+"""Depth-Anything-V2 parity: the bf16 HIP network against transformers' fp32
+DepthAnythingForDepthEstimation on the same seeded weights and the same
+preprocessed input (keep-aspect, multiple-of-14 resize; app.py:78-82, 109-116).
+
+Tolerance, as for DPT (bf16 operands / fp32 accumulation vs an fp32 network,
+SURVEY §8c D9): relative L2 error of the depth <= 2e-2 and max |err| <= 6e-2 * max |ref|.
+Non-square inputs exercise the bicubic position-embedding interpolation and the
+non-square neck/fusion/head sizes.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+transformers = pytest.importorskip("transformers")
+pytestmark = pytest.mark.gpu
+
+
+def _hf_model(spec, sd, dev):
+    from transformers import DepthAnythingConfig, DepthAnythingForDepthEstimation
+    m = DepthAnythingForDepthEstimation(DepthAnythingConfig(**spec.hf_config_kwargs()))
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected and not missing, (missing, unexpected)
+    return m.to(dev).eval()
+
+
+def _images(B, h, w, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    out = []
+    for i in range(B):
+        base = 127 + 100 * np.sin(u / (11.0 + i)) * np.cos(v / (7.0 + i))
+        out.append(np.clip(base[..., None] + rng.normal(0, 20, (h, w, 3)), 0, 255).astype(np.uint8))
+    return np.stack(out)
+
+
+@pytest.mark.parametrize("which,B,hw", [("tiny", 2, (168, 168)), ("tiny", 2, (150, 230)), ("small", 2, (384, 384)),
+                                        ("small", 1, (768, 1024))])
+def test_depth_anything_matches_transformers_fp32(which, B, hw):
+    from image_to_pointcloud_amd.depth_anything import DA_TINY, DA_V2_SMALL, DepthAnythingModel, synthetic_state_dict
+    from image_to_pointcloud_amd.preprocess import DEPTH_ANYTHING_PROCESSOR, Preprocessor, ProcessorSpec
+    from oracle import preprocess_ref as pre
+    spec = DA_V2_SMALL if which == "small" else DA_TINY
+    dev = torch.device("cuda")
+    sd = synthetic_state_dict(spec, seed=0)
+    ours = DepthAnythingModel(spec, sd, dev)
+    ref = _hf_model(spec, sd, dev)
+    P = DEPTH_ANYTHING_PROCESSOR
+    pspec = ProcessorSpec(size=(spec.image, spec.image), mean=P.mean, std=P.std, keep_aspect_ratio=True, multiple=14)
+    imgs = _images(B, hw[0], hw[1], 11)
+    prep = Preprocessor(hw[0], hw[1], pspec, patch=spec.patch)
+    timgs = torch.from_numpy(imgs).to(dev)
+    pix = prep(timgs, layout="nchw")
+    exp_pix = np.stack([pre.dpt_preprocess(im, size=pspec.size, mean=P.mean, std=P.std, keep_aspect_ratio=True,
+                                           multiple=14) for im in imgs])
+    assert np.array_equal(pix.cpu().numpy(), exp_pix), "preprocess not bit-exact"
+    gh, gw = prep.out_h // 14, prep.out_w // 14
+    patches = prep(timgs, layout="patches")
+    depth = ours(patches, B, gh, gw)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        exp = ref(pixel_values=pix).predicted_depth.float()
+    assert depth.shape == exp.shape, (depth.shape, exp.shape)
+    err = depth - exp
+    rel = (err.norm() / exp.norm()).item()
+    mx = (err.abs().max() / exp.abs().max()).item()
+    assert exp.abs().max() > 0 and exp.std() > 1e-3 * exp.abs().max(), "degenerate reference depth"
+    assert rel <= 2e-2 and mx <= 6e-2, f"rel L2 {rel:.3e} max {mx:.3e}"
+
+
+@pytest.mark.parametrize("B,h,w,c,oh,ow,ac", [(2, 19, 19, 64, 37, 37, True), (1, 296, 296, 64, 518, 518, True),
+                                              (2, 37, 49, 64, 74, 98, True), (1, 10, 13, 16, 23, 7, False)])
+def test_resize_bilinear_matches_torch(B, h, w, c, oh, ow, ac):
+    from image_to_pointcloud_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(h * w)
+    x = torch.randn(B, h, w, c, generator=g).to(torch.bfloat16).cuda()
+    add = torch.randn(B, oh, ow, c, generator=g).to(torch.bfloat16).cuda()
+    got = ops.resize_bilinear(x, oh, ow, align_corners=ac, add=add).float()
+    ref = torch.nn.functional.interpolate(x.float().permute(0, 3, 1, 2), size=(oh, ow), mode="bilinear",
+                                          align_corners=ac).permute(0, 2, 3, 1) + add.float()
+    err = (got - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
