@@ -50,7 +50,18 @@ def _args():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-profile", action="store_true")
+    ap.add_argument("--all-gather", action="store_true",
+                    help="C3 layout: all-gather every rank's point buffers (RCCL over xGMI) inside each step")
+    ap.add_argument("--model", default="dpt-large", choices=["dpt-large", "depth-anything-v2"])
     return ap.parse_args()
+
+
+def _spec(name):
+    if name == "depth-anything-v2":
+        from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL
+        return DA_V2_SMALL
+    from image_to_pointcloud_amd.dpt import DPT_LARGE
+    return DPT_LARGE
 
 
 def _images(batch, size, rank, device):
@@ -92,35 +103,43 @@ def _kernel_profile(pipe, images):
     return per, geo_t
 
 
-def _cpu_baseline():
-    """Reference CPU path (restated) on one 1024^2 image, density high."""
+def _cpu_baseline(spec, size, density):
+    """Reference CPU path (restated) on one image of the bench's size, density high."""
     import numpy as np
     import torch
-    from transformers import DPTConfig, DPTForDepthEstimation
 
-    from image_to_pointcloud_amd.dpt import DPT_LARGE, synthetic_state_dict
     from oracle import preprocess_ref, unproject_ref
+    from image_to_pointcloud_amd.pipeline import default_processor
 
     threads = os.cpu_count() or 1
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     torch.set_num_threads(threads)
-    model = DPTForDepthEstimation(DPTConfig(**DPT_LARGE.hf_config_kwargs()))
-    model.load_state_dict(synthetic_state_dict(DPT_LARGE, 0), strict=False)
+    if spec.family == "depth-anything":
+        from transformers import DepthAnythingConfig as Cfg, DepthAnythingForDepthEstimation as Net
+        from image_to_pointcloud_amd.depth_anything import synthetic_state_dict
+    else:
+        from transformers import DPTConfig as Cfg, DPTForDepthEstimation as Net
+        from image_to_pointcloud_amd.dpt import synthetic_state_dict
+    model = Net(Cfg(**spec.hf_config_kwargs()))
+    model.load_state_dict(synthetic_state_dict(spec, 0), strict=False)
     model.eval()
+    proc = default_processor(spec)
+    psize = proc.size if spec.family == "depth-anything" else (spec.image, spec.image)
     rng = np.random.Generator(np.random.PCG64(1000))
-    img = rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8)
+    img = rng.integers(0, 256, (size, size, 3), dtype=np.uint8)
     t0 = time.perf_counter()
-    pix = preprocess_ref.dpt_preprocess(img)                            # app.py:103,109
+    pix = preprocess_ref.dpt_preprocess(img, size=psize, mean=proc.mean, std=proc.std,          # app.py:103,109
+                                        keep_aspect_ratio=proc.keep_aspect_ratio, multiple=proc.multiple)
     with torch.no_grad():                                               # app.py:111-116
         depth = model(pixel_values=torch.from_numpy(pix)[None]).predicted_depth[0].numpy().astype(np.float32)
     t1 = time.perf_counter()
-    pts, _ = unproject_ref.depth_to_point_cloud(img, depth, density="high", loop=True)   # app.py:174-250
+    pts, _ = unproject_ref.depth_to_point_cloud(img, depth, density=density, loop=True)  # app.py:174-250
     unproject_ref.gis_bounds(pts)
     t2 = time.perf_counter()
     n = len(pts)
     return {"value": n / (t2 - t0) / 1e6, "unit": "Mpoints/s", "cores": threads, "kind": "port",
-            "sample": f"1 image 1024x1024, density high ({n} points): Pillow-exact preprocessing + transformers "
-                      f"fp32 DPT-Large forward on {threads} threads ({t1 - t0:.2f} s) + the reference per-point "
+            "sample": f"1 image {size}x{size}, density {density} ({n} points): Pillow-exact preprocessing + transformers "
+                      f"fp32 {spec.name} forward on {threads} threads ({t1 - t0:.2f} s) + the reference per-point "
                       f"Python loop, single-threaded ({t2 - t1:.2f} s)",
             "seconds": t2 - t0}
 
@@ -130,9 +149,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from image_to_pointcloud_amd import distributed as D
+    rank, local, world = D.world()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -140,11 +158,11 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    from image_to_pointcloud_amd.dpt import DPT_LARGE
     from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    spec = _spec(a.model)
 
     B, S = a.batch, a.size
-    pipe = PointCloudPipeline(B, S, S, spec=DPT_LARGE, density=a.density, device=device, seed=0)
+    pipe = PointCloudPipeline(B, S, S, spec=spec, density=a.density, device=device, seed=0)
     images = _images(B, S, rank, device)
     if a.no_graph:
         step = lambda: pipe.run(images)     # noqa: E731
@@ -152,6 +170,14 @@ def main():
     else:
         pipe.capture(images)
         step = pipe.replay
+    if a.all_gather and world > 1:
+        gx = torch.empty((world * B, pipe.points_per_image, 3), dtype=torch.float32, device=device)
+        gr = torch.empty((world * B, pipe.points_per_image, 3), dtype=torch.uint8, device=device)
+        inner = step
+
+        def step():
+            out = inner()
+            D.gather_points(out.xyz, out.rgb, out_xyz=gx, out_rgb=gr)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -164,11 +190,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, device)
     points_step = world * B * pipe.points_per_image
     value = points_step * a.steps / elapsed / 1e6
     ms = elapsed / a.steps * 1e3
@@ -190,8 +212,7 @@ def main():
             ach = d["bytes"] / (d["t"]) / 1e9
             roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
-        g = DPT_LARGE.grid * DPT_LARGE.patch
-        geo_bytes = B * (4.0 * g * g + 18.0 * pipe.points_per_image)
+        geo_bytes = B * (4.0 * pipe.pre.out_h * pipe.pre.out_w + 18.0 * pipe.points_per_image)
         roof_geo = {"kernel": "i2pc_unproject (select + unproject + bbox launches)", "bound": "hbm",
                     "achieved": round(geo_bytes / geo_t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(geo_bytes / geo_t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
@@ -203,20 +224,22 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            cpu = _cpu_baseline()
+            cpu = _cpu_baseline(spec, S, a.density)
         except Exception as e:   # the GPU figure stands on its own; say why the baseline is missing
             cpu = {"value": None, "unit": "Mpoints/s", "cores": os.cpu_count(), "kind": "port",
                    "sample": f"failed: {type(e).__name__}: {e}"}
 
     if rank == 0:
-        flops_img = DPT_LARGE.flops_per_image()
+        flops_img = (spec.flops_per_image(pipe.gh, pipe.gw) if spec.family == "depth-anything"
+                     else spec.flops_per_image())
         out = {
             "metric": "Mpoints/sec end-to-end (depth+unproject), 1024² batch",
             "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16", "data": "synthetic (uint8 RGB uniform, PCG64 seeds 1000+i; seeded random DPT-Large weights)",
-            "config": {"workload": f"DPT-Large bf16 depth + unproject, batch {B} x {S}x{S} per GPU, density {a.density}",
-                       "model": "DPT-Large (ViT-L/16, 384x384 network input)", "global_batch": B * world,
+            "dtype": "bf16", "data": f"synthetic (uint8 RGB uniform, PCG64 seeds 1000+i; seeded random {spec.name} weights)",
+            "config": {"workload": f"{spec.name} bf16 depth + unproject, batch {B} x {S}x{S} per GPU, density {a.density}"
+                                   + (", all-gather of points" if a.all_gather and world > 1 else ""),
+                       "model": spec.name, "network_input": [pipe.pre.out_h, pipe.pre.out_w], "global_batch": B * world,
                        "image": [S, S], "points_per_image": pipe.points_per_image, "parallelism": f"dp{world}",
                        "hip_graph": not a.no_graph},
             "network_tflops": round(flops_img * B * world / (elapsed / a.steps) / 1e12, 1),

@@ -946,6 +946,30 @@ __global__ void k_finalize(const SelState* st, int B, double* bbox, double* stat
   }
 }
 
+// Depth preview colouring (create_depth_preview, app.py:124-172): the model-res depth
+// after fill / p2-p98 normalise / invert, (d * 255).astype(uint8) in the branch's dtype,
+// then a 256-entry BGR colour table (cv2.applyColorMap).
+__global__ void k_preview(const float* depth, const SelState* st, int B, int n, int invert, const uint8_t* lut,
+                          uint8_t* out) {
+  __shared__ uint8_t tab[768];
+  for (int i = threadIdx.x; i < 768; i += blockDim.x) tab[i] = lut[i];
+  __syncthreads();
+  const int64_t total = (int64_t)B * n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / n);
+    const SelState* S = st + b;
+    const Norm nm = load_norm(S, invert);
+    float val = depth[i];
+    if (S->has_med && !isfinite(val)) val = S->med;
+    const double d = normalize(val, nm);
+    const int q = nm.mode == 0 ? (int)(d * 255.0) : (int)((float)d * 255.0f);   // astype(uint8) truncates
+    const int k = min(max(q, 0), 255) * 3;
+    out[i * 3 + 0] = tab[k];
+    out[i * 3 + 1] = tab[k + 1];
+    out[i * 3 + 2] = tab[k + 2];
+  }
+}
+
 __global__ void k_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,
                                 float* oxyz, float* orgb) {
   const int64_t cnt = (n + stride - 1) / stride;
@@ -1100,4 +1124,38 @@ extern "C" int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t 
   const int blocks = (int)std::min<int64_t>((cnt + 255) / 256, 4096);
   hipLaunchKernelGGL(k_gather_stride, dim3(blocks), dim3(256), 0, as_stream(stream), xyz, rgb, n, stride, out_xyz, out_rgb);
   return check_launch("gather_stride");
+}
+
+extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, int invert, const uint8_t* lut_bgr,
+                                  uint8_t* out_bgr, double* stats, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  clear_error();
+  I2PC_REQUIRE(depth && lut_bgr && out_bgr && workspace, "NULL device pointer");
+  I2PC_REQUIRE(batch > 0 && h > 0 && w > 0, "empty shape");
+  I2PC_REQUIRE((int64_t)h * w < (1ll << 31), "depth map too large");
+  const Layout L = layout(batch, h, w, 0);
+  if (workspace_bytes < L.total) return set_error(I2PC_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
+  hipStream_t s = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  SelState* st = reinterpret_cast<SelState*>(ws + L.state);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
+  Tap* xt = reinterpret_cast<Tap*>(ws + L.xtab);
+  Tap* yt = reinterpret_cast<Tap*>(ws + L.ytab);
+  if (hipMemsetAsync(hist, 0, sizeof(uint32_t) * kSlots * kBins * (size_t)batch, s) != hipSuccess)
+    return set_error(I2PC_ELAUNCH, "memset failed");
+  const int n = h * w;
+  const int init_threads = std::max(std::max(batch, h), w);
+  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, h, w, h, w);
+  Geo g{depth, h, w, h, w, xt, yt, 1};
+  const int sel_rows = std::max(1, std::min(16, (8 * 1024 + w - 1) / w));
+  const Sweep ssel = plan_sweep(h, 1, h, w, h, true, sel_rows);
+  int rc = launch_select<0>(g, st, hist, batch, ssel, s);
+  if (rc) return rc;
+  rc = launch_select<1>(g, st, hist, batch, ssel, s);
+  if (rc) return rc;
+  const int64_t total = (int64_t)batch * n;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_preview, dim3(blocks), dim3(256), 0, s, depth, st, batch, n, invert ? 1 : 0, lut_bgr, out_bgr);
+  if (stats) hipLaunchKernelGGL(k_finalize, dim3((batch + 63) / 64), dim3(64), 0, s, st, batch, nullptr, stats);
+  return check_launch("depth_preview");
 }

@@ -1,0 +1,55 @@
+"""Multi-GPU layout of the path: one process per GPU, images sharded by batch.
+
+Every image is independent (percentiles, intrinsics and bbox are per image,
+backend/app.py:197-223), so ranks own contiguous slices of the global batch and
+compute without any data-path collective (weak scaling).  The north star's C3
+configuration additionally gathers every rank's fixed-size point buffers onto
+every rank (`gather_points`, one RCCL all-gather per tensor over xGMI); the
+result is image-major, i.e. exactly the concatenation of the per-image
+reference outputs.
+"""
+from __future__ import annotations
+
+import os
+
+
+def world():
+    """(rank, local_rank, world_size) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def shard(global_batch: int, world_size: int, rank: int) -> range:
+    """Contiguous slice of the global image indices owned by `rank` (sizes differ by at most one)."""
+    if world_size <= 0 or not 0 <= rank < world_size:
+        raise ValueError(f"bad rank {rank} / world {world_size}")
+    base, extra = divmod(global_batch, world_size)
+    start = rank * base + min(rank, extra)
+    return range(start, start + base + (1 if rank < extra else 0))
+
+
+def gather_points(xyz, rgb, group=None, out_xyz=None, out_rgb=None):
+    """All-gather [B, N, 3] point buffers from every rank -> [world*B, N, 3] (rank-major = image-major).
+
+    Requires equal B on every rank (the bench's weak-scaling layout)."""
+    import torch
+    import torch.distributed as dist
+    ws = dist.get_world_size(group)
+    if out_xyz is None:
+        out_xyz = torch.empty((ws * xyz.shape[0],) + tuple(xyz.shape[1:]), dtype=xyz.dtype, device=xyz.device)
+    if out_rgb is None:
+        out_rgb = torch.empty((ws * rgb.shape[0],) + tuple(rgb.shape[1:]), dtype=rgb.dtype, device=rgb.device)
+    dist.all_gather_into_tensor(out_xyz, xyz.contiguous(), group=group)
+    dist.all_gather_into_tensor(out_rgb, rgb.contiguous(), group=group)
+    return out_xyz, out_rgb
+
+
+def max_over_ranks(seconds: float, device=None) -> float:
+    """The slowest rank's elapsed time (the bench's whole-job clock)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return seconds
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

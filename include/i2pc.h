@@ -81,6 +81,18 @@ int i2pc_unproject(const float* depth, int dep_h, int dep_w,
                    float* xyz, uint8_t* rgb, double* bbox, double* stats,
                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* Depth preview image (create_depth_preview, backend/app.py:124-172) for a batch of
+ * model-resolution depth maps, before any resize: nanmedian fill, exact p2/p98 of
+ * the map itself, clip/normalise/invert exactly as i2pc_unproject, then
+ * (d*255).astype(uint8) and a colour table.
+ * depth   : float32 [batch, h, w]
+ * lut_bgr : uint8 [256][3] device colour table in B,G,R order (cv2.COLORMAP_PLASMA)
+ * out_bgr : uint8 [batch, h, w, 3]   (what cv2.imencode('.png') receives)
+ * stats   : float64 [batch, 4] as in i2pc_unproject, or NULL
+ * workspace: i2pc_unproject_workspace_bytes(batch, h, w, 0) bytes. */
+int i2pc_depth_preview(const float* depth, int batch, int h, int w, int invert, const uint8_t* lut_bgr,
+                       uint8_t* out_bgr, double* stats, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Gather every stride-th point (preview subsample, app.py:496-506):
  * out_xyz/out_rgb [count] with count = ceil(n / stride). */
 int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,
@@ -172,6 +184,18 @@ void i2pc_preprocess_plan_destroy(i2pc_preprocess_plan* plan);
  * (c, py, px) (the im2col of the patch-embedding conv, modeling_dpt.py:60-69,
  * modeling_dinov2.py Dinov2PatchEmbeddings); the pad columns are never written (zero them once). */
 int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* bgr, int batch, int layout, void* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Artefact writers (save_point_cloud, backend/app.py:310-389) from HOST buffers
+ * (xyz float32 [n][3], rgb uint8 [n][3] or NULL for grey 128). Not stream-ordered.
+ * ------------------------------------------------------------------------ */
+/* XYZ ASCII "%.6f %.6f %.6f %d %d %d\n" (save_xyz, app.py:380-389); `threads` format in parallel. */
+int i2pc_write_xyz(const char* path, const float* xyz, const uint8_t* rgb, int64_t n, int threads);
+/* Binary little-endian PLY, double x/y/z + uchar red/green/blue (save_ply via Open3D, app.py:333-345). */
+int i2pc_write_ply(const char* path, const float* xyz, const uint8_t* rgb, int64_t n);
+/* LAS 1.2 point format 2, offsets = per-axis min, scale `scale` (0.01 in the reference),
+ * RGB = c*256 (save_las via laspy, app.py:347-378). n must be > 0. */
+int i2pc_write_las(const char* path, const float* xyz, const uint8_t* rgb, int64_t n, double scale);
 
 #ifdef __cplusplus
 }

@@ -200,6 +200,14 @@ def normalize_depth(depth_full: np.ndarray, invert: bool):
     return dd, {"p2": p2, "p98": p98, "branch": branch, "median": med}
 
 
+def depth_preview_u8(depth: np.ndarray, invert: bool = True) -> np.ndarray:
+    """create_depth_preview (app.py:124-150) up to the colour map: the uint8 image
+    (d * 255.0).astype(np.uint8) of the model-resolution depth normalised exactly
+    as app.py:191-206 does (the two blocks are the same code)."""
+    d, _ = normalize_depth(depth, invert)
+    return (d * 255.0).astype(np.uint8)                                   # :146
+
+
 def intrinsics(w: int, h: int, fov: Optional[float]):
     """app.py:219-223.  (The REST route drops `fov`, so the reference always takes
     the 1.2*max(w,h) branch -- SURVEY D5.)"""

@@ -14,7 +14,8 @@ back through the reference's own `except` branches exactly as they would
 without Open3D.
 
 Outputs: tests/golden/unproject_cases.npz, tests/golden/pipeline_case.npz,
-tests/golden/pipeline_case.json.  Nothing here runs on the GPU box.
+tests/golden/pipeline_case.json, tests/golden/routes.json, tests/golden/preview_cases.npz
+(the uint8 image create_depth_preview hands to cv2.applyColorMap, recorded by the stub).  Nothing here runs on the GPU box.
 """
 from __future__ import annotations
 
@@ -205,7 +206,33 @@ def main():
     models = asyncio.run(ref.list_available_models())
     with open(os.path.join(OUT_DIR, "routes.json"), "w") as fh:
         json.dump({"routes": routes, "models": models}, fh, indent=1, sort_keys=True)
-    print("wrote", len(meta), "unprojection cases + pipeline case + routes")
+    # 9. depth preview (create_depth_preview, app.py:124-172): record the uint8 image the reference
+    #    hands to cv2.applyColorMap (cv2 is absent: the colour table and PNG bytes stay unpinned)
+    seen = []
+    cv2 = sys.modules["cv2"]
+    cv2.applyColorMap = lambda img, cmap: (seen.append(np.array(img, copy=True)), np.zeros(img.shape + (3,), np.uint8))[1]
+    cv2.imencode = lambda ext, img: (True, np.frombuffer(b"png", np.uint8))
+    prev = {}
+    pmeta = []
+    d_nf = smooth_depth(33, 47, 4)
+    d_nf.reshape(-1)[[5, 77, 300]] = [np.nan, np.inf, -np.inf]
+    d_mm = np.full((40, 40), 1.0, np.float32)
+    d_mm[0, :10] = 3.0
+    d_mm[5, 3:7] = 0.25
+    for name, d in (("smooth", smooth_depth(37, 53, 11)), ("dpt384", smooth_depth(384, 384, 12)),
+                    ("const", np.full((20, 24), 2.5, np.float32)), ("minmax", d_mm), ("nonfinite", d_nf)):
+        for invert in (True, False):
+            seen.clear()
+            url = ref.create_depth_preview(d, invert=invert)
+            assert url is not None and len(seen) == 1, (name, url)
+            key = f"{name}_{int(invert)}"
+            prev[key + "__depth"] = d
+            prev[key + "__u8"] = seen[0]
+            pmeta.append({"name": key, "invert": invert})
+    np.savez_compressed(os.path.join(OUT_DIR, "preview_cases.npz"), **prev)
+    with open(os.path.join(OUT_DIR, "preview_cases.json"), "w") as fh:
+        json.dump(pmeta, fh, indent=1)
+    print("wrote", len(meta), "unprojection cases + pipeline case + routes +", len(pmeta), "preview cases")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,66 @@
+"""End-to-end drop-in parity of the REST job (process_image_pipeline, app.py:419-565)
+against the reference's own output for the golden pipeline case
+(tests/golden/pipeline_case.json): same status fields, pointCloud, gisData
+(bounds from the device bbox), preview sha256 and the downloaded XYZ bytes.
+
+The network is replaced by the fixture's depth map on both sides (the reference
+case was recorded the same way: no offline weights), so everything after the
+depth network runs the HIP path and must match bit-for-bit.
+"""
+import hashlib
+import io
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytest.importorskip("fastapi")
+pytestmark = pytest.mark.gpu
+
+
+def test_rest_job_matches_reference(pipeline_case, monkeypatch, tmp_path):
+    from fastapi.testclient import TestClient
+    from PIL import Image
+    from image_to_pointcloud_amd import app_api, server
+    monkeypatch.chdir(tmp_path)
+    depth = torch.from_numpy(pipeline_case["depth"]).cuda()
+    monkeypatch.setattr(app_api, "load_model", lambda name: {"type": "depth"})
+    monkeypatch.setattr(app_api, "_depth_device", lambda img, mi: depth)
+    buf = io.BytesIO()
+    Image.fromarray(pipeline_case["image"][:, :, ::-1]).save(buf, format="PNG")     # lossless: decodes to the same BGR
+    c = TestClient(server.app)
+    r = c.post("/process", files={"file": ("img.png", buf.getvalue(), "image/png")},
+               params={"point_density": "high", "output_format": "xyz", "fov": 30.0})
+    assert r.status_code == 200
+    job = r.json()["job_id"]
+    st = c.get(f"/status/{job}").json()
+    exp = pipeline_case["summary"]
+    assert st["status"] == exp["status"], st["message"]
+    assert (st["progress"], st["message"]) == (exp["progress"], exp["message"])
+    res = st["results"]
+    assert res["pointCloud"] == {**exp["pointCloud"], "filepath": f"outputs/{job}.xyz"}
+    assert res["gisData"] == exp["gisData"]
+    assert res["downloadUrl"] == f"/download/{job}"
+    assert res["meshPreview"] is None
+    assert res["depthMap"].startswith("data:image/png;base64,")          # reference: None (no cv2 in its container)
+    assert len(res["preview"]["points"]) == exp["preview_len"]
+    pp = np.asarray(res["preview"]["points"], dtype=np.float64)
+    pc = np.asarray(res["preview"]["colors"], dtype=np.float64)
+    assert hashlib.sha256(pp.tobytes()).hexdigest() == exp["preview_points_sha256"]
+    assert hashlib.sha256(pc.tobytes()).hexdigest() == exp["preview_colors_sha256"]
+    dl = c.get(f"/download/{job}")
+    assert dl.status_code == 200
+    assert hashlib.sha256(dl.content).hexdigest() == exp["xyz_sha256"]
+
+
+def test_load_model_and_depth_shapes():
+    from image_to_pointcloud_amd import app_api
+    mi = app_api.load_model("depth-anything-v2")
+    assert mi["type"] == "depth" and app_api.load_model("depth-anything-v2") is mi       # cached
+    rng = np.random.Generator(np.random.PCG64(0))
+    for (h, w), exp in (((384, 384), (518, 518)), ((768, 1024), (518, 686))):
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        d = app_api.process_with_depth_anything(img, mi)
+        assert d.dtype == np.float32 and d.shape == exp and np.isfinite(d).all()
+    with pytest.raises(Exception):
+        app_api.load_model("no-such-model")

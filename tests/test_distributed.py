@@ -1,0 +1,66 @@
+"""Multi-rank layout on CPU (gloo, world_size 2): batch sharding, the optional
+point all-gather and the max-over-ranks clock that bench.py uses."""
+import os
+import socket
+
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from image_to_pointcloud_amd import distributed as D  # noqa: E402
+
+
+def test_shard_covers_batch_contiguously():
+    for gb in (1, 7, 32, 256):
+        for ws in (1, 2, 3, 8):
+            parts = [D.shard(gb, ws, r) for r in range(ws)]
+            flat = [i for p in parts for i in p]
+            assert flat == list(range(gb))
+            assert max(map(len, parts)) - min(map(len, parts)) <= 1
+    with pytest.raises(ValueError):
+        D.shard(8, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        B, N = 3, 5
+        mine = D.shard(B * ws, ws, rank)
+        idx = torch.tensor(list(mine), dtype=torch.float32)
+        xyz = idx[:, None, None].expand(B, N, 3).contiguous() + torch.arange(N, dtype=torch.float32)[None, :, None]
+        rgb = (idx[:, None, None].expand(B, N, 3) % 256).to(torch.uint8).contiguous()
+        gx, gr = D.gather_points(xyz, rgb)
+        t = D.max_over_ranks(1.0 + rank)
+        q.put((rank, gx.numpy().copy(), gr.numpy().copy(), t))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_points_image_major_and_max_clock():
+    ws, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(ws)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, gx, gr, t in out:
+        assert gx.shape == (6, 5, 3) and gr.shape == (6, 5, 3)
+        for img in range(6):                      # image-major: rank 0's images, then rank 1's
+            assert (gx[img, :, 0] == img + torch.arange(5).numpy()).all()
+            assert (gr[img] == img).all()
+        assert t == 2.0

@@ -70,3 +70,20 @@ def test_resize_linear_matches_torch_bilinear():
         t = torch.nn.functional.interpolate(torch.from_numpy(d)[None, None], size=(H, W),
                                             mode="bilinear", align_corners=False)[0, 0].numpy()
         assert np.max(np.abs(got - t)) < 2e-4   # torch rounds the source coordinate in fp32, cv2 in fp64
+
+
+def test_depth_preview_u8_matches_reference_fixtures():
+    """The uint8 image create_depth_preview (app.py:124-150) hands to cv2.applyColorMap,
+    recorded from the reference itself (tests/golden/gen_golden.py, section 9)."""
+    import json
+    import os
+    import numpy as np
+    from oracle import unproject_ref as ref
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    meta = json.load(open(os.path.join(here, "preview_cases.json")))
+    z = np.load(os.path.join(here, "preview_cases.npz"))
+    assert len(meta) == 10
+    for m in meta:
+        got = ref.depth_preview_u8(z[m["name"] + "__depth"], m["invert"])
+        exp = z[m["name"] + "__u8"]
+        assert got.dtype == exp.dtype and np.array_equal(got, exp), m["name"]
