@@ -26,6 +26,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 
 #pragma clang fp contract(off)
@@ -66,7 +67,19 @@ struct alignas(16) SelState {
   float lo32, hi32, den32, pad1;
   uint32_t bbox_key[6];
   uint32_t pad2[2];
+  double rden64;         // RN(1 / den64): quotient seed for div_rn
+  double pad3;
 };
+
+// Correctly rounded a / b from r = RN(1 / b) (Markstein's correction: q0 = RN(a r),
+// rem = a - q0 b exactly by FMA, q = RN(q0 + rem r)).  Three FP64 ops instead of the
+// ~10-op scaled division sequence; bit-identical to IEEE a / b (brute-forced on 2e8
+// random operand pairs incl. all-ones significands, tools/check_div_rn.c).
+__device__ __forceinline__ double div_rn(double a, double b, double r) {
+  const double q0 = a * r;
+  const double rem = __builtin_fma(-q0, b, a);
+  return __builtin_fma(rem, r, q0);
+}
 
 struct Geo {
   const float* depth;
@@ -74,7 +87,11 @@ struct Geo {
   const Tap* xt;
   const Tap* yt;
   int same;  // depth already at image resolution: app.py:187 skips cv2.resize
+  double sx, sy;  // cv2 inverse scales 1 / (out / in) per axis (host-computed, IEEE-identical)
 };
+
+// cv2's inverse scale for one axis (resize.cpp: scale_x = 1. / inv_scale_x, inv_scale_x = dsize / ssize)
+inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
   size_t state, hist, xtab, ytab, field, tmp, total;
@@ -171,8 +188,7 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
 }
 
 // cv2 resize.cpp INTER_LINEAR tap geometry (fx computed in double, cast to float).
-__device__ Tap make_tap(int dx, int in, int out) {
-  const double scale = 1.0 / ((double)out / (double)in);
+__device__ Tap make_tap(int dx, int in, double scale) {
   float fx = (float)(((double)dx + 0.5) * scale - 0.5);
   int sx = (int)floorf(fx);
   fx = fx - (float)sx;
@@ -189,7 +205,8 @@ __device__ Tap make_tap(int dx, int in, int out) {
 
 // ---------------------------------------------------------------- kernels
 
-__global__ void k_init(SelState* st, int B, int n, Tap* xt, Tap* yt, int dh, int dw, int H, int W) {
+__global__ void k_init(SelState* st, int B, int n, Tap* xt, Tap* yt, int dh, int dw, int H, int W, double sx,
+                       double sy) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid < B) {
     SelState s{};
@@ -202,12 +219,12 @@ __global__ void k_init(SelState* st, int B, int n, Tap* xt, Tap* yt, int dh, int
     st[tid] = s;
   }
   if (tid < W) {
-    Tap t = make_tap(tid, dw, W);
+    Tap t = make_tap(tid, dw, sx);
     if (dw == 1) { t.i0 = 0; t.i1 = -1; t.w0 = 1.f; t.w1 = 0.f; }
     xt[tid] = t;
   }
   if (tid < H) {
-    Tap t = make_tap(tid, dh, H);
+    Tap t = make_tap(tid, dh, sy);
     // vertical pass always uses two rows: the second clamps to the last row
     if (t.i1 < 0) t.i1 = t.i0;
     yt[tid] = t;
@@ -260,6 +277,8 @@ __device__ __forceinline__ float sample_rows(const Geo& g, const float* rows, in
   return h0 * ty.w0 + h1 * ty.w1;
 }
 
+// (Materialising the keys in the first sweep and streaming them in the later ones
+// was measured slower: the sweeps are bound by the histogram, not the resize.)
 template <int LEVEL, int PASS>
 __global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32_t* hist, int B, Sweep sw) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
@@ -431,6 +450,7 @@ __device__ void finalize_pct(SelState& s) {
   if (p98 > p2) {
     s.mode = branch;
     s.den64 = (p98 - p2) + 1e-6;
+    s.rden64 = 1.0 / s.den64;
     s.lo32 = (float)p2;
     s.hi32 = (float)p98;
     s.den32 = (float)((p98 - p2) + 1e-6);
@@ -534,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_resolve(SelState* st, uint32_t* 
 
 struct Norm {
   int mode, invert;
-  double p2, p98, den64;
+  double p2, p98, den64, rden64;
   float lo32, hi32, den32;
 };
 
@@ -545,6 +565,7 @@ __device__ __forceinline__ Norm load_norm(const SelState* S, int invert) {
   nm.p2 = S->p2;
   nm.p98 = S->p98;
   nm.den64 = S->den64;
+  nm.rden64 = S->rden64;
   nm.lo32 = S->lo32;
   nm.hi32 = S->hi32;
   nm.den32 = S->den32;
@@ -557,7 +578,7 @@ __device__ __forceinline__ double normalize(float val, const Norm& nm) {
     double d = (double)val;
     d = d < nm.p2 ? nm.p2 : d;          // np.clip -> min(max(x, lo), hi)
     d = d > nm.p98 ? nm.p98 : d;
-    d = (d - nm.p2) / nm.den64;
+    d = div_rn(d - nm.p2, nm.den64, nm.rden64);
     if (nm.invert) d = 1.0 - d;
     return d;
   }
@@ -572,15 +593,15 @@ __device__ __forceinline__ double normalize(float val, const Norm& nm) {
 }
 
 struct Cam {
-  double cx, cy, f, scale;
+  double cx, cy, f, rf, scale;   // rf = RN(1 / f)
   int step, Wn, N;
 };
 
 __device__ __forceinline__ void project(double d, int v, int u, const Cam& c, float& x, float& y, float& z) {
   const double zd = d * c.scale;                       // app.py:233
   const double zz = zd != 0.0 ? zd : 1e-6;             // app.py:234-235
-  x = (float)((((double)u - c.cx) * zz) / c.f);
-  y = (float)((((double)v - c.cy) * zz) / c.f);
+  x = (float)div_rn(((double)u - c.cx) * zz, c.f, c.rf);
+  y = (float)div_rn(((double)v - c.cy) * zz, c.f, c.rf);
   z = (float)zd;
 }
 
@@ -735,12 +756,12 @@ __global__ __launch_bounds__(kBlock) void k_unproject(Geo g, const SelState* st,
 }
 
 __device__ __forceinline__ Tap xtap(const Geo& g, int u) {
-  Tap t = make_tap(u, g.dw, g.W);
+  Tap t = make_tap(u, g.dw, g.sx);
   if (g.dw == 1) { t.i0 = 0; t.i1 = -1; t.w0 = 1.f; t.w1 = 0.f; }
   return t;
 }
 __device__ __forceinline__ Tap ytap(const Geo& g, int v) {
-  Tap t = make_tap(v, g.dh, g.H);
+  Tap t = make_tap(v, g.dh, g.sy);
   if (t.i1 < 0) t.i1 = t.i0;
   return t;
 }
@@ -750,7 +771,6 @@ __device__ __forceinline__ Tap ytap(const Geo& g, int v) {
 // the compiler never parks a wave on a divergent vmcnt(0); the RGB of both point
 // groups a thread owns is in flight before any arithmetic; cv2 taps are recomputed
 // in registers (no table loads).
-constexpr int kGroupsPerThread = 2;
 template <int STEP>
 __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState* st, const uint8_t* img, int B,
                                                            Sweep sw, int invert, Cam cam, float* xyz, uint8_t* rgb,
@@ -758,6 +778,9 @@ __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState
   extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
   float* rows = reinterpret_cast<float*>(smem_u);
   __shared__ uint32_t red[6][4];
+  __shared__ float4 sx[kBlock / 64][192];
+  __shared__ uint32_t sc[kBlock / 64][192];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int b, rb;
   map_rows(blockIdx.x, B, sw.nrb, b, rb);
   const SelState* S = st + b;
@@ -782,6 +805,8 @@ __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState
   const size_t img_base = (size_t)b * g.H * g.W;
   const float* dimg = g.depth + (size_t)b * g.dh * g.dw;
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  // groups of 4 points whose RGB a thread has in flight at once (3 dwords each at STEP 1)
+  constexpr int kGroupsPerThread = STEP == 1 ? 4 : 2;
   for (int base = 0; base < G; base += kGroupsPerThread * kBlock) {
     int row[kGroupsPerThread], ui0[kGroupsPerThread];
     uint32_t q[kGroupsPerThread][4][3];
@@ -846,16 +871,36 @@ __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int c = 0; c < 3; ++c) { mn[c] = fminf(mn[c], px[j][c]); mx[c] = fmaxf(mx[c], px[j][c]); }
-        const size_t o = (size_t)b * cam.N + (size_t)row[k] * cam.Wn + ui0[k];
-        float4* dst = reinterpret_cast<float4*>(xyz + o * 3);
-        dst[0] = make_float4(px[0][0], px[0][1], px[0][2], px[1][0]);
-        dst[1] = make_float4(px[1][1], px[1][2], px[2][0], px[2][1]);
-        dst[2] = make_float4(px[2][2], px[3][0], px[3][1], px[3][2]);
-        uint32_t* cd = reinterpret_cast<uint32_t*>(rgb + o * 3);
-        cd[0] = pc[0][0] | (pc[0][1] << 8) | (pc[0][2] << 16) | (pc[1][0] << 24);
-        cd[1] = pc[1][1] | (pc[1][2] << 8) | (pc[2][0] << 16) | (pc[2][1] << 24);
-        cd[2] = pc[2][2] | (pc[3][0] << 8) | (pc[3][1] << 16) | (pc[3][2] << 24);
       }
+      // The wave's 64 groups are 256 consecutive points: stage its 3 KB of xyz and 768 B of
+      // rgb through LDS so every store instruction writes one contiguous 1 KB / 256 B run
+      // (the direct per-lane 48 B / 12 B strided stores left 2/3 of each request empty).
+      float4* wx = sx[wid];
+      uint32_t* wc = sc[wid];
+      wx[lane * 3 + 0] = make_float4(px[0][0], px[0][1], px[0][2], px[1][0]);
+      wx[lane * 3 + 1] = make_float4(px[1][1], px[1][2], px[2][0], px[2][1]);
+      wx[lane * 3 + 2] = make_float4(px[2][2], px[3][0], px[3][1], px[3][2]);
+      wc[lane * 3 + 0] = pc[0][0] | (pc[0][1] << 8) | (pc[0][2] << 16) | (pc[1][0] << 24);
+      wc[lane * 3 + 1] = pc[1][1] | (pc[1][2] << 8) | (pc[2][0] << 16) | (pc[2][1] << 24);
+      wc[lane * 3 + 2] = pc[2][2] | (pc[3][0] << 8) | (pc[3][1] << 16) | (pc[3][2] << 24);
+      __builtin_amdgcn_wave_barrier();
+      const int wbase = base + k * kBlock + wid * 64;             // first group of this wave
+      const size_t o = (size_t)b * cam.N + (size_t)r0 * cam.Wn + (size_t)wbase * 4;
+      float4* dx = reinterpret_cast<float4*>(xyz + o * 3);
+      uint32_t* dc = reinterpret_cast<uint32_t*>(rgb + o * 3);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int f = q * 64 + lane;
+        if (wbase + f / 3 < G) {      // streamed once: non-temporal (no cache residency to keep)
+          const float4 vx = wx[f];
+          __builtin_nontemporal_store(vx.x, &dx[f].x);
+          __builtin_nontemporal_store(vx.y, &dx[f].y);
+          __builtin_nontemporal_store(vx.z, &dx[f].z);
+          __builtin_nontemporal_store(vx.w, &dx[f].w);
+          __builtin_nontemporal_store(wc[f], &dc[f]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   }
   uint32_t kk[6];
@@ -864,7 +909,6 @@ __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState
     kk[2 * c] = any ? f2key(mn[c]) : 0xffffffffu;
     kk[2 * c + 1] = any ? f2key(mx[c]) : 0u;
   }
-  const int wid = threadIdx.x >> 6;
   for (int c = 0; c < 6; ++c) {
     uint32_t x = (c & 1) ? wave_max_u32(kk[c]) : wave_min_u32(kk[c]);
     if ((threadIdx.x & 63) == 0) red[c][wid] = x;
@@ -997,6 +1041,8 @@ static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same
   }
   sw.R = std::max(1, R);
   sw.nrb = (rows_out + sw.R - 1) / sw.R;
+  // allocate only the window R output rows can span (not the whole budget): occupancy
+  if (cap_rows) cap_rows = std::min(cap_rows, (int)std::floor((double)(sw.R - 1) * step * dh / H) + 3);
   sw.lds_rows = cap_rows;
   return sw;
 }
@@ -1056,9 +1102,11 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
     return set_error(I2PC_ELAUNCH, "memset failed");
   const int n = img_h * img_w;
   const int init_threads = std::max(std::max(batch, img_h), img_w);
-  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, dep_h, dep_w, img_h, img_w);
+  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, dep_h, dep_w, img_h, img_w,
+                     cv_scale(dep_w, img_w), cv_scale(dep_h, img_h));
 
-  Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0};
+  Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
+        cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
   // selection sweeps: ~8 output rows per workgroup for 1024-wide images
   const int sel_rows = std::max(1, std::min(16, (8 * 1024 + img_w - 1) / img_w));
   const Sweep ssel = plan_sweep(img_h, 1, dep_h, dep_w, img_h, g.same != 0, sel_rows);
@@ -1076,6 +1124,7 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
   } else {
     cam.f = (double)std::max(img_w, img_h) * 1.2;     // app.py:223
   }
+  cam.rf = 1.0 / cam.f;
   cam.scale = params->depth_scale;
   cam.step = step;
   cam.Wn = (img_w + step - 1) / step;
@@ -1097,7 +1146,8 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
                        channels, batch, sunp, params->invert, cam, xyz, rgb, st);
   } else if (channels == 3 && cam.N % 4 == 0 && cam.Wn % 4 == 0) {
     // 2 rows of 1024 points (or the equivalent) per workgroup: 2 groups of 4 points per thread
-    const int fast_rows = std::max(1, std::min(kMaxRows, (2 * 1024 + cam.Wn - 1) / cam.Wn));
+    static const int pts_per_wg = [] { const char* e = getenv("I2PC_UNP_PTS"); return e ? atoi(e) : 8192; }();
+    const int fast_rows = std::max(1, std::min(16, (pts_per_wg + cam.Wn - 1) / cam.Wn));
     const Sweep sf = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, fast_rows);
     const size_t lf = sweep_lds(sf, dep_w);
     const dim3 grid(batch * sf.nrb), block(kBlock);
@@ -1145,8 +1195,8 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
     return set_error(I2PC_ELAUNCH, "memset failed");
   const int n = h * w;
   const int init_threads = std::max(std::max(batch, h), w);
-  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, h, w, h, w);
-  Geo g{depth, h, w, h, w, xt, yt, 1};
+  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, h, w, h, w, 1.0, 1.0);
+  Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
   const int sel_rows = std::max(1, std::min(16, (8 * 1024 + w - 1) / w));
   const Sweep ssel = plan_sweep(h, 1, h, w, h, true, sel_rows);
   int rc = launch_select<0>(g, st, hist, batch, ssel, s);
