@@ -77,18 +77,22 @@ def _images(batch, size, rank, device):
 def _kernel_profile(pipe, images):
     """One eager step with HIP events around every network launch + the geometry stage."""
     import torch
-    from image_to_pointcloud_amd import geometry, ops
+    from image_to_pointcloud_amd import _lib, geometry, ops
     ops.profile = []
     stream = torch.cuda.current_stream()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     pipe.pre(images, layout="patches", out=pipe._patches)
     depth = pipe.model(pipe._patches, pipe.batch)
+    lib = _lib.load()
+    lib.i2pc_profile_enable(1)
     e0.record(stream)
     geometry.unproject_batch(depth, images, density=pipe.density, invert=pipe.invert,
                              depth_scale=pipe.depth_scale, out=pipe._out)
     e1.record(stream)
     torch.cuda.synchronize()
+    unp_ms = lib.i2pc_profile_unproject_ms()
+    lib.i2pc_profile_enable(0)
     recs = ops.profile
     ops.profile = None
     per = {}
@@ -100,7 +104,7 @@ def _kernel_profile(pipe, images):
         d["flops"] += flops
         d["bytes"] += nbytes
     geo_t = e0.elapsed_time(e1) * 1e-3
-    return per, geo_t
+    return per, geo_t, (unp_ms * 1e-3 if unp_ms > 0 else None)
 
 
 def _cpu_baseline(spec, size, density):
@@ -195,10 +199,10 @@ def main():
     value = points_step * a.steps / elapsed / 1e6
     ms = elapsed / a.steps * 1e3
 
-    roofline = roof_geo = None
+    roofline = roof_geo = rooflines = None
     kernels = None
     if rank == 0 and not a.no_kernel_profile:
-        per, geo_t = _kernel_profile(pipe, images)
+        per, geo_t, unp_t = _kernel_profile(pipe, images)
         dom = max(per.items(), key=lambda kv: kv[1]["t"])
         name, d = dom
         if d["flops"] > 0:
@@ -217,6 +221,22 @@ def main():
                     "achieved": round(geo_bytes / geo_t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(geo_bytes / geo_t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                     "ms": round(geo_t * 1e3, 3), "bytes_per_step": geo_bytes}
+        rooflines = {"unproject_stage": roof_geo}
+        if unp_t:
+            a_unp = geo_bytes / unp_t / 1e9
+            rooflines["unproject_kernel"] = {
+                "kernel": "k_unproject_fast (back-projection + RGB gather + bbox)", "bound": "hbm",
+                "achieved": round(a_unp, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a_unp / HBM_PEAK_GBS, 4), "traffic": None, "us": round(unp_t * 1e6, 1),
+                "bytes_per_launch": geo_bytes, "bytes_per_point": 18.0,
+                "note": "algorithmic bytes 4*h'*w' + 18*N per image (SURVEY 8d), one launch per batch"}
+        net_t = sum(v["t"] for v in per.values())
+        net_f = sum(v["flops"] for v in per.values())
+        rooflines["dpt_blocks"] = {"kernel": "all network launches (GEMM/conv/attention/LN/resize/head)",
+                                   "bound": "mfma", "achieved": round(net_f / net_t / 1e12, 1),
+                                   "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                   "frac": round(net_f / net_t / 1e12 / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                                   "ms": round(net_t * 1e3, 3)}
         kernels = {k: {"launches": v["n"], "ms": round(v["t"] * 1e3, 3),
                        "tflops": round(v["flops"] / v["t"] / 1e12, 1) if v["flops"] else None}
                    for k, v in sorted(per.items(), key=lambda kv: -kv[1]["t"])}
@@ -244,7 +264,7 @@ def main():
                        "hip_graph": not a.no_graph},
             "network_tflops": round(flops_img * B * world / (elapsed / a.steps) / 1e12, 1),
             "roofline": roofline,
-            "roofline_unproject": roof_geo,
+            "rooflines": rooflines,
             "cpu_baseline": cpu,
             "kernels": kernels,
         }

@@ -48,6 +48,8 @@ _SIGNATURES = {
                                ctypes.POINTER(UnprojectParams), c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_size_t, c_void_p]),
     "i2pc_gather_stride": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "i2pc_profile_enable": (c_int, [c_int]),
+    "i2pc_profile_unproject_ms": (c_float, []),
 }
 
 _lib = None

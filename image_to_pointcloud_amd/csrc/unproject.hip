@@ -1068,6 +1068,37 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, cons
 using namespace i2pc;
 using namespace i2pc::unproj;
 
+// ---- profiling hook: HIP events around the unprojection kernel (bench.py's roofline)
+namespace {
+hipEvent_t g_prof_ev[2] = {nullptr, nullptr};
+bool g_prof_on = false;
+bool g_prof_recorded = false;
+void prof_mark(int i, hipStream_t s) {
+  if (!g_prof_on) return;
+  (void)hipEventRecord(g_prof_ev[i], s);
+  if (i == 1) g_prof_recorded = true;
+}
+}  // namespace
+
+extern "C" int i2pc_profile_enable(int on) {
+  clear_error();
+  if (on && !g_prof_ev[0]) {
+    for (auto& e : g_prof_ev)
+      if (hipEventCreate(&e) != hipSuccess) return set_error(I2PC_ELAUNCH, "hipEventCreate failed");
+  }
+  g_prof_on = on != 0;
+  g_prof_recorded = false;
+  return I2PC_OK;
+}
+
+extern "C" float i2pc_profile_unproject_ms(void) {
+  if (!g_prof_recorded) return -1.f;
+  float ms = -1.f;
+  if (hipEventSynchronize(g_prof_ev[1]) != hipSuccess) return -1.f;
+  if (hipEventElapsedTime(&ms, g_prof_ev[0], g_prof_ev[1]) != hipSuccess) return -1.f;
+  return ms;
+}
+
 extern "C" size_t i2pc_unproject_workspace_bytes(int batch, int img_h, int img_w, int smooth) {
   if (batch <= 0 || img_h <= 0 || img_w <= 0) return 0;
   return layout(batch, img_h, img_w, smooth).total;
@@ -1145,18 +1176,20 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
     hipLaunchKernelGGL((k_unproject<true>), dim3(batch * sunp.nrb), dim3(kBlock), 0, s, g, st, field, image,
                        channels, batch, sunp, params->invert, cam, xyz, rgb, st);
   } else if (channels == 3 && cam.N % 4 == 0 && cam.Wn % 4 == 0) {
-    // 2 rows of 1024 points (or the equivalent) per workgroup: 2 groups of 4 points per thread
+    // 8 rows of 1024 points (or the equivalent) per workgroup
     static const int pts_per_wg = [] { const char* e = getenv("I2PC_UNP_PTS"); return e ? atoi(e) : 8192; }();
     const int fast_rows = std::max(1, std::min(16, (pts_per_wg + cam.Wn - 1) / cam.Wn));
     const Sweep sf = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, fast_rows);
     const size_t lf = sweep_lds(sf, dep_w);
     const dim3 grid(batch * sf.nrb), block(kBlock);
+    prof_mark(0, s);
     if (step == 1)
       hipLaunchKernelGGL((k_unproject_fast<1>), grid, block, lf, s, g, st, image, batch, sf, params->invert, cam, xyz, rgb, st);
     else if (step == 2)
       hipLaunchKernelGGL((k_unproject_fast<2>), grid, block, lf, s, g, st, image, batch, sf, params->invert, cam, xyz, rgb, st);
     else
       hipLaunchKernelGGL((k_unproject_fast<4>), grid, block, lf, s, g, st, image, batch, sf, params->invert, cam, xyz, rgb, st);
+    prof_mark(1, s);
   } else {
     hipLaunchKernelGGL((k_unproject<false>), dim3(batch * sunp.nrb), dim3(kBlock), unp_lds, s, g, st, field, image,
                        channels, batch, sunp, params->invert, cam, xyz, rgb, st);

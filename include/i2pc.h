@@ -93,6 +93,14 @@ int i2pc_unproject(const float* depth, int dep_h, int dep_w,
 int i2pc_depth_preview(const float* depth, int batch, int h, int w, int invert, const uint8_t* lut_bgr,
                        uint8_t* out_bgr, double* stats, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Profiling hook (bench.py's roofline): while enabled, i2pc_unproject records two HIP
+ * events on its stream around the unprojection kernel (the HBM-bound back-projection +
+ * RGB gather + bbox launch, when the fast layout applies), and
+ * i2pc_profile_unproject_ms() returns that kernel's duration of the last such call
+ * (synchronising on the stop event), or -1 if none was recorded. Not thread-safe. */
+int i2pc_profile_enable(int on);
+float i2pc_profile_unproject_ms(void);
+
 /* Gather every stride-th point (preview subsample, app.py:496-506):
  * out_xyz/out_rgb [count] with count = ceil(n / stride). */
 int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,
