@@ -16,6 +16,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace i2pc {
 namespace attn {
@@ -209,6 +210,182 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_attention_tr: same decomposition, with
+//  * V staged like K (global_load_lds, row-major [key][d] image, 128-B rows) and read
+//    with ds_read_b64_tr_b16 (gfx950's transposing LDS read) straight into the
+//    V^T A-operand -- no register round trip, no 16 ds_write_b16 per thread per tile;
+//    chunk swizzle ((row >> 1) & 1) << 2 keeps the transposed reads conflict-free;
+//  * the 1/sqrt(d) * log2(e) scale folded into the exponent (one FMA per score:
+//    p = exp2(s*c - m*c), max taken on the raw scores since c > 0);
+//  * key masking only on the last tile, and a last tile of <= 32 keys computes one
+//    32-key half (T = 577 = 9*64 + 1: the tail was a whole wasted 64-key tile);
+//  * waves whose 32 query rows are all beyond T skip the MFMA/softmax work.
+__device__ __forceinline__ int v_swz(int row) { return ((row >> 1) & 1) << 2; }
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4s tr_read(const uint8_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+__global__ __launch_bounds__(256, 2) void k_attention_tr(const bf16_t* __restrict__ qkv, int B, int T, int NH,
+                                                         float scale_log2, bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * kTileBytes];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int qtiles = (T + kQ - 1) / kQ;
+  int bid = blockIdx.x;
+  const int qt = bid % qtiles;
+  bid /= qtiles;
+  const int h = bid % NH;
+  const int b = bid / NH;
+  const int D = NH * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const bf16_t* Qg = qkv + (int64_t)b * T * ld + h * 64;
+  const bf16_t* Kg = Qg + D;
+  const bf16_t* Vg = Qg + 2 * D;
+
+  const int hh = lane >> 5;
+  const int lq = lane & 31;
+  const int q = qt * kQ + wid * 32 + lq;
+  const int qc = min(q, T - 1);
+  const bool wave_active = qt * kQ + wid * 32 < T;      // wave-uniform
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qg + qc * ld + 16 * s + 8 * hh);
+
+  // K and V glds: 8 wave-instructions per tile each (8 keys x 128 B), 2 + 2 per wave
+  auto stage = [&](int buf, int kt) {
+    uint8_t* sK = smem + buf * 2 * kTileBytes;
+    uint8_t* sV = sK + kTileBytes;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (wid * 2 + j) * 8 + (lane >> 3);
+      const int pchunk = lane & 7;
+      const int key = min(kt * kKV + row, T - 1);
+      glds16(Kg + key * ld + (pchunk ^ (row & 7)) * 8, sK + (wid * 2 + j) * 8 * 128);
+      glds16(Vg + key * ld + (pchunk ^ v_swz(row)) * 8, sV + (wid * 2 + j) * 8 * 128);
+    }
+  };
+
+  f32x16 o[2];
+  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+  float m_run = -INFINITY, l_run = 0.f;          // m_run on the raw (unscaled) scores
+  const float c = scale_log2;
+
+  // transposed-read lane geometry: 16-lane group g, lane 4q'+p inside it
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int nt = (T + kKV - 1) / kKV;
+  stage(0, 0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) stage(cur ^ 1, kt + 1);
+    const uint8_t* sK = smem + cur * 2 * kTileBytes;
+    const uint8_t* sV = sK + kTileBytes;
+    const int kbase = kt * kKV;
+    const int nvalid = T - kbase;                  // keys of this tile that exist (>= 1)
+    const bool half = nvalid <= 32;                // uniform: one 32-key half suffices
+    if (wave_active) {
+      f32x16 st[2];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        if (k2 == 1 && half) break;
+        for (int i = 0; i < 16; ++i) st[k2][i] = 0.f;
+        const int key = 32 * k2 + lq;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int lchunk = 2 * s + hh;
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ (key & 7)) << 4));
+          st[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[k2], 0, 0, 0);
+        }
+      }
+      if (half) for (int i = 0; i < 16; ++i) st[1][i] = -INFINITY;
+      if (nvalid < kKV) {                          // last tile only
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = 32 * k2 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= nvalid) st[k2][r] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[k2][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2f((m_run - m_new) * c);
+      const float mc = m_new * c;
+      m_run = m_new;
+      float ls = 0.f;
+      uint32_t pk[2][8];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const float p0 = exp2f(__builtin_fmaf(st[k2][r], c, -mc));
+          const float p1 = exp2f(__builtin_fmaf(st[k2][r + 1], c, -mc));
+          ls += p0 + p1;
+          pk[k2][r >> 1] = pack_bf16(p0, p1);
+        }
+      l_run = l_run * alpha + ls;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+      // O^T += V^T P^T over 16-key steps; V^T fragments by transposed reads
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        if (k2 == 1 && half) break;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pf;
+          {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 u = {pk[k2][4 * s + 0], pk[k2][4 * s + 1], pk[k2][4 * s + 2], pk[k2][4 * s + 3]};
+            pf = __builtin_bit_cast(bf16x8, u);
+          }
+          // P's k order (swapped S^T layout): elements 0-3 = keys kb..kb+3, 4-7 = kb+8..kb+11
+          const int kb = 32 * k2 + 16 * s + 4 * (tg >> 1);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int d0 = 32 * dt + 16 * (tg & 1) + 4 * tp;      // logical column of this lane's address
+            const int lch = d0 >> 3, within = (d0 & 7) * 2;
+            const int r0 = kb + tq, r1 = kb + 8 + tq;
+            const v4s lo = tr_read(sV + r0 * 128 + ((lch ^ v_swz(r0)) << 4) + within);
+            const v4s hi = tr_read(sV + r1 * 128 + ((lch ^ v_swz(r1)) << 4) + within);
+            typedef short v8s __attribute__((ext_vector_type(8)));
+            const v8s u = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, u);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  const float inv = 1.0f / l_tot;
+  if (q < T) {
+    bf16_t* orow = out + ((int64_t)b * T + q) * D + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * hh;
+        uint2 w;
+        w.x = pack_bf16(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        w.y = pack_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d) = w;
+      }
+  }
+}
+
 }  // namespace attn
 }  // namespace i2pc
 
@@ -220,7 +397,12 @@ extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads,
   I2PC_REQUIRE(batch > 0 && tokens > 0 && heads > 0, "attention: empty shape");
   const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
   const float scale_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn::k_attention, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+  static const int old_kernel = [] { const char* e = getenv("I2PC_ATTN_OLD"); return e ? atoi(e) : 0; }();
+  if (old_kernel)
+    hipLaunchKernelGGL(attn::k_attention, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+  else
+    hipLaunchKernelGGL(attn::k_attention_tr, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
   return check_launch("attention");
 }

@@ -663,17 +663,14 @@ __global__ __launch_bounds__(512) void k_gemm8(Args p) {
 #undef I2PC_BAR
 #undef I2PC_VMCNT
 
-  // epilogue: wave (wm, wn) holds rows wm*128 + i*16, cols wn*64 + j*16
+  // epilogue: wave (wm, wn) holds rows wm*128 + i*16, cols wn*64 + j*16 (the generic
+  // kernel's 128 x 64 wave tile), staged through LDS in two passes of 4 m-tiles
+  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + frow;
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + fq * 4;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      epilogue4(p, m, n, v);
-    }
+  for (int i0 = 0; i0 < 8; i0 += 4) {
+    tile_epilogue<8, 4>(p, acc, i0, 4, m0 + wm * 128, n0 + wn * 64,
+                        reinterpret_cast<float*>(smem) + wid * 4 * 16 * 64);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

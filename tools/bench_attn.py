@@ -1,0 +1,15 @@
+"""Attention microbenchmark on the DPT-Large / DA-small shapes (I2PC_ATTN_OLD=1 selects the previous kernel)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from image_to_pointcloud_amd import ops
+for B, T, H in [(32, 577, 16), (32, 1370, 6), (8, 1370, 6)]:
+    qkv = (torch.randn(B * T, 3 * H * 64, device="cuda") * 1.5).to(torch.bfloat16)
+    out = torch.empty(B * T, H * 64, dtype=torch.bfloat16, device="cuda")
+    ops.attention(qkv, B, T, H, 0.125, out=out); torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20): ops.attention(qkv, B, T, H, 0.125, out=out)
+    e1.record(); torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 20 * 1e-3
+    print(f"old={os.environ.get('I2PC_ATTN_OLD', '0')} B={B} T={T} H={H}: {t*1e6:8.1f} us {4*B*H*T*T*64/t/1e12:6.1f} TF")
