@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu -x > gpurun_out/t_all.log 2>&1 || { echo tests_failed; tail -40 gpurun_out/t_all.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/t_all.log 2>&1 || { echo tests_failed; tail -40 gpurun_out/t_all.log; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke_failed; tail -20 gpurun_out/smoke.log; exit 1; }
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench_failed; tail -20 gpurun_out/bench.err; exit 1; }
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
