@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace i2pc {
 namespace gemm {
@@ -33,7 +34,7 @@ typedef uint16_t bf16_t;
 
 constexpr int BK = 64;
 
-__device__ __attribute__((aligned(16))) uint8_t g_zero[512];   // conv zero padding source
+__device__ __attribute__((aligned(16))) uint8_t g_zero[1024];  // conv zero padding / absent-bias source
 #ifdef I2PC_STAMPS
 // diagnostic build only: per-block s_memtime stamps (start, after prologue, after K loop, end)
 __device__ unsigned long long g_stamps[65536 * 8];
@@ -45,8 +46,18 @@ __device__ unsigned long long g_stamps[65536 * 8];
       g_stamps[blockIdx.x * 8 + (k)] = t;                                             \
     }                                                                                 \
   } while (0)
+// persistent engine: per (block, tile ordinal < 8) four stamps
+#define PSTAMP(ti, k)                                                                 \
+  do {                                                                                \
+    if (threadIdx.x == 0 && (ti) < 8) {                                               \
+      unsigned long long t_;                                                          \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+      g_stamps[(blockIdx.x * 8 + (ti)) * 8 + (k)] = t_;                               \
+    }                                                                                 \
+  } while (0)
 #else
 #define STAMP(k) do {} while (0)
+#define PSTAMP(ti, k) do {} while (0)
 #endif
 
 struct Args {
@@ -65,6 +76,7 @@ struct Args {
   int ct_s, ct_h, ct_w, ct_c;
   int tiles_m, tiles_n;
   int group_m;
+  uint32_t a_bytes, w_bytes;   // buffer ranges of A and W (persistent engine)
 };
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
@@ -77,7 +89,22 @@ __device__ __forceinline__ bf16_t f2bf(float x) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// GELU with the exact (erf) form, erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far
+// below the bf16 rounding of the output): one reciprocal, one exp2, six FMAs instead of
+// ocml's branchy erff (which made the fc1 epilogue cost ~half a K-loop).
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  y *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+  const float erf_abs = fmaf(-y, e, 1.0f);
+  const float erf_v = __builtin_copysignf(erf_abs, x);
+  return 0.5f * x * (1.0f + erf_v);
+}
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_base), 16, 0, 0);
@@ -439,7 +466,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
 
   // ---- epilogue through this wave's LDS region (the K loop ended with a barrier)
   constexpr int EP_RM0 = (2 * STAGE) / (NW * TN * 4 * 16);   // m-tiles per pass that fit
-  constexpr int EP_RM = EP_RM0 < RM ? EP_RM0 : RM;
+  constexpr int EP_RM1 = EP_RM0 < RM ? EP_RM0 : RM;
+  constexpr int EP_RM = RM % EP_RM1 == 0 ? EP_RM1 : RM % (EP_RM1 - 1) == 0 ? EP_RM1 - 1
+                      : RM % (EP_RM1 - 2) == 0 ? EP_RM1 - 2 : 1;   // largest divisor of RM that fits
   static_assert(EP_RM >= 1 && RM % EP_RM == 0, "epilogue LDS");
 #pragma unroll
   for (int i0 = 0; i0 < RM; i0 += EP_RM) {
@@ -467,345 +496,402 @@ static void launch(const Args& p, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// 256 x 256 x 64 tile, 8 waves (2 M x 4 N, 128 x 64 outputs per wave), 8 phases
-// per pair of K-tiles (cdna_hip_programming.md §5 "256^2 8-phase template",
-// re-derived for this layout).  Each K-tile buffer is four 16 KiB half-tiles:
-//   A0/A1 = the first/second 64 activation rows of every wave's 128,
-//   B0/B1 = the first/second 32 weight rows of every wave's 64.
-// Phase q (1..4) of a K-tile computes C-quadrant Q_q = (A0,B0) (A0,B1) (A1,B1)
-// (A1,B0) from register subtiles, so half-tiles retire early and are refilled
-// one phase after their last ds_read:
-//   phase 1: read A0,B0 | glds odd.A1 (tile t+1)     phase 5: read A0,B0 (odd) | glds even.A1 (t+2)
-//   phase 2: read B1    | glds even.A0 (t+2)         phase 6: read B1          | glds odd.A0 (t+3)
-//   phase 3: read A1    | glds even.B0 (t+2)         phase 7: read A1          | glds odd.B0 (t+3)
-//   phase 4: -          | glds even.B1, vmcnt(6)     phase 8: -                | glds odd.B1, vmcnt(6)
-// Every phase: reads, glds, [vmcnt], lgkmcnt(0), s_barrier, 16 MFMA, s_barrier.
-// The counted vmcnt(6) keeps three half-tiles in flight across the barriers.
-template <bool CONV, bool RELU_A>
-__global__ __launch_bounds__(512) void k_gemm8(Args p) {
-  constexpr int HALF = 128 * 128;            // bytes per half-tile
-  constexpr int BUF = 4 * HALF;              // A0 A1 B0 B1
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wm = wid >> 2;                   // 0..1
-  const int wn = wid & 3;                    // 0..3
+// Persistent 256-column GEMM (BM x 256 x 64 tiles, BM = 256 or 320, 8 waves as
+// 2 M x 4 N, wave tile (BM/2) x 64).  One workgroup per CU walks a strided list
+// of tiles (XCD-contiguous slots, GROUP_M order inside a round).  What it hides
+// that the one-tile-per-workgroup kernel cannot:
+//  * the next tile's first K-stage (and its bias row) is issued by
+//    global_load_lds during the current tile's last K-step, so no tile starts
+//    cold;
+//  * the epilogue is register-direct (no LDS round trip; bf16 pairs widened to
+//    16-B stores with v_permlane16_swap) through buffer stores whose count per
+//    wave is fixed, so the next tile's first wait is a counted vmcnt that lets
+//    those stores drain behind the next tile's MFMAs instead of stalling on them;
+//  * residual operands are read by inline-asm buffer loads one m-subtile ahead
+//    with counted waits, so they never wait for the stores issued before them.
+// Every epilogue memory operation is unconditional (rows past M go to an
+// out-of-range buffer offset: loads read 0, stores are dropped), which is what
+// makes the counted waits exact.
+namespace pers {
 
-  int tm, tn;
-  tile_coords(p, blockIdx.x, tm, tn);
-  const int m0 = tm * 256;
-  const int n0 = tn * 256;
+enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4 };
+constexpr int OOB = 0x7FFFFFF0;   // buffer range; offsets >= OOB are dropped / read as 0
 
-  // per-lane glds sources.  Lane fills local row lr0 = wid*16 + lane/8 (+8 for slab 1) of
-  // every half; A half h local row wm'*64 + r <-> tile row wm'*128 + h*64 + r, B half h
-  // local row wn'*32 + c <-> weight row wn'*64 + h*32 + c.  Dense rows are affine in
-  // (h, slab) (the dispatcher sends row-remapped A to the 128-row kernel), so one base
-  // pointer per operand suffices; conv rows keep (pixel base, y, x) per (h, slab).
-  const int pchunk = lane & 7;
-  const int lr0 = wid * 16 + (lane >> 3);                 // slab 0 row; slab 1 = +8 (same lr>>6, lr>>5)
-  const int lchunk0 = pchunk ^ (lr0 & 7);                 // (lr0 + 8) & 7 == lr0 & 7
-  const bf16_t* a_base;
-  int cpix[2][2], cyx[2][2];
-  {
-    const int mrow = m0 + (lr0 >> 6) * 128 + (lr0 & 63);
-    if (!CONV) {
-      a_base = p.A + (int64_t)(mrow + p.a_o) * p.lda + lchunk0 * 8;
-    } else {
-      a_base = p.A + lchunk0 * 8;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          int m = mrow + h * 64 + j * 8;
-          if (m > p.M - 1) m = p.M - 1;
-          const int hw = p.coh * p.cow;
-          const int b = m / hw;
-          const int rem = m - b * hw;
-          const int oy = rem / p.cow;
-          const int ox = rem - oy * p.cow;
-          cpix[h][j] = b * p.ch * p.cw;
-          cyx[h][j] = ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff);
-        }
-    }
-  }
-  const bf16_t* w_base = p.W + (int64_t)(n0 + (lr0 >> 5) * 64 + (lr0 & 31)) * p.ldw + lchunk0 * 8;
-  const int64_t a_step_h = (int64_t)64 * p.lda, a_step_j = (int64_t)8 * p.lda;
-  const int64_t w_step_h = (int64_t)32 * p.ldw, w_step_j = (int64_t)8 * p.ldw;
-  const int m_last = p.M - 1;
-  const int row_hi = m0 + (lr0 >> 6) * 128 + (lr0 & 63);   // for dense row clamping
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-  // glds of one half-tile (2 instructions per thread); which: 0 A0, 1 A1, 2 B0, 3 B1
-  auto stage_half = [&](int buf, int which, int k0) {
-    uint8_t* dst = smem + buf * BUF + which * HALF;
-    const int h = which & 1;
-    if (which < 2) {
-      if (!CONV) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int m = row_hi + h * 64 + j * 8;
-          const bf16_t* src = m <= m_last ? a_base + h * a_step_h + j * a_step_j
-                                          : a_base + (int64_t)(m_last - row_hi) * p.lda;
-          glds16(src + k0, dst + (wid * 2 + j) * 8 * 128);
-        }
-      } else {
-        const int kk = k0 / p.cc;
-        const int ky = kk / p.ck;
-        const int kx = kk - ky * p.ck;
-        const int ci0 = k0 - kk * p.cc;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int yi = (cyx[h][j] >> 16) + ky, xi = ((int)(short)(cyx[h][j] & 0xffff)) + kx;
-          const bool ok = yi >= 0 && yi < p.ch && xi >= 0 && xi < p.cw;
-          const void* src = ok ? (const void*)(a_base + ((int64_t)cpix[h][j] + (int64_t)yi * p.cw + xi) * p.cc + ci0)
-                               : (const void*)(g_zero + pchunk * 16);
-          glds16(src, dst + (wid * 2 + j) * 8 * 128);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) glds16(w_base + h * w_step_h + j * w_step_j + k0, dst + (wid * 2 + j) * 8 * 128);
-    }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int frow = lane & 15;
-  const int fq = lane >> 4;
-  bf16x8 af[2][4];     // A subtile: [substep][m-tile of the quadrant]
-  bf16x8 b0f[2][2], b1f[2][2];
-
-  auto read_a = [&](int buf, int h) {
-    const uint8_t* base = smem + buf * BUF + h * HALF;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int lr = wm * 64 + i * 16 + frow;
-        bf16x8 v = *reinterpret_cast<const bf16x8*>(base + lr * 128 + (((4 * s + fq) ^ (lr & 7)) << 4));
-        if (RELU_A) v = relu8(v);
-        af[s][i] = v;
-      }
-  };
-  auto read_b = [&](int buf, int h, bf16x8 (&bf)[2][2]) {
-    const uint8_t* base = smem + buf * BUF + (2 + h) * HALF;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int lr = wn * 32 + j * 16 + frow;
-        bf[s][j] = *reinterpret_cast<const bf16x8*>(base + lr * 128 + (((4 * s + fq) ^ (lr & 7)) << 4));
-      }
-  };
-  auto mma = [&](int mh, int nh, const bf16x8 (&bf)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[mh * 4 + i][nh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[s][j], af[s][i], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-#define I2PC_BAR()                             \
-  do {                                         \
-    __builtin_amdgcn_sched_barrier(0);         \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-    __builtin_amdgcn_s_barrier();              \
-    __builtin_amdgcn_sched_barrier(0);         \
-  } while (0)
-#define I2PC_VMCNT(n)                          \
-  do {                                         \
-    __builtin_amdgcn_sched_barrier(0);         \
-    asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); \
-  } while (0)
-
-  const int nk = p.K / BK;        // even (checked by the dispatcher)
-  // prologue: tile 0 complete, tile 1 A0 B0 B1 in flight
-  stage_half(0, 0, 0); stage_half(0, 2, 0); stage_half(0, 3, 0); stage_half(0, 1, 0);
-  if (nk > 1) { stage_half(1, 0, BK); stage_half(1, 2, BK); stage_half(1, 3, BK); I2PC_VMCNT(6); }
-  else { I2PC_VMCNT(0); }
-  I2PC_BAR();
-
-  for (int t = 0; t < nk; t += 2) {
-    const bool more = t + 2 < nk;                 // tiles t+2, t+3 exist
-    const int k2 = (t + 2) * BK, k3 = (t + 3) * BK;
-    // ---- even buffer (tile t)
-    read_a(0, 0); read_b(0, 0, b0f);
-    stage_half(1, 1, (t + 1) * BK);
-    I2PC_BAR(); mma(0, 0, b0f); I2PC_BAR();
-    read_b(0, 1, b1f);
-    if (more) stage_half(0, 0, k2);
-    I2PC_BAR(); mma(0, 1, b1f); I2PC_BAR();
-    read_a(0, 1);
-    if (more) stage_half(0, 2, k2);
-    I2PC_BAR(); mma(1, 1, b1f); I2PC_BAR();
-    if (more) { stage_half(0, 3, k2); I2PC_VMCNT(6); } else { I2PC_VMCNT(0); }
-    I2PC_BAR(); mma(1, 0, b0f); I2PC_BAR();
-    // ---- odd buffer (tile t+1)
-    read_a(1, 0); read_b(1, 0, b0f);
-    if (more) stage_half(0, 1, k2);
-    I2PC_BAR(); mma(0, 0, b0f); I2PC_BAR();
-    read_b(1, 1, b1f);
-    if (more) stage_half(1, 0, k3);
-    I2PC_BAR(); mma(0, 1, b1f); I2PC_BAR();
-    read_a(1, 1);
-    if (more) stage_half(1, 2, k3);
-    I2PC_BAR(); mma(1, 1, b1f); I2PC_BAR();
-    if (more) { stage_half(1, 3, k3); I2PC_VMCNT(6); } else { I2PC_VMCNT(0); }
-    I2PC_BAR(); mma(1, 0, b0f); I2PC_BAR();
-  }
-#undef I2PC_BAR
-#undef I2PC_VMCNT
-
-  // epilogue: wave (wm, wn) holds rows wm*128 + i*16, cols wn*64 + j*16 (the generic
-  // kernel's 128 x 64 wave tile), staged through LDS in two passes of 4 m-tiles
-  __syncthreads();
-#pragma unroll
-  for (int i0 = 0; i0 < 8; i0 += 4) {
-    tile_epilogue<8, 4>(p, acc, i0, 4, m0 + wm * 128, n0 + wn * 64,
-                        reinterpret_cast<float*>(smem) + wid * 4 * 16 * 64);
-    __builtin_amdgcn_wave_barrier();
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
   }
 }
 
-// ---------------------------------------------------------------------------
-// 256 x 256 x 32 tile, 8 waves (2 M x 4 N; 128 x 64 outputs per wave), a ring of
-// four 32 KiB LDS stages with THREE K-steps of global_load_lds in flight: the
-// load of step k+3 is issued before step k computes and only step k+1 is waited
-// for (counted vmcnt), so L2-miss / MALL latency (~1 us under load) hides behind
-// ~3 K-steps of MFMA work (the 2-stage 128^2 kernel stalls on every step).
-// Rows are 64 B (32 bf16); fragments read with ds_read_b128 through the
-// conflict-free swizzle chunk ^ ((row >> 1) & 3), applied to the glds SOURCE.
-template <bool CONV, bool RELU_A>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_gemm_ring(Args p) {
-  constexpr int RBK = 32;
-  constexpr int ROWB = RBK * 2;              // 64 B per row
-  constexpr int PART = 256 * ROWB;           // 16 KiB (A or W of one stage)
-  constexpr int STG = 2 * PART;              // 32 KiB
-  constexpr int NST = 4;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* ptr) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), 0, OOB, 0x00020000);
+}
+
+__device__ __forceinline__ void grouped(const Args& p, int tile, int& tm, int& tn) {
+  const int gsz = p.group_m * p.tiles_n;
+  const int g = tile / gsz;
+  const int first = g * p.group_m;
+  const int gm = min(p.tiles_m - first, p.group_m);
+  const int in = tile - g * gsz;
+  tm = first + in % gm;
+  tn = in / gm;
+}
+
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float x) {
+  if constexpr (ACT == 1) return gelu_erf(x);
+  else if constexpr (ACT == 2) return fmaxf(x, 0.f);
+  else return x;
+}
+
+// Byte offset of output element (m, n) (row remap or ConvTranspose pixel shuffle).
+__device__ __forceinline__ int out_elem(const Args& p, int m, int n, int64_t ld, bool ct) {
+  if (ct) {
+    const int hw = p.ct_h * p.ct_w;
+    const int bi = m / hw;
+    const int rem = m - bi * hw;
+    const int iy = rem / p.ct_w;
+    const int ix = rem - iy * p.ct_w;
+    const int tap = n / p.ct_c;
+    const int co = n - tap * p.ct_c;
+    const int dy = tap / p.ct_s, dx = tap - dy * p.ct_s;
+    const int W2 = p.ct_w * p.ct_s;
+    return (((bi * p.ct_h + iy) * p.ct_s + dy) * W2 + ix * p.ct_s + dx) * p.ct_c + co;
+  }
+  return remap(m, p.o_g, p.o_gs, p.o_o) * (int)ld + n;
+}
+
+#define I2PC_WAIT_VM(n)                                      \
+  do {                                                       \
+    __builtin_amdgcn_sched_barrier(0);                       \
+    asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory");    \
+  } while (0)
+#define I2PC_LDS_BARRIER()                                   \
+  do {                                                       \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
+    __builtin_amdgcn_s_barrier();                            \
+    __builtin_amdgcn_sched_barrier(0);                       \
+  } while (0)
+
+template <int EPI> struct EpiCount {
+  static constexpr int loads = EPI == EPI_RESF32 || EPI == EPI_RESBF16 ? 4 : EPI == EPI_RES2 ? 8 : 0;
+  static constexpr int stores = EPI == EPI_RESF32 ? 4 : 2;
+};
+
+// Register-direct tile epilogue of the persistent engines for one wave: rows mw0 + i*16 + (lane & 15),
+// columns ncol + j*16 + (lane >> 4)*4 (the swapped 16x16x32 MFMA layout).  Issues exactly
+// RM * (loads + stores) vector-memory instructions (EpiCount), all unconditional.
+template <int RM, int EPI>
+__device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][4], int mw0, int ncol, const float* bias_lds,
+                                           rsrc_t c_rs, rsrc_t r_rs, rsrc_t r2_rs) {
+    constexpr int RN = 4;
+    constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
+    const int lane = threadIdx.x & 63;
+    const int frow = lane & 15, fq = lane >> 4;
+    float4 bias4[RN];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bias4[j] = *reinterpret_cast<const float4*>(bias_lds + fq * 4 + j * 16);
+    const int mrow = mw0 + frow;       // + i * 16
+    const int act = p.act;
+    constexpr bool CT = EPI == EPI_CT;
+    constexpr bool OUTF = EPI == EPI_RESF32;
+    // residual loads of m-subtile i into slot i & 1 (acc layout: 4 columns per lane)
+    f32x4 rf[2][RN];
+    u32x2 rb[2][RN], rb2[2][RN];
+    auto load_res = [&](int i, int slot) {
+      const int m = mrow + i * 16;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int n = ncol + j * 16 + fq * 4;
+        if constexpr (EPI == EPI_RESF32) {
+          const int off = m < p.M ? (remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldr + n) * 4 : OOB;
+          asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(rf[slot][j]) : "v"(off), "s"(r_rs) : "memory");
+        }
+        if constexpr (EPI == EPI_RESBF16 || EPI == EPI_RES2) {
+          const int off = m < p.M ? (remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldr + n) * 2 : OOB;
+          asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(rb[slot][j]) : "v"(off), "s"(r_rs) : "memory");
+        }
+        if constexpr (EPI == EPI_RES2) {
+          const int off = m < p.M ? (remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldr2 + n) * 2 : OOB;
+          asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(rb2[slot][j]) : "v"(off), "s"(r2_rs) : "memory");
+        }
+      }
+    };
+    // one straight-line copy of the epilogue per activation
+    auto epilogue = [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
+    if constexpr (NRL > 0) load_res(0, 0);
+    static_for<0, RM>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int slot = i & 1;
+      if constexpr (NRL > 0) {
+        if constexpr (i + 1 < RM) load_res(i + 1, slot ^ 1);
+        constexpr int after = (i + 1 < RM ? NRL : 0) + (i > 0 ? NS : 0);
+        if constexpr (EPI == EPI_RESF32)
+          asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rf[slot][0]), "+v"(rf[slot][1]), "+v"(rf[slot][2]), "+v"(rf[slot][3])
+                       : "i"(after) : "memory");
+        else if constexpr (EPI == EPI_RESBF16)
+          asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb[slot][2]), "+v"(rb[slot][3])
+                       : "i"(after) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%c8)"
+                       : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb[slot][2]), "+v"(rb[slot][3]),
+                         "+v"(rb2[slot][0]), "+v"(rb2[slot][1]), "+v"(rb2[slot][2]), "+v"(rb2[slot][3])
+                       : "i"(after) : "memory");
+      }
+      const int m = mrow + i * 16;
+      const bool ok = m < p.M;
+      float v[RN][4];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        v[j][0] = act_f<ACT>(acc[i][j][0] + bias4[j].x);
+        v[j][1] = act_f<ACT>(acc[i][j][1] + bias4[j].y);
+        v[j][2] = act_f<ACT>(acc[i][j][2] + bias4[j].z);
+        v[j][3] = act_f<ACT>(acc[i][j][3] + bias4[j].w);
+        if constexpr (EPI == EPI_RESF32) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[j][e] += rf[slot][j][e];
+        }
+        if constexpr (EPI == EPI_RESBF16 || EPI == EPI_RES2) {
+          v[j][0] += __uint_as_float(rb[slot][j].x << 16); v[j][1] += __uint_as_float(rb[slot][j].x & 0xffff0000u);
+          v[j][2] += __uint_as_float(rb[slot][j].y << 16); v[j][3] += __uint_as_float(rb[slot][j].y & 0xffff0000u);
+        }
+        if constexpr (EPI == EPI_RES2) {
+          v[j][0] += __uint_as_float(rb2[slot][j].x << 16); v[j][1] += __uint_as_float(rb2[slot][j].x & 0xffff0000u);
+          v[j][2] += __uint_as_float(rb2[slot][j].y << 16); v[j][3] += __uint_as_float(rb2[slot][j].y & 0xffff0000u);
+        }
+      }
+      if constexpr (OUTF) {
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const int off = ok ? out_elem(p, m, ncol + j * 16 + fq * 4, p.ldc, false) * 4 : OOB;
+          const u32x4 d = {__float_as_uint(v[j][0]), __float_as_uint(v[j][1]), __float_as_uint(v[j][2]),
+                           __float_as_uint(v[j][3])};
+          __builtin_amdgcn_raw_buffer_store_b128(d, c_rs, off, 0, 0);
+        }
+      } else {
+        // pairs (2p, 2p+1): after the swap lane fq holds 8 consecutive columns at
+        // 32p + (fq & 1) * 16 + (fq >> 1) * 8
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          uint32_t x0 = pack_bf16(v[2 * pp][0], v[2 * pp][1]), x1 = pack_bf16(v[2 * pp][2], v[2 * pp][3]);
+          uint32_t y0 = pack_bf16(v[2 * pp + 1][0], v[2 * pp + 1][1]), y1 = pack_bf16(v[2 * pp + 1][2], v[2 * pp + 1][3]);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+          const int n = ncol + 32 * pp + (fq & 1) * 16 + (fq >> 1) * 8;
+          const int off = ok ? out_elem(p, m, n, p.ldc, CT) * 2 : OOB;
+          const u32x4 d = {s0[0], s1[0], s0[1], s1[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(d, c_rs, off, 0, 0);
+        }
+      }
+    });
+    };
+    if (act == 1) epilogue(std::integral_constant<int, 1>{});
+    else if (act == 2) epilogue(std::integral_constant<int, 2>{});
+    else epilogue(std::integral_constant<int, 0>{});
+}
+
+template <int BM, bool CONV, bool RELU_A, int EPI>
+__global__ __launch_bounds__(512) void k_gemm_p(Args p) {
+  constexpr int BN = 256, TM = BM / 2, RM = TM / 16, RN = 4;
+  constexpr int ROWB = 128, RPI = 8;
+  constexpr int A_LOADS = BM / 64, W_LOADS = BN / 64;
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int BIAS_OFF = 2 * STAGE;
+  constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
+  constexpr int E_ALL = RM * (NRL + NS);
+  static_assert(BM == 256 || BM == 320, "BM");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int wm = wid >> 2;                   // 0..1  -> activation rows wm*128
-  const int wn = wid & 3;                    // 0..3  -> output cols wn*64
-  int tm, tn;
-  tile_coords(p, blockIdx.x, tm, tn);
-  const int m0 = tm * 256;
-  const int n0 = tn * 256;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, pchunk = lane & 7;
 
-  // glds mapping: wave-instruction = 16 rows x 4 chunks; thread does 2 A + 2 W per stage
-  const int pchunk = lane & 3;
-  const bf16_t* a_src[2];
-  const bf16_t* w_src[2];
-  int cpix[2], cyx[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (wid * 2 + j) * 16 + (lane >> 2);          // 0..255
-    const int lchunk = pchunk ^ ((row >> 1) & 3);
-    int m = m0 + row;
-    if (m > p.M - 1) m = p.M - 1;
-    if (!CONV) {
-      a_src[j] = p.A + (int64_t)remap(m, p.a_g, p.a_gs, p.a_o) * p.lda + lchunk * 8;
-      cpix[j] = cyx[j] = 0;
+  const int T = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, xl = blockIdx.x >> 3, q = G >> 3, rr = G & 7;
+  int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + xl;
+  if (t >= T) return;
+
+  // operands through buffer descriptors: rows past M and conv taps outside the image
+  // read as zero (offset >= range), so no per-row clamping and one VGPR offset per operand
+  const rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, p.a_bytes, 0x00020000);
+  const rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W), 0, p.w_bytes, 0x00020000);
+  const rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias), 0, p.bias ? p.N * 4 : 0, 0x00020000);
+  const int chunk16 = (pchunk ^ lrow) << 4;           // swizzled 16-B chunk (row & 7 == lrow)
+  const int a_row0 = wid * A_LOADS * RPI + lrow;      // + j * RPI
+  const int w_row0 = wid * W_LOADS * RPI + lrow;
+  const int a_sstep = RPI * (int)p.lda * 2, w_sstep = RPI * (int)p.ldw * 2;
+
+  uint32_t a_off;                 // dense A: byte offset of this lane's slab-0 row
+  uint32_t w_off;
+  int cpix[CONV ? A_LOADS : 1], cyx[CONV ? A_LOADS : 1];
+  int nm0, nn0;   // coordinates of the tile the offsets point at
+  auto setup = [&](int tile) {
+    int tm, tn;
+    grouped(p, tile, tm, tn);
+    nm0 = tm * BM;
+    nn0 = tn * BN;
+    if constexpr (!CONV) {
+      a_off = (uint32_t)(nm0 + a_row0) * (uint32_t)(p.lda * 2) + chunk16;
     } else {
-      const int hw = p.coh * p.cow;
-      const int b = m / hw;
-      const int rem = m - b * hw;
-      const int oy = rem / p.cow;
-      const int ox = rem - oy * p.cow;
-      cpix[j] = b * p.ch * p.cw;
-      cyx[j] = ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff);
-      a_src[j] = p.A + lchunk * 8;
-    }
-    w_src[j] = p.W + (int64_t)(n0 + row) * p.ldw + lchunk * 8;
-  }
-  auto stage = [&](int buf, int k0) {
-    uint8_t* sA = smem + buf * STG;
-    uint8_t* sW = sA + PART;
-    if (!CONV) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) glds16(a_src[j] + k0, sA + (wid * 2 + j) * 16 * ROWB);
+      for (int j = 0; j < A_LOADS; ++j) {
+        const int m = nm0 + a_row0 + j * RPI;
+        const int hw = p.coh * p.cow;
+        const int b = m / hw;
+        const int rem = m - b * hw;
+        const int oy = rem / p.cow;
+        const int ox = rem - oy * p.cow;
+        // rows past M: an out-of-image y so every tap reads zero
+        cpix[j] = b * p.ch * p.cw;
+        cyx[j] = m < p.M ? ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff) : (int)(0x4000u << 16);
+      }
+    }
+    w_off = (uint32_t)(nn0 + w_row0) * (uint32_t)(p.ldw * 2) + chunk16;
+  };
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  // one K-stage (A BM x 64, W 256 x 64) into LDS buffer `buf`; with `bias_par` >= 0
+  // wave 0 first stages the tile's 256 bias values into bias slot bias_par
+  auto stage = [&](int buf, int k0, int bias_par) {
+    uint8_t* sA = smem + buf * STAGE;
+    uint8_t* sW = sA + A_BYTES;
+    if (bias_par >= 0 && wid == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, (lds_ptr_t)(smem + BIAS_OFF + bias_par * 1024), 16,
+                                                (nn0 + lane * 4) * 4, 0, 0, 0);
+    if constexpr (!CONV) {
+#pragma unroll
+      for (int j = 0; j < A_LOADS; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid * A_LOADS + j) * RPI * ROWB), 16,
+                                                  a_off + j * a_sstep, k0 * 2, 0, 0);   // row part in voffset: range-checked
     } else {
       const int kk = k0 / p.cc;
       const int ky = kk / p.ck;
       const int kx = kk - ky * p.ck;
       const int ci0 = k0 - kk * p.cc;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < A_LOADS; ++j) {
         const int yi = (cyx[j] >> 16) + ky, xi = ((int)(short)(cyx[j] & 0xffff)) + kx;
-        const bool ok = yi >= 0 && yi < p.ch && xi >= 0 && xi < p.cw;
-        const void* src = ok ? (const void*)(a_src[j] + ((int64_t)cpix[j] + (int64_t)yi * p.cw + xi) * p.cc + ci0)
-                             : (const void*)(g_zero + pchunk * 16);
-        glds16(src, sA + (wid * 2 + j) * 16 * ROWB);
+        const bool ok = (unsigned)yi < (unsigned)p.ch && (unsigned)xi < (unsigned)p.cw;
+        const int off = ok ? ((cpix[j] + yi * p.cw + xi) * p.cc + ci0) * 2 + chunk16 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid * A_LOADS + j) * RPI * ROWB), 16, off, 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(w_src[j] + k0, sW + (wid * 2 + j) * 16 * ROWB);
+    for (int j = 0; j < W_LOADS; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rs, (lds_ptr_t)(sW + (wid * W_LOADS + j) * RPI * ROWB), 16, w_off,
+                                                j * w_sstep + k0 * 2, 0, 0);
   };
 
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const rsrc_t c_rs = make_rsrc(p.C);
+  const rsrc_t r_rs = make_rsrc(p.res);
+  const rsrc_t r2_rs = make_rsrc(p.res2);
+  const int nk = p.K / BK;
 
-  const int frow = lane & 15;
-  const int fq = lane >> 4;
-  const int nk = p.K / RBK;
-  // prologue: stages 0..2 in flight, wait for stage 0
-  stage(0, 0);
-  if (nk > 1) stage(1, RBK);
-  if (nk > 2) stage(2, 2 * RBK);
-  __builtin_amdgcn_sched_barrier(0);
-  if (nk > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
+  setup(t);
+  int m0 = nm0, n0 = nn0;
+  stage(0, 0, 0);
+  int g = 0, tpar = 0, tord = 0;
+  bool after_epi = false;
+  for (;;) {
+    const int t_next = t + G;
+    const bool has_next = t_next < T;
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 3 < nk) stage((kt + 3) & (NST - 1), (kt + 3) * RBK);
-    const uint8_t* sA = smem + (kt & (NST - 1)) * STG;
-    const uint8_t* sW = sA + PART;
-    bf16x8 wf[4];
+    PSTAMP(tord, 0);
+#ifdef I2PC_STAMPS
+    unsigned long long st_wait = 0, st_a = 0, st_b = 0;
+#endif
+    for (int kt = 0; kt < nk; ++kt) {
+#ifdef I2PC_STAMPS
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_a)::"memory");
+#endif
+      // stage g landed: everything issued after it (the previous epilogue) may stay in flight
+      if (kt == 0 && after_epi) {
+        // any count <= E_ALL is safe (in-order completion); use the largest available
+        if constexpr (E_ALL >= 63) I2PC_WAIT_VM(63);
+        else if constexpr (E_ALL >= 48) I2PC_WAIT_VM(48);
+        else if constexpr (E_ALL >= 40) I2PC_WAIT_VM(40);
+        else if constexpr (E_ALL >= 32) I2PC_WAIT_VM(32);
+        else if constexpr (E_ALL >= 20) I2PC_WAIT_VM(20);
+        else if constexpr (E_ALL >= 16) I2PC_WAIT_VM(16);
+        else I2PC_WAIT_VM(0);
+      } else {
+        I2PC_WAIT_VM(0);
+      }
+      I2PC_LDS_BARRIER();
+#ifdef I2PC_STAMPS
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_b)::"memory");
+      st_wait += st_b - st_a;
+#endif
+      if (kt == 0) PSTAMP(tord, 1);
+      if (kt + 1 < nk) {
+        stage((g + 1) & 1, (kt + 1) * BK, -1);
+      } else if (has_next) {
+        setup(t_next);
+        stage((g + 1) & 1, 0, tpar ^ 1);
+      }
+      const uint8_t* sA = smem + (g & 1) * STAGE;
+      const uint8_t* sW = sA + A_BYTES;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = wn * 64 + j * 16 + frow;
-      wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * ROWB + ((fq ^ ((row >> 1) & 3)) << 4));
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 wf[RN];
+        const int lchunk = 4 * s + fq;
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const int row = wn * 64 + j * 16 + frow;
+          wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * ROWB + ((lchunk ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+          const int row = wm * TM + i * 16 + frow;
+          bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((lchunk ^ (row & 7)) << 4));
+          if (RELU_A) af = relu8(af);
+#pragma unroll
+          for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
+        }
+      }
+      ++g;
     }
-    bf16x8 af[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = wm * 128 + i * 16 + frow;
-      af[i] = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((fq ^ ((row >> 1) & 3)) << 4));
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (RELU_A) af[i] = relu8(af[i]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    // step kt+1 must have landed; everyone must be done reading stage kt before it is refilled
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + 3 < nk) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    else if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
+
+    PSTAMP(tord, 2);
+#ifdef I2PC_STAMPS
+    if (threadIdx.x == 0 && tord < 8) g_stamps[(blockIdx.x * 8 + tord) * 8 + 4] = st_wait;
+#endif
+    // ---- epilogue of tile (m0, n0): register-direct, counted
+    epilogue_p<RM, EPI>(p, acc, m0 + wm * TM, n0 + wn * 64,
+                        reinterpret_cast<const float*>(smem + BIAS_OFF + tpar * 1024) + wn * 64, c_rs, r_rs, r2_rs);
+    PSTAMP(tord, 3);
+    ++tord;
+    if (!has_next) break;
+    t = t_next;
+    m0 = nm0;
+    n0 = nn0;
+    tpar ^= 1;
+    after_epi = true;
   }
-
-  // epilogue in two passes of 64 rows through this wave's 16 KiB LDS region
-  float* elds = reinterpret_cast<float*>(smem) + wid * 64 * 64;
-  tile_epilogue<8, 4>(p, acc, 0, 4, m0 + wm * 128, n0 + wn * 64, elds);
-  __builtin_amdgcn_wave_barrier();
-  tile_epilogue<8, 4>(p, acc, 4, 4, m0 + wm * 128, n0 + wn * 64, elds);
 }
+#undef I2PC_WAIT_VM
+#undef I2PC_LDS_BARRIER
+
+}  // namespace pers
 
 static int group_m_for(int tiles_m) {
   static const int env = [] { const char* e = getenv("I2PC_GEMM_GM"); return e ? atoi(e) : 0; }();
@@ -813,58 +899,175 @@ static int group_m_for(int tiles_m) {
   return std::max(1, std::min(g, tiles_m));
 }
 
-template <bool CONV, bool RELU_A>
-static void launch_ring(const Args& p, hipStream_t s) {
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+template <int BM, bool CONV, bool RELU_A, int EPI>
+static void launch_p(const Args& p, hipStream_t s) {
   Args q = p;
-  q.tiles_m = (p.M + 255) / 256;
+  if (!CONV) {                        // dense rows: fold the row offset into the base
+    q.A = p.A + (int64_t)p.a_o * p.lda;
+    q.a_o = 0;
+    q.a_bytes = (uint32_t)((int64_t)p.M * p.lda * 2);
+  } else {
+    q.a_bytes = (uint32_t)((int64_t)p.cb * p.ch * p.cw * p.cc * 2);
+  }
+  q.w_bytes = (uint32_t)((int64_t)p.N * p.ldw * 2);
+  q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = p.N / 256;
   q.group_m = group_m_for(q.tiles_m);
-  const int smem = 4 * 32 * 1024;   // 128 KiB
-  auto kern = k_gemm_ring<CONV, RELU_A>;
+  const int smem = 2 * (BM + 256) * 128 + 2048;
+  auto kern = pers::k_gemm_p<BM, CONV, RELU_A, EPI>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(q.tiles_m * q.tiles_n), dim3(512), smem, s, q);
+  const int tiles = q.tiles_m * q.tiles_n;
+  const int grid = std::min(tiles, num_cus());
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
 }
 
-template <bool CONV, bool RELU_A>
-static void launch8(const Args& p, hipStream_t s) {
-  Args q = p;
-  q.tiles_m = (p.M + 255) / 256;
-  q.tiles_n = p.N / 256;
-  q.group_m = group_m_for(q.tiles_m);
-  const int smem = 8 * 128 * 128;   // 128 KiB
-  auto kern = k_gemm8<CONV, RELU_A>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
+// Which kernel a call runs: the persistent 256-column engine when the epilogue is one it
+// implements and every byte offset fits its 31-bit buffer range; else the tile kernel.
+struct Plan {
+  int kind;      // 0 tile kernel, 1 persistent engine
+  int bm, bn, epi;
+};
+
+// 0 auto, 1 tile kernel only, 2 persistent engine wherever its epilogue applies;
+// initial value from I2PC_GEMM_P (0 -> 1, 2 -> 2)
+static int g_engine = [] {
+  const char* e = getenv("I2PC_GEMM_P");
+  return !e ? 0 : atoi(e) == 0 ? 1 : atoi(e) == 2 ? 2 : 0;
+}();
+
+static int64_t max_row(const Args& p) {
+  const int64_t m = p.M - 1;
+  return p.o_g > 0 ? (m / p.o_g) * p.o_gs + (p.o_g - 1) + p.o_o : m + p.o_o;
+}
+
+static Plan plan_for(const Args& p, bool conv, bool relu) {
+  static const int force = [] { const char* e = getenv("I2PC_GEMM_TILE"); return e ? atoi(e) : 0; }();
+  const int pforce = g_engine;
+  Plan pl{0, 0, 0, -1};
+  // persistent engine
+  int epi = -1;
+  if (p.N % 256 == 0 && !p.rbias && !p.tbl && force == 0 && pforce != 1) {
+    const bool ct = p.ct_s > 0;
+    if (ct) epi = (!p.res && !p.res2 && !p.c_f32 && p.ct_c % 8 == 0) ? pers::EPI_CT : -1;
+    else if (!p.res && !p.res2 && !p.c_f32) epi = pers::EPI_PLAIN;
+    else if (p.res && p.res_f32 && p.c_f32 && !p.res2) epi = pers::EPI_RESF32;
+    else if (p.res && !p.res_f32 && !p.c_f32 && !p.res2) epi = pers::EPI_RESBF16;
+    else if (p.res && !p.res_f32 && !p.c_f32 && p.res2) epi = pers::EPI_RES2;
+    // instantiated combinations
+    if (!conv && relu) epi = -1;
+    if (!conv && (epi == pers::EPI_RESBF16 || epi == pers::EPI_RES2)) epi = -1;
+    if (conv && (epi == pers::EPI_RESF32 || epi == pers::EPI_CT)) epi = -1;
+    if (conv && relu && epi != pers::EPI_PLAIN) epi = -1;
+    if (!conv && p.a_g != 0) epi = -1;
+    if (epi >= 0) {
+      const int64_t esz = p.c_f32 ? 4 : 2;
+      const int64_t abytes = conv ? (int64_t)p.cb * p.ch * p.cw * p.cc * 2 : (int64_t)(p.M + 320) * p.lda * 2;
+      if (abytes >= pers::OOB || (int64_t)p.N * p.ldw * 2 >= pers::OOB) epi = -1;
+      const int64_t cbytes = ct ? (int64_t)p.M * p.N * 2 : (max_row(p) * p.ldc + p.N) * esz;
+      int64_t rbytes = 0;
+      if (p.res) rbytes = std::max(rbytes, (max_row(p) * p.ldr + p.N) * (p.res_f32 ? 4 : 2));
+      if (p.res2) rbytes = std::max(rbytes, (max_row(p) * p.ldr2 + p.N) * 2);
+      if (cbytes >= pers::OOB || rbytes >= pers::OOB) epi = -1;
+    }
   }
-  hipLaunchKernelGGL(kern, dim3(q.tiles_m * q.tiles_n), dim3(512), smem, s, q);
-}
-
-
-template <bool CONV, bool RELU_A>
-static int dispatch(const Args& p, hipStream_t s) {
+  if (epi >= 0) {
+    static const int bm_force = [] { const char* e = getenv("I2PC_GEMM_PBM"); return e ? atoi(e) : 0; }();
+    const int64_t ncu = num_cus();
+    int best = 256;
+    int64_t best_cost = -1;
+    for (int bm : {256}) {   // 320 spills registers (scratch would break the counted waits)
+      const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * (p.N / 256);
+      const int64_t cost = (tiles + ncu - 1) / ncu * bm;
+      if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = bm; }
+    }
+    if (bm_force == 256) best = bm_force;
+    // The persistent engine pays where a CU runs several tiles (it hides each tile's first
+    // stage and epilogue behind the neighbouring tiles); at one or two tiles per CU the
+    // tile kernel's 128 x 128 configurations quantise better (profiles/r01_gemm_engines.txt).
+    const int64_t tiles = (int64_t)((p.M + best - 1) / best) * (p.N / 256);
+    if (pforce == 2 || tiles >= 3 * ncu) {
+      pl = Plan{1, best, 256, epi};
+      return pl;
+    }
+  }
   const int64_t t256 = (int64_t)((p.M + 255) / 256) * (p.N / 256);
   const int64_t t128 = (int64_t)((p.M + 127) / 128) * (p.N / 128);
-  static const int force = [] { const char* e = getenv("I2PC_GEMM_TILE"); return e ? atoi(e) : 0; }();
-  const bool even_k = (p.K / BK) % 2 == 0;
-  const bool big_ok = p.N % 256 == 0 && even_k && (CONV || p.a_g == 0);
-  if (force == 8 && big_ok) launch8<CONV, RELU_A>(p, s);
-  else if (force == 4 && p.N % 256 == 0) launch_ring<CONV, RELU_A>(p, s);
-  else if (force == 256 && p.N % 256 == 0) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
-  else if (force == 25632 && p.N % 256 == 0) launch<256, 256, 2, 4, 32, CONV, RELU_A>(p, s);
-  else if (force == 128 && p.N % 128 == 0) launch<128, 128, 2, 2, 64, CONV, RELU_A>(p, s);
-  else if (force == 12832 && p.N % 128 == 0) launch<128, 128, 2, 2, 32, CONV, RELU_A>(p, s);
-  else if (p.N % 256 == 0 && t256 >= 512) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
-  else if (p.N % 128 == 0 && t128 >= 512) launch<128, 128, 2, 2, 64, CONV, RELU_A>(p, s);
-  else if (p.N % 64 == 0) launch<128, 64, 2, 2, 64, CONV, RELU_A>(p, s);
-  else if (p.N % 32 == 0) launch<128, 32, 4, 1, 64, CONV, RELU_A>(p, s);
-  else return set_error(I2PC_EUNSUPPORTED, "gemm: N=%d must be a multiple of 32", p.N);
+  if (force == 256 && p.N % 256 == 0) pl = Plan{0, 256, 256, 64};
+  else if (force == 25632 && p.N % 256 == 0) pl = Plan{0, 256, 256, 32};
+  else if (force == 320 && p.N % 256 == 0) pl = Plan{0, 320, 256, 64};
+  else if (force == 192 && p.N % 256 == 0) pl = Plan{0, 192, 256, 64};
+  else if (force == 128 && p.N % 128 == 0) pl = Plan{0, 128, 128, 64};
+  else if (force == 12832 && p.N % 128 == 0) pl = Plan{0, 128, 128, 32};
+  else if (p.N % 256 == 0 && t256 >= 512) pl = Plan{0, 256, 256, 64};
+  else if (p.N % 128 == 0 && t128 >= 512) pl = Plan{0, 128, 128, 64};
+  else if (p.N % 64 == 0) pl = Plan{0, 128, 64, 64};
+  else if (p.N % 32 == 0) pl = Plan{0, 128, 32, 64};
+  else pl = Plan{-1, 0, 0, 0};
+  return pl;
+}
+
+template <bool CONV, bool RELU_A>
+static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
+  using namespace pers;
+  if constexpr (!CONV && !RELU_A) {
+    if (pl.epi == EPI_PLAIN) launch_p<256, false, false, EPI_PLAIN>(p, s);
+    else if (pl.epi == EPI_RESF32) launch_p<256, false, false, EPI_RESF32>(p, s);
+    else launch_p<256, false, false, EPI_CT>(p, s);
+  } else if constexpr (CONV && !RELU_A) {
+    if (pl.epi == EPI_PLAIN) launch_p<256, true, false, EPI_PLAIN>(p, s);
+    else if (pl.epi == EPI_RESBF16) launch_p<256, true, false, EPI_RESBF16>(p, s);
+    else launch_p<256, true, false, EPI_RES2>(p, s);
+  } else if constexpr (CONV && RELU_A) {
+    launch_p<256, true, true, EPI_PLAIN>(p, s);
+  } else {
+    return set_error(I2PC_EUNSUPPORTED, "gemm: no persistent variant");
+  }
   return check_launch("gemm");
+}
+
+template <bool CONV, bool RELU_A>
+static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
+  if (pl.kind == 1) return run_persistent<CONV, RELU_A>(pl, p, s);
+  if (pl.kind < 0) return set_error(I2PC_EUNSUPPORTED, "gemm: N=%d must be a multiple of 32", p.N);
+  if (pl.bm == 256 && pl.epi == 64) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
+  else if (pl.bm == 256) launch<256, 256, 2, 4, 32, CONV, RELU_A>(p, s);
+  else if (pl.bm == 320) launch<320, 256, 2, 4, 64, CONV, RELU_A>(p, s);
+  else if (pl.bm == 192) launch<192, 256, 2, 4, 64, CONV, RELU_A>(p, s);
+  else if (pl.bn == 128 && pl.epi == 64) launch<128, 128, 2, 2, 64, CONV, RELU_A>(p, s);
+  else if (pl.bn == 128) launch<128, 128, 2, 2, 32, CONV, RELU_A>(p, s);
+  else if (pl.bn == 64) launch<128, 64, 2, 2, 64, CONV, RELU_A>(p, s);
+  else launch<128, 32, 4, 1, 64, CONV, RELU_A>(p, s);
+  return check_launch("gemm");
+}
+
+static const char* plan_name(const Plan& pl, bool conv, bool relu) {
+  static thread_local char buf[96];
+  const char* c = conv ? "true" : "false";
+  const char* r = relu ? "true" : "false";
+  if (pl.kind == 1) {
+    static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT"};
+    snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
+  } else if (pl.kind == 0) {
+    const int wm = pl.bn == 32 ? 4 : 2, wn = pl.bn == 256 ? 4 : pl.bn == 32 ? 1 : 2;
+    snprintf(buf, sizeof buf, "k_gemm<%d, %d, %d, %d, %d, %s, %s>", pl.bm, pl.bn, wm, wn, pl.epi, c, r);
+  } else {
+    snprintf(buf, sizeof buf, "unsupported");
+  }
+  return buf;
 }
 
 }  // namespace gemm
@@ -878,14 +1081,13 @@ extern "C" int i2pc_debug_stamps(unsigned long long* host, int n) {
 }
 #endif
 
-extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) {
-  clear_error();
+static int make_args(const i2pc_gemm_desc* d, gemm::Args& p) {
   I2PC_REQUIRE(d != nullptr, "desc is NULL");
   I2PC_REQUIRE(d->a && d->w && d->c, "NULL operand");
   I2PC_REQUIRE(d->m > 0 && d->n > 0 && d->k > 0, "empty gemm");
   I2PC_REQUIRE(d->k % 64 == 0, "gemm: K=%d must be a multiple of 64", d->k);
   I2PC_REQUIRE(d->n % 4 == 0, "gemm: N must be a multiple of 4");
-  gemm::Args p{};
+  p = gemm::Args{};
   p.A = static_cast<const gemm::bf16_t*>(d->a);
   p.lda = d->lda; p.M = d->m; p.N = d->n; p.K = d->k;
   p.a_g = d->a_group; p.a_gs = d->a_group_stride; p.a_o = d->a_offset;
@@ -899,14 +1101,37 @@ extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) {
   p.C = d->c; p.c_f32 = d->c_f32; p.ldc = d->ldc;
   p.o_g = d->out_group; p.o_gs = d->out_group_stride; p.o_o = d->out_offset;
   p.ct_s = d->convt_s; p.ct_h = d->convt_h; p.ct_w = d->convt_w; p.ct_c = d->convt_c;
-  hipStream_t s = as_stream(stream);
   if (d->conv) {
     I2PC_REQUIRE(d->conv_c % 64 == 0, "conv: Cin=%d must be a multiple of 64", d->conv_c);
     I2PC_REQUIRE(d->k == d->conv_k * d->conv_k * d->conv_c, "conv: K != k*k*Cin");
     I2PC_REQUIRE(d->m == d->conv_batch * d->conv_oh * d->conv_ow, "conv: M != B*OH*OW");
     p.cb = d->conv_batch; p.ch = d->conv_h; p.cw = d->conv_w; p.cc = d->conv_c;
     p.coh = d->conv_oh; p.cow = d->conv_ow; p.ck = d->conv_k; p.cs = d->conv_stride; p.cp = d->conv_pad;
-    return d->conv_relu_in ? gemm::dispatch<true, true>(p, s) : gemm::dispatch<true, false>(p, s);
   }
-  return d->conv_relu_in ? gemm::dispatch<false, true>(p, s) : gemm::dispatch<false, false>(p, s);
+  return I2PC_OK;
+}
+
+extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) {
+  clear_error();
+  gemm::Args p;
+  const int rc = make_args(d, p);
+  if (rc != I2PC_OK) return rc;
+  hipStream_t s = as_stream(stream);
+  const bool conv = d->conv != 0, relu = d->conv_relu_in != 0;
+  const gemm::Plan pl = gemm::plan_for(p, conv, relu);
+  if (conv) return relu ? gemm::run_plan<true, true>(pl, p, s) : gemm::run_plan<true, false>(pl, p, s);
+  return relu ? gemm::run_plan<false, true>(pl, p, s) : gemm::run_plan<false, false>(pl, p, s);
+}
+
+extern "C" const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* d) {
+  gemm::Args p;
+  if (make_args(d, p) != I2PC_OK) return "invalid";
+  return gemm::plan_name(gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0), d->conv != 0, d->conv_relu_in != 0);
+}
+
+extern "C" int i2pc_gemm_set_engine(int mode) {
+  clear_error();
+  I2PC_REQUIRE(mode >= 0 && mode <= 2, "gemm engine mode %d (0 auto, 1 tile kernel only, 2 persistent wherever it applies)", mode);
+  gemm::g_engine = mode;
+  return I2PC_OK;
 }

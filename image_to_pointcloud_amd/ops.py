@@ -8,7 +8,6 @@ Layouts: activations bf16 NHWC / [rows][features]; residual stream fp32.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional
 
 from . import _lib
@@ -39,6 +38,8 @@ class GemmDesc(ctypes.Structure):
 
 
 _lib.register("i2pc_gemm", ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p])
+_lib.register("i2pc_gemm_kernel_name", ctypes.c_char_p, [ctypes.POINTER(GemmDesc)])
+_lib.register("i2pc_gemm_set_engine", ctypes.c_int, [ctypes.c_int])
 _lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
                                                ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_attention", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -108,28 +109,13 @@ class _Timed:
 
 
 def gemm_kernel_label(desc: GemmDesc) -> str:
-    """Name of the k_gemm instance i2pc_gemm dispatches to (mirrors gemm.hip `dispatch`)."""
-    M, N = desc.m, desc.n
-    t256 = ((M + 255) // 256) * (N // 256)
-    t128 = ((M + 127) // 128) * (N // 128)
-    force = int(os.environ.get("I2PC_GEMM_TILE", "0") or 0)
-    kb = 64
-    if force in (256, 25632) and N % 256 == 0:
-        bm, bn, kb = 256, 256, (64 if force == 256 else 32)
-    elif force in (128, 12832) and N % 128 == 0:
-        bm, bn, kb = 128, 128, (64 if force == 128 else 32)
-    elif N % 256 == 0 and t256 >= 512:
-        bm, bn = 256, 256
-    elif N % 128 == 0 and t128 >= 512:
-        bm, bn = 128, 128
-    elif N % 64 == 0:
-        bm, bn = 128, 64
-    else:
-        bm, bn = 128, 32
-    wm, wn = {(256, 256): (2, 4), (128, 128): (2, 2), (128, 64): (2, 2), (128, 32): (4, 1)}[(bm, bn)]
-    conv = "true" if desc.conv else "false"
-    relu = "true" if desc.conv_relu_in else "false"
-    return f"k_gemm<{bm}, {bn}, {wm}, {wn}, {kb}, {conv}, {relu}>"
+    """Name of the kernel instance i2pc_gemm dispatches to (asked of the C side, so it cannot drift)."""
+    return _lib.load().i2pc_gemm_kernel_name(ctypes.byref(desc)).decode()
+
+
+def set_gemm_engine(mode: int) -> None:
+    """0 = automatic, 1 = tile kernel only, 2 = persistent engine wherever its epilogue applies."""
+    _lib.call("i2pc_gemm_set_engine", int(mode))
 
 
 def gemm(desc: GemmDesc) -> None:

@@ -145,6 +145,16 @@ typedef struct i2pc_gemm_desc {
 
 int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
 
+/* Name of the kernel instance i2pc_gemm would launch for `desc` (profiling labels;
+ * no device work).  Returns "invalid" for a descriptor i2pc_gemm would reject. */
+const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* desc);
+
+/* GEMM engine selection (process-wide): 0 = automatic (the persistent 256-column
+ * engine for calls with >= 3 tiles per CU whose epilogue it implements, else the
+ * tile kernel), 1 = tile kernel only, 2 = persistent engine wherever its epilogue
+ * applies.  All produce bit-identical results; tests use this to cross-check them. */
+int i2pc_gemm_set_engine(int mode);
+
 /* LayerNorm over the last dim: x fp32 [rows][dim] (row stride ldx) -> y bf16 [rows][dim]
  * (row stride ldy); gamma/beta fp32 [dim]; two-pass mean/variance in fp32.
  * (nn.LayerNorm, modeling_dpt.py:233-234). dim % 64 == 0, dim <= 2048. */

@@ -1,0 +1,154 @@
+"""The persistent 256-column GEMM engine against the tile kernel (bit-exact) and torch fp32.
+
+Both engines accumulate the same MFMA sequence and apply the epilogue in the same
+fp32 order (bias, activation, residual, second residual, bf16 rounding), so their
+outputs must be identical bit for bit.  Shapes cover several tiles per workgroup
+(more tiles than CUs: the cross-tile prefetch and counted epilogue waits), a
+partial last M-tile, K = 64 (one K-step per tile), and every epilogue the engine
+implements.  torch tolerance: relative Frobenius error <= 8e-3.
+"""
+import math
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+F = torch.nn.functional
+
+
+def _ops():
+    from image_to_pointcloud_amd import ops
+    return ops
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _both(fn):
+    """(persistent engine forced, tile kernel) outputs; the automatic choice must equal both."""
+    ops = _ops()
+    outs = []
+    try:
+        for mode in (1, 2):
+            ops.set_gemm_engine(mode)
+            outs.append(fn().clone())
+    finally:
+        ops.set_gemm_engine(0)
+    auto = fn()
+    torch.cuda.synchronize()
+    assert torch.equal(auto, outs[0]), "automatic engine choice differs from the tile kernel"
+    return outs[1], outs[0]
+
+
+def _fro(got, ref):
+    got, ref = got.float(), ref.float()
+    return ((got - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("M,N,K,act", [(8200, 2048, 1024, None), (18464, 3072, 64, "gelu"), (9000, 1024, 192, None), (4100, 4096, 512, "gelu"),
+                                       (300, 256, 512, None), (257, 512, 128, "relu")])
+def test_linear_plain_engines_bitexact(M, N, K, act):
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = _bf(torch.randn(M, K, generator=g)).to(dev)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    got, ref = _both(lambda: ops.linear(x, w, bias=b, act=act, out=out))
+    ops.set_gemm_engine(2)
+    try:
+        assert "k_gemm_p" in ops.gemm_kernel_label(_desc_of(ops, x, w, b, out)), "persistent engine not selected"
+    finally:
+        ops.set_gemm_engine(0)
+    assert torch.equal(got, ref), f"engines differ: {(got.float() - ref.float()).abs().max().item()}"
+    y = x.float() @ w.float().T + b
+    y = F.gelu(y) if act == "gelu" else F.relu(y) if act == "relu" else y
+    assert _fro(got, y) <= 8e-3
+
+
+def _desc_of(ops, x, w, b, out):
+    d = ops.GemmDesc()
+    d.a, d.lda, d.m, d.n, d.k = x.data_ptr(), x.stride(0), x.shape[0], w.shape[0], w.shape[1]
+    d.w, d.ldw = w.data_ptr(), w.stride(0)
+    d.bias = b.data_ptr()
+    d.c, d.ldc = out.data_ptr(), out.stride(0)
+    return d
+
+
+@pytest.mark.parametrize("M,N,K", [(8200, 1024, 1024), (18464, 1024, 4096), (1000, 256, 192)])
+def test_linear_residual_f32_engines_bitexact(M, N, K):
+    """Transformer residual: out = x + (h @ W^T + b), fp32 stream updated in place."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(M * 3 + K)
+    h = _bf(torch.randn(M, K, generator=g)).to(dev)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    x0 = torch.randn(M, N, generator=g).to(dev)
+
+    def run():
+        x = x0.clone()
+        ops.linear(h, w, bias=b, res=x, out=x)
+        return x
+    got, ref = _both(run)
+    assert torch.equal(got, ref)
+    assert _fro(got, x0 + h.float() @ w.float().T + b) <= 8e-3
+
+
+def _pack_conv(w):
+    return _bf(w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)).contiguous()
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,stride", [(20, 64, 64, 256, 256, 1), (4, 48, 48, 512, 256, 2),
+                                                (3, 37, 29, 256, 256, 1)])
+def test_conv_engines_bitexact(B, H, W, C, Co, stride):
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(B + H + C)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    w = (torch.randn(Co, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    b = torch.randn(Co, generator=g).to(dev)
+    wp = _pack_conv(w)
+    got, ref = _both(lambda: ops.conv2d(x, wp, bias=b, stride=stride))
+    assert torch.equal(got, ref)
+    r = F.conv2d(x.float().permute(0, 3, 1, 2), _bf(w).float(), b, stride=stride, padding=1).permute(0, 2, 3, 1)
+    assert _fro(got, r) <= 8e-3
+
+
+def test_conv_residual_units_engines_bitexact():
+    """Pre-activation residual unit: ReLU-in conv + ReLU, then conv + bias + res + res2 (and res only)."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    B, H, W, C = 20, 48, 48, 256
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    hid = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    w1 = _pack_conv(torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    w2 = _pack_conv(torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    b1 = (torch.randn(C, generator=g) * 0.1).to(dev)
+    b2 = (torch.randn(C, generator=g) * 0.1).to(dev)
+    y1, r1 = _both(lambda: ops.conv2d(x, w1, bias=b1, relu_in=True, act="relu"))
+    assert torch.equal(y1, r1)
+    y2, r2 = _both(lambda: ops.conv2d(y1, w2, bias=b2, res=x, res2=hid))
+    assert torch.equal(y2, r2)
+    y3, r3 = _both(lambda: ops.conv2d(y1, w2, bias=b2, res=x))
+    assert torch.equal(y3, r3)
+
+
+@pytest.mark.parametrize("s,C", [(4, 256), (2, 512)])
+def test_conv_transpose_engines_bitexact(s, C):
+    ops = _ops()
+    dev = torch.device("cuda")
+    B, H, W = 16, 24, 24
+    g = torch.Generator(device="cpu").manual_seed(s + C)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    w = (torch.randn(C, C, s, s, generator=g) / math.sqrt(C)).to(dev)
+    b = torch.randn(C, generator=g).to(dev)
+    wp = _bf(w.permute(2, 3, 1, 0).reshape(s * s * C, C)).contiguous()
+    bt = b.repeat(s * s).contiguous()
+    got, ref = _both(lambda: ops.conv_transpose(x, wp, bt, s))
+    assert torch.equal(got, ref)
+    r = F.conv_transpose2d(x.float().permute(0, 3, 1, 2), _bf(w).float(), b, stride=s).permute(0, 2, 3, 1)
+    assert _fro(got, r) <= 8e-3

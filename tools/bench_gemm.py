@@ -25,11 +25,11 @@ for name, m, n, k in shapes:
     t = timeit(lambda: ops.linear(x, w, bias=b, out=out))
     ref = x[:2048].float() @ w.float().T + b
     err = ((out[:2048].float() - ref).norm() / ref.norm()).item()
-    print(f"tile={os.environ.get('I2PC_GEMM_TILE')} {name:4s} M={m} N={n} K={k}: {t*1e6:8.1f} us  {2*m*n*k/t/1e12:7.1f} TF  relerr={err:.2e}")
+    print(f"P={os.environ.get('I2PC_GEMM_P','-')} tile={os.environ.get('I2PC_GEMM_TILE')} {name:4s} M={m} N={n} K={k}: {t*1e6:8.1f} us  {2*m*n*k/t/1e12:7.1f} TF  relerr={err:.2e}")
 # conv shapes (neck/fusion at 96x96 and head)
 for (B, H, W, C, Co) in [(32, 96, 96, 256, 256), (32, 48, 48, 256, 256), (32, 192, 192, 256, 128), (32, 384, 384, 128, 32)]:
     x = (torch.rand(B, H, W, C, generator=g) * 2 - 1).to(torch.bfloat16).to(dev)
     w = ((torch.rand(Co, 9 * C, generator=g) * 2 - 1) / math.sqrt(9 * C)).to(torch.bfloat16).to(dev)
     out = torch.empty(B, H, W, Co, dtype=torch.bfloat16, device=dev)
     t = timeit(lambda: ops.conv2d(x, w, out=out), iters=10)
-    print(f"tile={os.environ.get('I2PC_GEMM_TILE')} conv {B}x{H}x{W}x{C}->{Co}: {t*1e6:8.1f} us  {2*B*H*W*Co*9*C/t/1e12:7.1f} TF")
+    print(f"P={os.environ.get('I2PC_GEMM_P','-')} tile={os.environ.get('I2PC_GEMM_TILE')} conv {B}x{H}x{W}x{C}->{Co}: {t*1e6:8.1f} us  {2*B*H*W*Co*9*C/t/1e12:7.1f} TF")
