@@ -1012,6 +1012,11 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   else if (force == 192 && p.N % 256 == 0) pl = Plan{0, 192, 256, 64};
   else if (force == 128 && p.N % 128 == 0) pl = Plan{0, 128, 128, 64};
   else if (force == 12832 && p.N % 128 == 0) pl = Plan{0, 128, 128, 32};
+  // one round of 320 x 256 tiles (e.g. M = 18464, N = 1024: 232 tiles) beats two rounds of
+  // 256^2 or 2.3 rounds of 128^2 once K is long enough to amortise the bigger epilogue
+  // (fc2: 156 vs 192 us, O: 53 vs 57 us, 48x48 neck conv: 102 vs 131 us; profiles/r01_gemm_engines.txt)
+  else if (p.N % 256 == 0 && p.K >= 1024 && (int64_t)((p.M + 319) / 320) * (p.N / 256) <= num_cus() &&
+           t256 > num_cus()) pl = Plan{0, 320, 256, 64};
   else if (p.N % 256 == 0 && t256 >= 512) pl = Plan{0, 256, 256, 64};
   else if (p.N % 128 == 0 && t128 >= 512) pl = Plan{0, 128, 128, 64};
   else if (p.N % 64 == 0) pl = Plan{0, 128, 64, 64};
