@@ -50,6 +50,9 @@ _SIGNATURES = {
     "i2pc_gather_stride": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "i2pc_profile_enable": (c_int, [c_int]),
     "i2pc_profile_unproject_ms": (c_float, []),
+    "i2pc_sor_workspace_bytes": (c_size_t, [c_int64]),
+    "i2pc_sor": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 
 _lib = None

@@ -13,9 +13,13 @@ functions, so backend/app.py can import them in place of its own:
   generate_gis_metadata(points, req)     app.py:391-417
   process_image_pipeline(job, data, req) app.py:419-565  (the depth branch, one GPU pass)
 
-Statistical outlier removal (refine_point_cloud, app.py:252-269) needs Open3D,
-which this image lacks; it is a pass-through here (as it is in the reference when
-Open3D raises) -- SURVEY §8f row 4.
+  refine_point_cloud(points, colors)     app.py:252-269  (geometry.remove_statistical_outlier:
+                                                         Open3D's statistical outlier removal
+                                                         restated as an exact device kNN)
+
+REFINE_POINT_CLOUD switches the refinement step of the depth job (app.py:479) off;
+the golden pipeline fixture was recorded with Open3D absent, where the reference's
+refine_point_cloud raises inside its try and hands the cloud back unchanged.
 """
 from __future__ import annotations
 
@@ -35,6 +39,7 @@ logger = logging.getLogger(__name__)
 MAX_IMAGE_DIM = 3072                      # app.py:42
 MAX_FILE_SIZE = 50 * 1024 * 1024          # app.py:44
 MAX_PREVIEW = 20000                       # app.py:497
+REFINE_POINT_CLOUD = True                 # app.py:479 (see the module docstring)
 
 models_cache: Dict[str, dict] = {}
 processing_jobs: Dict[str, dict] = {}
@@ -145,8 +150,27 @@ save_point_cloud = writers.save_point_cloud
 
 
 def refine_point_cloud(points, colors, nb_neighbors: int = 20, std_ratio: float = 2.0):
-    """app.py:252-269 without Open3D: pass-through."""
-    return points, colors
+    """app.py:252-269: statistical outlier removal on the device; (points[ind], colors[ind]).
+
+    Same error behaviour as the reference (any failure is logged and the cloud comes
+    back unrefined), except that a missing libi2pc.so / HIP device raises.
+    """
+    from . import _lib
+    try:
+        if points is None or len(points) == 0:
+            return points, colors
+        import torch
+        dev = geometry.require_device()
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(points, dtype=np.float32).reshape(-1, 3))).to(dev)
+        ind = geometry.remove_statistical_outlier(t, None, nb_neighbors, std_ratio).index.cpu().numpy()
+        points_f = points[ind]
+        colors_f = colors[ind] if colors is not None and len(colors) == len(points) else colors
+        return points_f, colors_f
+    except _lib.I2PCError:
+        raise
+    except Exception as e:
+        logger.warning(f"Point cloud refinement failed: {e}")
+        return points, colors
 
 
 def generate_gis_metadata(points, request: ProcessingRequest, bounds: Optional[dict] = None) -> dict:
@@ -179,7 +203,7 @@ def decode_image(image_data: bytes) -> np.ndarray:
 
 def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, model_info: dict) -> dict:
     """The depth branch of process_image_pipeline (app.py:456-559) as one device pass:
-    depth -> preview -> unprojection + bbox -> preview subsample -> artefact."""
+    depth -> preview -> unprojection + bbox -> outlier removal -> preview subsample -> artefact."""
     import torch
     dev = geometry.require_device()
     timg = torch.from_numpy(np.ascontiguousarray(image)).to(dev)
@@ -193,7 +217,10 @@ def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, mo
     pb = geometry.unproject_batch(depth[None], timg[None], density=request.point_density,
                                   invert=request.invert_depth, depth_scale=request.depth_scale,
                                   smooth=request.smooth_depth, smooth_ksize=request.smooth_ksize)
-    xyz, rgb = pb.xyz[0], pb.rgb[0]
+    xyz, rgb, bbox = pb.xyz[0], pb.rgb[0], pb.bbox[0]
+    if REFINE_POINT_CLOUD:                                                # app.py:479
+        sr = geometry.remove_statistical_outlier(xyz, rgb)
+        xyz, rgb, bbox = sr.xyz, sr.rgb, sr.bbox
     n = xyz.shape[0]
     prev_pts, prev_cols = geometry.preview_subsample(xyz, rgb, MAX_PREVIEW)
     points = xyz.cpu().numpy()
@@ -201,7 +228,7 @@ def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, mo
     if request.output_format.lower() in {"mesh_ply", "mesh"}:
         raise ValueError("mesh output (Poisson reconstruction, app.py:514-516) is out of scope for this backend")
     filepath = save_point_cloud(points, colors, request.output_format, job_id)
-    metadata = generate_gis_metadata(points, request, bounds=geometry.generate_gis_bounds(pb.bbox[0].cpu()))
+    metadata = generate_gis_metadata(points, request, bounds=geometry.generate_gis_bounds(bbox.cpu()))
     return {"pointCloud": {"filepath": filepath, "points": int(n), "format": request.output_format.upper()},
             "gisData": metadata, "downloadUrl": f"/download/{job_id}",
             "preview": {"points": prev_pts, "colors": prev_cols},

@@ -30,6 +30,7 @@ SOURCES = [
     "misc.hip",
     "attention.hip",
     "preprocess.hip",
+    "sor.hip",
     "writers.cpp",
 ]
 HEADERS = ["common.h", "../../include/i2pc.h"]

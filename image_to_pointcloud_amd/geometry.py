@@ -156,3 +156,44 @@ def preview_subsample(xyz, rgb, max_preview: int = 20000):
     _lib.call("i2pc_gather_stride", _ptr(xyz.contiguous()), _ptr(rgb.contiguous()), n, stride,
               _ptr(oxyz), _ptr(orgb), _stream_handle())
     return oxyz.cpu().double().tolist(), orgb.cpu().double().tolist()
+
+
+@dataclass
+class SorResult:
+    xyz: "object"     # torch.float32 [m, 3] kept points, original order (device)
+    rgb: "object"     # torch.uint8 [m, 3] or None
+    index: "object"   # torch.int64 [m] kept indices, ascending (Open3D's `ind`)
+    bbox: "object"    # torch.float64 [6] of the kept points (NaN if none)
+    avg: "object"     # torch.float64 [n] mean distance of every point to its k nearest
+
+
+def remove_statistical_outlier(xyz, rgb=None, nb_neighbors: int = 20, std_ratio: float = 2.0) -> SorResult:
+    """Open3D PointCloud.remove_statistical_outlier (refine_point_cloud, app.py:252-269) on the device.
+
+    xyz: torch.float32 [n, 3] on the device; rgb: torch.uint8 [n, 3] or None.
+    Raises ValueError on the parameters Open3D rejects (nb_neighbors < 1, std_ratio <= 0).
+    """
+    torch = _torch()
+    if nb_neighbors < 1 or not std_ratio > 0:
+        raise ValueError("Illegal input parameters, the number of neighbors and standard deviation ratio "
+                         "must be positive.")
+    if not xyz.is_cuda:
+        raise _lib.I2PCError("remove_statistical_outlier expects device tensors")
+    xyz = xyz.reshape(-1, 3).contiguous().to(torch.float32)
+    n, dev = xyz.shape[0], xyz.device
+    if rgb is not None:
+        rgb = rgb.reshape(-1, 3).contiguous()
+        if rgb.dtype != torch.uint8 or rgb.shape[0] != n or not rgb.is_cuda:
+            raise TypeError("rgb must be a device uint8 [n, 3] tensor matching xyz")
+    oxyz = torch.empty_like(xyz)
+    orgb = torch.empty_like(rgb) if rgb is not None else None
+    oidx = torch.empty(n, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    bbox = torch.empty(6, dtype=torch.float64, device=dev)
+    avg = torch.empty(n, dtype=torch.float64, device=dev)
+    lib = _lib.load()
+    ws = _workspace(lib.i2pc_sor_workspace_bytes(n), dev)
+    _lib.call("i2pc_sor", _ptr(xyz), _ptr(rgb), n, int(nb_neighbors), float(std_ratio), _ptr(oxyz), _ptr(orgb),
+              _ptr(oidx), _ptr(cnt), _ptr(bbox), _ptr(avg), _ptr(ws), ws.numel(), _stream_handle())
+    m = int(cnt.item())
+    return SorResult(oxyz[:m], orgb[:m] if orgb is not None else None, oidx[:m], bbox, avg)

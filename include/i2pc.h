@@ -106,6 +106,25 @@ float i2pc_profile_unproject_ms(void);
 int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,
                        float* out_xyz, float* out_rgb, void* stream);
 
+/* Statistical outlier removal of one cloud: replaces refine_point_cloud
+ * (backend/app.py:252-269), i.e. Open3D PointCloud::RemoveStatisticalOutliers
+ * (nb_neighbors, std_ratio) of open3d>=0.17.0 (backend/requirements.txt:14):
+ * avg[i] = mean distance to the min(nb_neighbors, n) nearest points (itself included,
+ * float64), keep i iff 0 < avg[i] < mean + std_ratio * std (Bessel), ascending order.
+ * Exact kNN on a device-sized uniform grid; stream-ordered, no host synchronisation.
+ * xyz       : float32 [n, 3] (finite; a non-finite cloud keeps nothing)
+ * rgb       : uint8 [n, 3] or NULL       out_rgb  : uint8 [n, 3] or NULL (needs rgb)
+ * out_xyz   : float32 [n, 3] or NULL     out_index: int64 [n] or NULL (Open3D's `ind`)
+ *             (the first *count rows of the outputs are the kept points, in index order)
+ * count     : int64 [1] number kept      bbox     : float64 [6] of the kept points or NULL
+ * avg_dist  : float64 [n] per-point mean neighbour distance, or NULL
+ * nb_neighbors in [1, 32], std_ratio > 0 (Open3D rejects the rest);
+ * workspace : i2pc_sor_workspace_bytes(n) bytes. */
+size_t i2pc_sor_workspace_bytes(int64_t n);
+int i2pc_sor(const float* xyz, const uint8_t* rgb, int64_t n, int nb_neighbors, double std_ratio,
+             float* out_xyz, uint8_t* out_rgb, int64_t* out_index, int64_t* count, double* bbox,
+             double* avg_dist, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------
  * Depth network building blocks (replace the PyTorch CPU conv / linear / SDPA /
  * LayerNorm arithmetic that process_with_depth_anything reaches through

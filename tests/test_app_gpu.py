@@ -26,6 +26,9 @@ def test_rest_job_matches_reference(pipeline_case, monkeypatch, tmp_path):
     depth = torch.from_numpy(pipeline_case["depth"]).cuda()
     monkeypatch.setattr(app_api, "load_model", lambda name: {"type": "depth"})
     monkeypatch.setattr(app_api, "_depth_device", lambda img, mi: depth)
+    # the fixture was recorded with Open3D absent: the reference's refine_point_cloud raised
+    # inside its try and returned the cloud unrefined (app.py:267-269)
+    monkeypatch.setattr(app_api, "REFINE_POINT_CLOUD", False)
     buf = io.BytesIO()
     Image.fromarray(pipeline_case["image"][:, :, ::-1]).save(buf, format="PNG")     # lossless: decodes to the same BGR
     c = TestClient(server.app)
