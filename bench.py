@@ -107,6 +107,25 @@ def _kernel_profile(pipe, images):
     return per, geo_t, (unp_ms * 1e-3 if unp_ms > 0 else None)
 
 
+def _pmc_traffic():
+    """HBM bytes per launch by kernel label from the newest profiles/r*_pmc_traffic.json
+    (tools/gpu_pmc_bench.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench,
+    gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or ({}, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return {}, None
+    with open(files[-1]) as fh:
+        return json.load(fh).get("kernels", {}), os.path.relpath(files[-1], ROOT)
+
+
+def _traffic(table, src, *names):
+    for n in names:
+        if n in table:
+            return table[n]["hbm_bytes_per_launch"], f"{src}: {n}"
+    return None, None
+
+
 def _cpu_baseline(spec, size, density):
     """Reference CPU path (restated) on one image of the bench's size, density high."""
     import numpy as np
@@ -203,6 +222,7 @@ def main():
     kernels = None
     if rank == 0 and not a.no_kernel_profile:
         per, geo_t, unp_t = _kernel_profile(pipe, images)
+        pmc, pmc_src = _pmc_traffic()
         dom = max(per.items(), key=lambda kv: kv[1]["t"])
         name, d = dom
         if d["flops"] > 0:
@@ -212,10 +232,12 @@ def main():
                         "launches": d["n"], "avg_us": round(d["t"] / d["n"] * 1e6, 2),
                         "flops_per_launch": d["flops"] / d["n"],
                         "share_of_step": round(d["t"] / (ms * 1e-3), 3)}
+            roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name)
         else:
             ach = d["bytes"] / (d["t"]) / 1e9
             roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+            roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name)
         geo_bytes = B * (4.0 * pipe.pre.out_h * pipe.pre.out_w + 18.0 * pipe.points_per_image)
         roof_geo = {"kernel": "i2pc_unproject (select + unproject + bbox launches)", "bound": "hbm",
                     "achieved": round(geo_bytes / geo_t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -230,6 +252,8 @@ def main():
                 "frac": round(a_unp / HBM_PEAK_GBS, 4), "traffic": None, "us": round(unp_t * 1e6, 1),
                 "bytes_per_launch": geo_bytes, "bytes_per_point": 18.0,
                 "note": "algorithmic bytes 4*h'*w' + 18*N per image (SURVEY 8d), one launch per batch"}
+            t, src = _traffic(pmc, pmc_src, "k_unproject_lane", "k_unproject_fast<1>")
+            rooflines["unproject_kernel"].update(traffic=t, traffic_source=src)
         net_t = sum(v["t"] for v in per.values())
         net_f = sum(v["flops"] for v in per.values())
         rooflines["dpt_blocks"] = {"kernel": "all network launches (GEMM/conv/attention/LN/resize/head)",

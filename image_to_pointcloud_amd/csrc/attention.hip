@@ -230,8 +230,9 @@ __device__ __forceinline__ v4s tr_read(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
-__global__ __launch_bounds__(256, 2) void k_attention_tr(const bf16_t* __restrict__ qkv, int B, int T, int NH,
-                                                         float scale_log2, bf16_t* __restrict__ out) {
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restrict__ qkv, int B, int T, int NH,
+                                                           float scale_log2, bf16_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * kTileBytes];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -398,11 +399,19 @@ extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads,
   const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
   const float scale_log2 = scale * 1.4426950408889634f;
   static const int old_kernel = [] { const char* e = getenv("I2PC_ATTN_OLD"); return e ? atoi(e) : 0; }();
+  // waves per SIMD the register budget targets (170 VGPRs at 2; <= 168 gives 3)
+  static const int occ = [] { const char* e = getenv("I2PC_ATTN_OCC"); return e ? atoi(e) : 3; }();
   if (old_kernel)
     hipLaunchKernelGGL(attn::k_attention, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+  else if (occ == 2)
+    hipLaunchKernelGGL(attn::k_attention_tr<2>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+  else if (occ == 4)
+    hipLaunchKernelGGL(attn::k_attention_tr<4>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
   else
-    hipLaunchKernelGGL(attn::k_attention_tr, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(attn::k_attention_tr<3>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
   return check_launch("attention");
 }

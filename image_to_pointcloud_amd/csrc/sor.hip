@@ -64,6 +64,32 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
   return x;
 }
 
+// Wave then block min/max of the ordered keys; one atomic per block and component (a
+// per-wave atomic on the same six addresses serialised into ~1 ms per pass).
+__device__ __forceinline__ void block_bbox_atomics(const uint32_t* mn, const uint32_t* mx, uint32_t* keys) {
+  __shared__ uint32_t red[6][kBlock / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const uint32_t a = wave_min(mn[c]), b = wave_max(mx[c]);
+    if (lane == 0) {
+      red[2 * c][wid] = a;
+      red[2 * c + 1][wid] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int c = threadIdx.x;
+    uint32_t x = red[c][0];
+    for (int w = 1; w < kBlock / 64; ++w) x = (c & 1) ? max(x, red[c][w]) : min(x, red[c][w]);
+    if (c & 1) {
+      if (x) atomicMax(&keys[c], x);
+    } else if (x != 0xffffffffu) {
+      atomicMin(&keys[c], x);
+    }
+  }
+}
+
 __global__ void k_init(State* st, int64_t* count) {
   const int t = threadIdx.x;
   if (t < 6) {
@@ -83,14 +109,7 @@ __global__ __launch_bounds__(kBlock) void k_bbox(const float* __restrict__ xyz, 
       mx[c] = max(mx[c], k);
     }
   }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const uint32_t a = wave_min(mn[c]), b = wave_max(mx[c]);
-    if ((threadIdx.x & 63) == 0) {
-      if (a != 0xffffffffu) atomicMin(&st->key[2 * c], a);
-      if (b) atomicMax(&st->key[2 * c + 1], b);
-    }
-  }
+  block_bbox_atomics(mn, mx, st->key);
 }
 
 // One thread: the smallest h (bisection) whose grid prod(floor(e/h)+1) has <= cap cells.
@@ -210,8 +229,14 @@ __global__ __launch_bounds__(kBlock) void k_knn(const float4* __restrict__ pts, 
             xs = xe = x;
           }
           const int s = (int)start[row + xs], e = (int)start[row + xe + 1];
-          for (int j = s; j < e; ++j) {
-            const float4 p = pts[j];
+          for (int j0 = s; j0 < e && !zero; j0 += 4) {
+            float4 pf[4];              // four candidate loads in flight per lane
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pf[u] = pts[min(j0 + u, e - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+            if (j0 + u >= e || zero) break;
+            const float4 p = pf[u];
             const double dx = qx - (double)p.x, dy = qy - (double)p.y, dz = qz - (double)p.z;
             const double d2 = (dx * dx + dy * dy) + dz * dz;
             ++held;
@@ -228,10 +253,8 @@ __global__ __launch_bounds__(kBlock) void k_knn(const float4* __restrict__ pts, 
               for (int m = 1; m < KC; ++m)
                 if (m == k - 1) b = best[m];
               dk = b;
-              if (dk == 0.0) {
-                zero = true;
-                break;
-              }
+              if (dk == 0.0) zero = true;
+            }
             }
           }
         }
@@ -323,14 +346,7 @@ __global__ __launch_bounds__(kBlock) void k_compact(const float* __restrict__ xy
     }
     if (oidx) oidx[j] = i;
   }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const uint32_t a = wave_min(mn[c]), b = wave_max(mx[c]);
-    if ((threadIdx.x & 63) == 0) {
-      if (a != 0xffffffffu) atomicMin(&st->kkey[2 * c], a);
-      if (b) atomicMax(&st->kkey[2 * c + 1], b);
-    }
-  }
+  block_bbox_atomics(mn, mx, st->kkey);
 }
 
 __global__ void k_finish(const State* st, double* bbox) {
@@ -418,7 +434,8 @@ static Layout layout(int64_t n) {
     o = align_up(o + bytes, 256);
     return at;
   };
-  L.cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(2 * n, 8), 1 << 24);
+  static const int cells_per_point = [] { const char* e = getenv("I2PC_SOR_CELLS"); return e ? atoi(e) : 4; }();
+  L.cap = (uint32_t)std::min<int64_t>(std::max<int64_t>(cells_per_point * n, 8), 1 << 24);
   const int64_t nc = (int64_t)L.cap + 1;
   L.grid = take(sizeof(Grid));
   L.state = take(sizeof(State));
@@ -436,7 +453,7 @@ static Layout layout(int64_t n) {
   return L;
 }
 
-static int grid_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 4096)); }
+static int grid_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 1024)); }
 
 }  // namespace sor
 }  // namespace i2pc

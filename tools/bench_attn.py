@@ -12,4 +12,4 @@ for B, T, H in [(32, 577, 16), (32, 1370, 6), (8, 1370, 6)]:
     for _ in range(20): ops.attention(qkv, B, T, H, 0.125, out=out)
     e1.record(); torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 20 * 1e-3
-    print(f"old={os.environ.get('I2PC_ATTN_OLD', '0')} B={B} T={T} H={H}: {t*1e6:8.1f} us {4*B*H*T*T*64/t/1e12:6.1f} TF")
+    print(f"old={os.environ.get('I2PC_ATTN_OLD', '0')} occ={os.environ.get('I2PC_ATTN_OCC', '-')} B={B} T={T} H={H}: {t*1e6:8.1f} us {4*B*H*T*T*64/t/1e12:6.1f} TF")
