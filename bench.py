@@ -252,7 +252,8 @@ def main():
                 "frac": round(a_unp / HBM_PEAK_GBS, 4), "traffic": None, "us": round(unp_t * 1e6, 1),
                 "bytes_per_launch": geo_bytes, "bytes_per_point": 18.0,
                 "note": "algorithmic bytes 4*h'*w' + 18*N per image (SURVEY 8d), one launch per batch"}
-            t, src = _traffic(pmc, pmc_src, "k_unproject_lane", "k_unproject_fast<1>")
+            step = {"high": 1, "medium": 2, "low": 4}[pipe.density]
+            t, src = _traffic(pmc, pmc_src, f"k_unproject_fast<{step}>")
             rooflines["unproject_kernel"].update(traffic=t, traffic_source=src)
         net_t = sum(v["t"] for v in per.values())
         net_f = sum(v["flops"] for v in per.values())

@@ -15,9 +15,9 @@ unproject_ref.py   numpy / pure-Python restatement of
 preprocess_ref.py  restatement of the DPT image processor (PIL bicubic resample,
                    rescale, normalize) that feeds the depth network
                    (app.py:103,109 -> transformers DPTImageProcessorPil).
-unproject_ref.c    the same unprojection arithmetic in C (fast full-size checks,
-                   multi-core-free scalar CPU baseline).
-pil_resample_ref.c integer restatement of Pillow's separable bicubic resample.
+sor_ref.py         restatement of refine_point_cloud (app.py:252-269): Open3D's
+                   RemoveStatisticalOutliers (open3d>=0.17.0) over an exact scipy
+                   cKDTree kNN, itself pinned to brute force.
 
 Parity pinning
 --------------
@@ -29,4 +29,10 @@ Parity pinning
   pinned against torch bilinear (align_corners=False) within fp32 rounding.
 * PIL bicubic resample: pinned bit-exact against Pillow 12.2 (present here and
   on the GPU box).
+* statistical outlier removal: Open3D is absent, so "parity unpinned" against
+  Open3D itself; the restatement's kNN is pinned to exhaustive search
+  (tests/test_sor.py).
+
+The reference's own C/C++ sources are not on this path (it is Python), so there
+is no oracle/_ref build.
 """
