@@ -98,6 +98,35 @@ def test_batched_mixed_branches_match_per_image_oracle():
                 assert _same_bits(rgb[i].astype(np.float32), ec)
 
 
+def test_full_width_mixed_branches_match_oracle():
+    """Resized depth, widths a multiple of 64 (the fast kernel's full-wave layout): every
+    normalisation branch, both inversions, points, colours and bbox bit-exact."""
+    g = _geom()
+    B, h, w, H, W = 6, 24, 40, 64, 128
+    deps = np.stack([_smooth_depth(h, w, 300 + i) for i in range(B)])
+    deps[1] = 3.0                                   # constant branch
+    deps[2] = 1.0; deps[2, 0, :5] = 4.0             # min/max float32 branch
+    deps[3, 5, 5] = np.nan; deps[3, 7, 9] = np.inf  # nanmedian fill
+    deps[4, :, :] = np.nan                          # all-NaN
+    imgs = np.stack([_rgb(H, W, 400 + i) for i in range(B)])
+    dev = torch.device("cuda")
+    for invert in (True, False):
+        pb = g.unproject_batch(torch.from_numpy(deps).to(dev), torch.from_numpy(imgs).to(dev),
+                               density="high", invert=invert, depth_scale=7.5)
+        xyz = pb.xyz.cpu().numpy()
+        rgb = pb.rgb.cpu().numpy()
+        bbox = pb.bbox.cpu().numpy()
+        for i in range(B):
+            with np.errstate(all="ignore"):
+                ep, ec = ref.depth_to_point_cloud(imgs[i], deps[i], density="high", invert=invert,
+                                                  depth_scale=7.5, loop=False)
+            assert _same_bits(xyz[i], ep), (i, invert, _first_diff(xyz[i], ep))
+            assert _same_bits(rgb[i].astype(np.float32), ec), (i, invert)
+            exp_bb = np.array([ep[:, 0].min(), ep[:, 0].max(), ep[:, 1].min(), ep[:, 1].max(),
+                               ep[:, 2].min(), ep[:, 2].max()], np.float64)
+            assert np.array_equal(bbox[i], exp_bb), (i, invert)
+
+
 def test_percentile_stats_match_numpy():
     g = _geom()
     dev = torch.device("cuda")
