@@ -31,6 +31,7 @@ SOURCES = [
     "attention.hip",
     "preprocess.hip",
     "sor.hip",
+    "head.hip",
     "writers.cpp",
 ]
 HEADERS = ["common.h", "../../include/i2pc.h"]

@@ -34,7 +34,7 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 
-from . import ops
+from . import dpt, ops
 from .dpt import _pack_conv
 from .preprocess import patch_pitch
 
@@ -359,6 +359,8 @@ class DepthAnythingModel:
             hidden = self._fuse(self.fusion[j], feat, hidden, size)
         t = ops.conv2d(hidden, self.w_h1, bias=self.b_h1)
         H, W = gh * s.patch, gw * s.patch
+        if dpt.FUSED_HEAD and s.head_hidden == 32:
+            return ops.head_upconv(t, H, W, self.w_h2, self.b_h2, self.w_h3, self.b_h3)
         u = ops.resize_bilinear(t, H, W, align_corners=True)
         t2 = ops.conv2d(u, self.w_h2, bias=self.b_h2, act="relu")
         return ops.head_out(t2, self.w_h3, self.b_h3)

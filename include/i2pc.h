@@ -204,6 +204,15 @@ int i2pc_f32_to_bf16(const float* x, int64_t n, void* y, void* stream);
 /* depth[b][p] = relu( sum_c x[b][p][c] * w[c] + bias ), x bf16 NHWC with c <= 64
  * (last 1x1 conv + ReLU of DPTDepthEstimationHead, modeling_dpt.py:701-702) */
 int i2pc_head_out(const void* x, int64_t pixels, int c, const float* w, float bias, float* depth, void* stream);
+/* Fused head tail (DPTDepthEstimationHead head[1..5], modeling_dpt.py:679-716, and the
+ * Depth-Anything head after conv1): depth[b][y][x] = relu(b4 + sum_co w4[co] *
+ * bf16(relu(b2[co] + conv3x3(resize_ac(x), w2)[co]))) where resize_ac is the bilinear
+ * align_corners=True resize of x (bf16 NHWC [batch, h, w, c], c % 64 == 0) to
+ * (out_h, out_w); w2: bf16 [32][9*c] packed (ky, kx, ci); b2, w4: fp32 [32]; depth fp32
+ * [batch, out_h, out_w].  Replaces i2pc_resize_bilinear + a 3x3 conv + i2pc_head_out
+ * without materialising the resized map. */
+int i2pc_head_upconv(const void* x, int batch, int h, int w, int c, int out_h, int out_w, const void* w2,
+                     const float* b2, const float* w4, float b4, float* depth, void* stream);
 
 /* ------------------------------------------------------------------------
  * Network input (app.py:103 cvtColor BGR->RGB + app.py:109 DPTImageProcessorPil):

@@ -164,3 +164,28 @@ def test_head_out(dev):
     got = ops.head_out(x, w, 0.25)
     ref = F.relu(x.float() @ w + 0.25)
     _close(got, ref, rel=1e-5, mx=1e-5)
+
+
+@pytest.mark.parametrize("B,h,w,C,H,W", [(2, 24, 24, 128, 48, 48), (1, 37, 37, 64, 518, 518),
+                                         (2, 19, 23, 128, 38, 46), (1, 1, 1, 64, 7, 9)])
+def test_head_upconv_matches_unfused_and_torch(dev, B, h, w, C, H, W):
+    """Fused resize -> 3x3 conv + ReLU -> 1x1 conv + ReLU against (1) the unfused kernels
+    (same bf16 rounding points; only the fp32 summation order differs) and (2) torch fp32."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(H + C)
+    x = _bf(torch.randn(B, h, w, C, generator=g)).to(dev)
+    w2 = _bf(torch.randn(32, C, 3, 3, generator=g) / math.sqrt(9 * C))
+    w2p = w2.permute(0, 2, 3, 1).reshape(32, 9 * C).contiguous().to(dev)
+    b2 = (torch.randn(32, generator=g) * 0.1).to(dev)
+    w4 = (torch.randn(32, generator=g) / math.sqrt(32)).to(dev)
+    b4 = 0.05
+    got = ops.head_upconv(x, H, W, w2p, b2, w4, b4)
+    assert got.shape == (B, H, W) and torch.isfinite(got).all()
+    u = ops.resize_bilinear(x, H, W, align_corners=True)
+    t2 = ops.conv2d(u, w2p, bias=b2, act="relu")
+    unfused = ops.head_out(t2, w4, b4)
+    _close(got, unfused, rel=2e-3, mx=5e-3)
+    xr = F.interpolate(x.float().permute(0, 3, 1, 2), size=(H, W), mode="bilinear", align_corners=True)
+    c = F.relu(F.conv2d(xr, w2.float().to(dev), b2, padding=1))
+    ref = F.relu((c * w4.view(1, 32, 1, 1)).sum(1) + b4)
+    _close(got, ref, rel=1.5e-2, mx=3e-2)
