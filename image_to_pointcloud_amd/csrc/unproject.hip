@@ -94,7 +94,7 @@ struct Geo {
 inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
-  size_t state, hist, xtab, ytab, field, tmp, total;
+  size_t state, hist, xtab, ytab, ex, field, tmp, total;
 };
 
 static Layout layout(int B, int H, int W, int smooth) {
@@ -104,6 +104,7 @@ static Layout layout(int B, int H, int W, int smooth) {
   L.hist = off;  off = align_up(off + sizeof(uint32_t) * kSlots * kBins * (size_t)B, 256);
   L.xtab = off;  off = align_up(off + sizeof(Tap) * (size_t)W, 256);
   L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
+  L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)B, 256);
   L.field = off;
   if (smooth) {
     off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
@@ -244,6 +245,8 @@ struct Sweep {
   int R;         // output rows per workgroup
   int nrb;       // row blocks per image
   int lds_rows;  // capacity of the LDS row window (0: sample from global)
+  int row0;      // first output row swept (a band of the image in tile-parallel mode)
+  int row_end;   // one past the last output row swept
 };
 
 __device__ __forceinline__ void map_rows(int bid, int B, int nrb, int& b, int& rb) { map_block(bid, B, nrb, b, rb); }
@@ -301,8 +304,8 @@ __global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32
   constexpr int bin_shift = LEVEL == 0 ? 21 : (LEVEL == 1 ? 10 : 0);
   constexpr uint32_t bin_mask = LEVEL == 2 ? 1023u : 2047u;
 
-  const int v0 = rb * sw.R;
-  const int v1 = min(g.H, v0 + sw.R);
+  const int v0 = sw.row0 + rb * sw.R;
+  const int v1 = min(sw.row_end, v0 + sw.R);
   for (int i = threadIdx.x; i < nslot * kBins; i += kBlock) sh[i] = 0;
   const int lo = stage_rows(g, b, v0, v1, rows, sw.lds_rows);
   const bool use_lds = sw.lds_rows > 0;
@@ -624,8 +627,8 @@ __global__ __launch_bounds__(kBlock) void k_unproject(Geo g, const SelState* st,
   const bool fill = S->has_med != 0;
   const float med = S->med;
   const int Hn = cam.N / cam.Wn;
-  const int r0 = rb * sw.R;
-  const int r1 = min(Hn, r0 + sw.R);
+  const int r0 = sw.row0 + rb * sw.R;
+  const int r1 = min(min(Hn, sw.row_end), r0 + sw.R);
   const int step = cam.step;
   const bool use_lds = !kField && sw.lds_rows > 0;
   int lo = 0;
@@ -788,8 +791,8 @@ __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState
   const bool fill = S->has_med != 0;
   const float med = S->med;
   const int Hn = cam.N / cam.Wn;
-  const int r0 = rb * sw.R;
-  const int r1 = min(Hn, r0 + sw.R);
+  const int r0 = sw.row0 + rb * sw.R;
+  const int r1 = min(min(Hn, sw.row_end), r0 + sw.R);
   const bool use_lds = sw.lds_rows > 0 && !g.same;
   int lo = 0;
   if (use_lds) {
@@ -1029,7 +1032,8 @@ __global__ void k_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n,
 constexpr int kRowBudget = 31 * 1024;   // LDS bytes for the staged model-row window (+32 KiB hist < 64 KiB)
 
 // Rows per workgroup so that the model-row window fits the LDS budget.
-static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same, int target_rows) {
+static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same, int target_rows, int row0 = 0,
+                        int row1 = -1) {
   Sweep sw{};
   int cap_rows = same ? 0 : kRowBudget / (int)(sizeof(float) * dw);
   int R = target_rows;
@@ -1040,7 +1044,10 @@ static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same
     cap_rows = 0;
   }
   sw.R = std::max(1, R);
-  sw.nrb = (rows_out + sw.R - 1) / sw.R;
+  if (row1 < 0) row1 = rows_out;
+  sw.row0 = row0;
+  sw.row_end = row1;
+  sw.nrb = std::max(1, (row1 - row0 + sw.R - 1) / sw.R);
   // allocate only the window R output rows can span (not the whole budget): occupancy
   if (cap_rows) cap_rows = std::min(cap_rows, (int)std::floor((double)(sw.R - 1) * step * dh / H) + 3);
   sw.lds_rows = cap_rows;
@@ -1049,15 +1056,59 @@ static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same
 
 static size_t sweep_lds(const Sweep& sw, int dw) { return sw.lds_rows ? (size_t)sw.lds_rows * dw * sizeof(float) : 0; }
 
+// Tile-parallel mode: the level-0 counters a sweep accumulates, out of / back into the
+// per-image state, as int64 [4][B] = {nan counts, non-finite counts, min key, max key}
+// (sum, sum, min, max across the bands).
+__global__ void k_band_export(const SelState* st, int B, int64_t* ex) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    ex[b] = st[b].nan_count;
+    ex[B + b] = st[b].nonfinite_count;
+    ex[2 * B + b] = st[b].kmin;
+    ex[3 * B + b] = st[b].kmax;
+  }
+}
+__global__ void k_band_import(SelState* st, int B, const int64_t* ex) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    st[b].nan_count = (uint32_t)ex[b];
+    st[b].nonfinite_count = (uint32_t)ex[B + b];
+    st[b].kmin = (uint32_t)ex[2 * B + b];
+    st[b].kmax = (uint32_t)ex[3 * B + b];
+  }
+}
+
+struct Exchange {
+  i2pc_exchange_fn fn;
+  void* user;
+  int64_t* ex;     // device int64 [4][B]
+};
+
+// Between a histogram sweep and its resolve, a band run hands the partial histograms (and,
+// at level 0, the counters) to the caller's collective, which must leave the sums (min /
+// max for the keys) over every band in place, ordered on `s`.
+template <int LEVEL>
+static int exchange(const Exchange* x, uint32_t* hist, SelState* st, int B, hipStream_t s) {
+  if (!x || !x->fn) return I2PC_OK;
+  if (LEVEL == 0) hipLaunchKernelGGL(k_band_export, dim3(1), dim3(64), 0, s, st, B, x->ex);
+  if (x->fn(x->user, hist, (int64_t)kSlots * kBins * B, LEVEL == 0 ? x->ex : nullptr, B, s) != 0)
+    return set_error(I2PC_ELAUNCH, "exchange callback failed at selection level %d", LEVEL);
+  if (LEVEL == 0) hipLaunchKernelGGL(k_band_import, dim3(1), dim3(64), 0, s, st, B, x->ex);
+  return I2PC_OK;
+}
+
 template <int PASS>
-static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, const Sweep& sw, hipStream_t s) {
+static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, const Sweep& sw, hipStream_t s,
+                         const Exchange* x = nullptr) {
   const size_t lds = sizeof(uint32_t) * kSlots * kBins + sweep_lds(sw, g.dw);
   const dim3 grid(B * sw.nrb), block(kBlock);
+  int rc;
   hipLaunchKernelGGL((k_sel_hist<0, PASS>), grid, block, lds, s, g, st, hist, B, sw);
+  if ((rc = exchange<0>(x, hist, st, B, s))) return rc;
   hipLaunchKernelGGL((k_sel_resolve<0, PASS>), dim3(B), block, 0, s, st, hist, B);
   hipLaunchKernelGGL((k_sel_hist<1, PASS>), grid, block, lds, s, g, st, hist, B, sw);
+  if ((rc = exchange<1>(x, hist, st, B, s))) return rc;
   hipLaunchKernelGGL((k_sel_resolve<1, PASS>), dim3(B), block, 0, s, st, hist, B);
   hipLaunchKernelGGL((k_sel_hist<2, PASS>), grid, block, lds, s, g, st, hist, B, sw);
+  if ((rc = exchange<2>(x, hist, st, B, s))) return rc;
   hipLaunchKernelGGL((k_sel_resolve<2, PASS>), dim3(B), block, 0, s, st, hist, B);
   return check_launch("select");
 }
@@ -1104,11 +1155,13 @@ extern "C" size_t i2pc_unproject_workspace_bytes(int batch, int img_h, int img_w
   return layout(batch, img_h, img_w, smooth).total;
 }
 
-extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const uint8_t* image, int channels,
-                              int batch, int img_h, int img_w, const i2pc_unproject_params* params,
-                              float* xyz, uint8_t* rgb, double* bbox, double* stats,
-                              void* workspace, size_t workspace_bytes, void* stream) {
-  clear_error();
+// Band [row0, row1) of the image rows (the whole image when row0 = 0, row1 = img_h);
+// `image`, `xyz`, `rgb` address the full image (band runs pass offset pointers).
+static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t* image, int channels,
+                         int batch, int img_h, int img_w, const i2pc_unproject_params* params,
+                         float* xyz, uint8_t* rgb, double* bbox, double* stats,
+                         void* workspace, size_t workspace_bytes, void* stream, int row0, int row1,
+                         const Exchange* xch) {
   I2PC_REQUIRE(params != nullptr, "params is NULL");
   I2PC_REQUIRE(depth && image && xyz && rgb && workspace, "NULL device pointer");
   I2PC_REQUIRE(batch > 0 && img_h > 0 && img_w > 0 && dep_h > 0 && dep_w > 0, "empty shape");
@@ -1140,10 +1193,12 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
   // selection sweeps: ~8 output rows per workgroup for 1024-wide images
   const int sel_rows = std::max(1, std::min(16, (8 * 1024 + img_w - 1) / img_w));
-  const Sweep ssel = plan_sweep(img_h, 1, dep_h, dep_w, img_h, g.same != 0, sel_rows);
-  int rc = launch_select<0>(g, st, hist, batch, ssel, s);
+  const Sweep ssel = plan_sweep(img_h, 1, dep_h, dep_w, img_h, g.same != 0, sel_rows, row0, row1);
+  Exchange xb = xch ? *xch : Exchange{nullptr, nullptr, nullptr};
+  xb.ex = reinterpret_cast<int64_t*>(ws + L.ex);
+  int rc = launch_select<0>(g, st, hist, batch, ssel, s, xch ? &xb : nullptr);
   if (rc) return rc;
-  rc = launch_select<1>(g, st, hist, batch, ssel, s);
+  rc = launch_select<1>(g, st, hist, batch, ssel, s, xch ? &xb : nullptr);
   if (rc) return rc;
 
   Cam cam;
@@ -1162,7 +1217,8 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
   const int Hn = (img_h + step - 1) / step;
   cam.N = cam.Wn * Hn;
   const int unp_rows = std::max(1, std::min(kMaxRows, (4 * 1024 + cam.Wn - 1) / cam.Wn));
-  const Sweep sunp = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, unp_rows);
+  const int prow0 = row0 / step, prow1 = (row1 + step - 1) / step;   // point rows of the band
+  const Sweep sunp = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, unp_rows, prow0, prow1);
   const size_t unp_lds = sweep_lds(sunp, dep_w);
   const double* field = nullptr;
   if (params->smooth) {
@@ -1179,7 +1235,7 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
     // 8 rows of 1024 points (or the equivalent) per workgroup
     static const int pts_per_wg = [] { const char* e = getenv("I2PC_UNP_PTS"); return e ? atoi(e) : 8192; }();
     const int fast_rows = std::max(1, std::min(16, (pts_per_wg + cam.Wn - 1) / cam.Wn));
-    const Sweep sf = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, fast_rows);
+    const Sweep sf = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, fast_rows, prow0, prow1);
     const size_t lf = sweep_lds(sf, dep_w);
     const dim3 grid(batch * sf.nrb), block(kBlock);
     prof_mark(0, s);
@@ -1196,6 +1252,40 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
   }
   hipLaunchKernelGGL(k_finalize, dim3((batch + 63) / 64), dim3(64), 0, s, st, batch, bbox, stats);
   return check_launch("unproject");
+}
+
+extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const uint8_t* image, int channels,
+                              int batch, int img_h, int img_w, const i2pc_unproject_params* params,
+                              float* xyz, uint8_t* rgb, double* bbox, double* stats,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  return run_unproject(depth, dep_h, dep_w, image, channels, batch, img_h, img_w, params, xyz, rgb, bbox, stats,
+                       workspace, workspace_bytes, stream, 0, img_h, nullptr);
+}
+
+extern "C" int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
+                                   int img_h, int img_w, int row0, int row1, const i2pc_unproject_params* params,
+                                   float* xyz_band, uint8_t* rgb_band, double* bbox, double* stats,
+                                   void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange_fn,
+                                   void* user, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(params != nullptr, "params is NULL");
+  I2PC_REQUIRE(image_band && xyz_band && rgb_band, "NULL device pointer");
+  I2PC_REQUIRE(img_h > 0 && img_w > 0 && channels >= 1 && channels <= 4, "bad image shape");
+  const int step = params->step;
+  I2PC_REQUIRE(step == 1 || step == 2 || step == 4, "step must be 1, 2 or 4 (low/medium/high)");
+  I2PC_REQUIRE(0 <= row0 && row0 < row1 && row1 <= img_h, "band rows [%d, %d) outside [0, %d)", row0, row1, img_h);
+  I2PC_REQUIRE(row0 % step == 0 && (row1 % step == 0 || row1 == img_h),
+               "band rows must start (and end, unless at the bottom) on a multiple of the step %d", step);
+  if (params->smooth) return set_error(I2PC_EUNSUPPORTED, "smooth_depth blurs across bands: not in tile-parallel mode");
+  // the kernels address the full image: shift the band buffers back to row 0
+  const int Wn = (img_w + step - 1) / step;
+  const uint8_t* image = image_band - (ptrdiff_t)row0 * img_w * channels;
+  float* xyz = xyz_band - (ptrdiff_t)(row0 / step) * Wn * 3;
+  uint8_t* rgb = rgb_band - (ptrdiff_t)(row0 / step) * Wn * 3;
+  const Exchange x{exchange_fn, user, nullptr};
+  return run_unproject(depth, dep_h, dep_w, image, channels, 1, img_h, img_w, params, xyz, rgb, bbox, stats,
+                       workspace, workspace_bytes, stream, row0, row1, exchange_fn ? &x : nullptr);
 }
 
 extern "C" int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,

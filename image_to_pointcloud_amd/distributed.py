@@ -53,3 +53,33 @@ def max_over_ranks(seconds: float, device=None) -> float:
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def band_exchange(group=None):
+    """The all-reduce i2pc_unproject_band needs between selection sweeps (C4 tile-parallel
+    mode): histogram words and level-0 counts summed, key range min / max, over RCCL."""
+    import torch.distributed as dist
+
+    def _exchange(hist, counters):
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+        if counters is not None:
+            sums, kmin, kmax = counters[:2].contiguous(), counters[2].contiguous(), counters[3].contiguous()
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(kmin, op=dist.ReduceOp.MIN, group=group)
+            dist.all_reduce(kmax, op=dist.ReduceOp.MAX, group=group)
+            counters[:2].copy_(sums)
+            counters[2].copy_(kmin)
+            counters[3].copy_(kmax)
+    return _exchange
+
+
+def reduce_bbox(bbox, group=None):
+    """Global bounds from per-band bboxes [6] (min x, max x, min y, max y, min z, max z)."""
+    import torch.distributed as dist
+    mins, maxs = bbox[0::2].contiguous(), bbox[1::2].contiguous()
+    dist.all_reduce(mins, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(maxs, op=dist.ReduceOp.MAX, group=group)
+    out = bbox.clone()
+    out[0::2] = mins
+    out[1::2] = maxs
+    return out

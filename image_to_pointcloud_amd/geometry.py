@@ -197,3 +197,98 @@ def remove_statistical_outlier(xyz, rgb=None, nb_neighbors: int = 20, std_ratio:
               _ptr(oidx), _ptr(cnt), _ptr(bbox), _ptr(avg), _ptr(ws), ws.numel(), _stream_handle())
     m = int(cnt.item())
     return SorResult(oxyz[:m], orgb[:m] if orgb is not None else None, oidx[:m], bbox, avg)
+
+
+# ----------------------------------------------------------------- tile-parallel (C4)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                               ctypes.c_int, ctypes.c_void_p)
+_lib.register("i2pc_unproject_band", ctypes.c_int,
+              [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+               ctypes.c_int, ctypes.c_int, ctypes.POINTER(_lib.UnprojectParams), ctypes.c_void_p, ctypes.c_void_p,
+               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, EXCHANGE_FN, ctypes.c_void_p,
+               ctypes.c_void_p])
+
+
+class _DevView:
+    """A device buffer handed over by the C side, viewed as a torch tensor (no copy)."""
+
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 2}
+
+
+def _as_tensor(ptr: int, n: int, typestr: str):
+    torch = _torch()
+    return torch.as_tensor(_DevView(ptr, n, typestr), device="cuda")
+
+
+def band_rows(img_h: int, parts: int, step: int = 1) -> list:
+    """Split image rows into `parts` contiguous bands [row0, row1) whose starts are multiples
+    of the density step (so every band owns whole point rows), as even as that allows."""
+    rows_pts = (img_h + step - 1) // step
+    out = []
+    for r in range(parts):
+        p0 = rows_pts * r // parts
+        p1 = rows_pts * (r + 1) // parts
+        out.append((min(p0 * step, img_h), min(p1 * step, img_h)))
+    return out
+
+
+def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: int, exchange,
+                   density: str = "high", invert: bool = True, depth_scale: float = 10.0,
+                   fov: Optional[float] = None, workspace=None):
+    """This rank's band [row0, row1) of one image's unprojection (i2pc_unproject_band).
+
+    depth      : torch.float32 [h, w] model-resolution depth of the WHOLE image (device)
+    image_band : torch.uint8 [row1 - row0, img_w, C] the band's image rows (device)
+    exchange   : callable(hist: int32 tensor, counters: int64 [4, B] tensor or None) that
+                 all-reduces in place across the ranks (hist SUM; counters rows 0-1 SUM,
+                 row 2 MIN, row 3 MAX) -- e.g. distributed.band_exchange(group)
+    workspace  : optional device uint8 buffer (default: the per-device cached one)
+    -> (xyz [Nb, 3] f32, rgb [Nb, 3] u8, band bbox f64 [6], stats f64 [4]) on the device.
+    """
+    torch = _torch()
+    if density not in DENSITY_STEP:
+        raise KeyError(density)
+    step = DENSITY_STEP[density]
+    if image_band.dim() == 2:
+        image_band = image_band.unsqueeze(-1)
+    if not depth.is_cuda or not image_band.is_cuda:
+        raise _lib.I2PCError("unproject_band expects device tensors")
+    depth = depth.contiguous().to(torch.float32)
+    image_band = image_band.contiguous()
+    C = image_band.shape[-1]
+    if tuple(image_band.shape[:2]) != (row1 - row0, img_w):
+        raise ValueError(f"image_band {tuple(image_band.shape)} does not hold rows [{row0}, {row1}) x {img_w}")
+    wn = (img_w + step - 1) // step
+    nb = ((row1 + step - 1) // step - row0 // step) * wn
+    dev = depth.device
+    xyz = torch.empty((nb, 3), dtype=torch.float32, device=dev)
+    rgb = torch.empty((nb, 3), dtype=torch.uint8, device=dev)
+    bbox = torch.empty(6, dtype=torch.float64, device=dev)
+    stats = torch.empty(4, dtype=torch.float64, device=dev)
+    lib = _lib.load()
+    ws = workspace if workspace is not None else _workspace(lib.i2pc_unproject_workspace_bytes(1, img_h, img_w, 0), dev)
+    errors = []
+
+    def _cb(user, hist, words, counters, batch, stream):
+        try:
+            h = _as_tensor(hist, int(words), "<i4")
+            c = _as_tensor(counters, 4 * int(batch), "<i8").view(4, int(batch)) if counters else None
+            exchange(h, c)
+            return 0
+        except Exception as e:           # surfaced after the call returns
+            errors.append(e)
+            return 1
+
+    cb = EXCHANGE_FN(_cb)
+    p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
+                             fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5)
+    try:
+        _lib.call("i2pc_unproject_band", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
+                  img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),
+                  _ptr(ws), ws.numel(), cb, None, _stream_handle())
+    except _lib.I2PCError:
+        if errors:
+            raise errors[0]
+        raise
+    return xyz, rgb, bbox, stats

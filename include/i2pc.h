@@ -81,6 +81,33 @@ int i2pc_unproject(const float* depth, int dep_h, int dep_w,
                    float* xyz, uint8_t* rgb, double* bbox, double* stats,
                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* Tile-parallel unprojection of ONE image split into row bands across ranks (SURVEY
+ * §8e, config C4: an 8192 x 4096 panorama across 8 GPUs).  Each rank calls this for its
+ * band [row0, row1) of the image rows with the full model-resolution depth; the exact
+ * global p2/p98 (and nanmedian) need the histograms of every band, so between each
+ * selection sweep and its resolve the call hands its partial histograms to `exchange`,
+ * which must all-reduce them in place across the ranks (ordered on `stream`):
+ *   hist     : uint32 [hist_words] -> element-wise SUM over ranks
+ *   counters : int64 [4][batch] or NULL -> rows 0-1 SUM, row 2 MIN, row 3 MAX
+ * and return 0 (non-zero aborts the call).  Every rank must make the same sequence of
+ * calls (6 per image: 3 levels x 2 passes).
+ * image_band : uint8 [row1 - row0, img_w, channels]   the band's rows of the image
+ * xyz_band   : float32 [Nb, 3], rgb_band uint8 [Nb, 3] with Nb = (ceil(row1/step) -
+ *              row0/step) * ceil(img_w/step): the band's points, row-major, i.e. the
+ *              slice [row0/step * ceil(img_w/step), ...) of the whole image's points
+ * bbox       : float64 [6] of this band's points (the caller min/max-reduces them)
+ * stats      : float64 [4] as i2pc_unproject (identical on every rank)
+ * row0 must be a multiple of step, and row1 too unless row1 == img_h; smooth is not
+ * supported (the blur crosses bands).  workspace: i2pc_unproject_workspace_bytes(1,
+ * img_h, img_w, 0). */
+typedef int (*i2pc_exchange_fn)(void* user, uint32_t* hist, int64_t hist_words, int64_t* counters, int batch,
+                                void* stream);
+int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
+                        int img_h, int img_w, int row0, int row1, const i2pc_unproject_params* params,
+                        float* xyz_band, uint8_t* rgb_band, double* bbox, double* stats,
+                        void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange, void* user,
+                        void* stream);
+
 /* Depth preview image (create_depth_preview, backend/app.py:124-172) for a batch of
  * model-resolution depth maps, before any resize: nanmedian fill, exact p2/p98 of
  * the map itself, clip/normalise/invert exactly as i2pc_unproject, then

@@ -64,3 +64,49 @@ def test_gather_points_image_major_and_max_clock():
             assert (gx[img, :, 0] == img + torch.arange(5).numpy()).all()
             assert (gr[img] == img).all()
         assert t == 2.0
+
+
+def test_band_rows_partition():
+    from image_to_pointcloud_amd.geometry import band_rows
+    for h in (1, 7, 100, 4096, 4097):
+        for parts in (1, 2, 3, 8):
+            for step in (1, 2, 4):
+                bands = band_rows(h, parts, step)
+                assert len(bands) == parts and bands[0][0] == 0 and bands[-1][1] == h
+                for (a0, a1), (b0, b1) in zip(bands, bands[1:]):
+                    assert a1 == b0
+                for r0, r1 in bands:
+                    assert r0 % step == 0 and (r1 % step == 0 or r1 == h) and r0 <= r1
+
+
+def _band_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        ex = D.band_exchange()
+        hist = torch.arange(8, dtype=torch.int32) * (rank + 1)
+        cnt = torch.tensor([[rank + 1], [10 * rank], [100 - rank], [7 + rank]], dtype=torch.int64)
+        ex(hist, cnt)
+        bb = torch.tensor([rank, rank + 5.0, -rank, 2.0, 0.5 * rank, 1.0 + rank], dtype=torch.float64)
+        q.put((rank, hist.numpy().copy(), cnt.numpy().copy(), D.reduce_bbox(bb).numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_band_exchange_protocol():
+    """The C4 exchange i2pc_unproject_band calls between selection sweeps: histogram SUM,
+    level-0 counts SUM, key MIN / MAX; and the band bbox min / max."""
+    ws, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_band_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, hist, cnt, bb in out:
+        assert hist.tolist() == [3 * i for i in range(8)]
+        assert cnt[:, 0].tolist() == [3, 10, 99, 8]
+        assert bb.tolist() == [0.0, 6.0, -1.0, 2.0, 0.0, 2.0]

@@ -193,3 +193,72 @@ def test_bad_arguments_raise():
         g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), density="ultra")
     with pytest.raises(I2PCError):
         g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), smooth=True, smooth_ksize=9)
+
+
+@pytest.mark.parametrize("density,parts", [("high", 1), ("high", 3), ("medium", 2), ("low", 4)])
+def test_band_unproject_matches_whole_image(density, parts):
+    """C4 tile-parallel mode: `parts` ranks (threads on their own streams here, with an
+    in-process all-reduce as the exchange) each unproject a row band of one image; the
+    concatenated bands are bit-identical to the whole-image unprojection, every rank gets
+    the same p2/p98 / nanmedian stats, and the min/max of the band bboxes is the bbox."""
+    import threading
+    g = _geom()
+    dev = torch.device("cuda")
+    h, w, H, W = 48, 64, 301, 410
+    dep = _smooth_depth(h, w, 51)
+    dep[3, 4] = np.nan                      # exercises the nanmedian pass as well
+    img = _rgb(H, W, 52)
+    tdep = torch.from_numpy(dep).to(dev)
+    timg = torch.from_numpy(img).to(dev)
+    whole = g.unproject_batch(tdep[None], timg[None], density=density, depth_scale=12.0)
+    torch.cuda.synchronize()
+    step = g.DENSITY_STEP[density]
+    bands = g.band_rows(H, parts, step)
+    results, slots, errs = [None] * parts, [None] * parts, []
+    bar = threading.Barrier(parts)
+    nbytes = g._lib.load().i2pc_unproject_workspace_bytes(1, H, W, 0)
+
+    def exchange_for(i):
+        def ex(hist, cnt):
+            torch.cuda.current_stream().synchronize()
+            slots[i] = (hist.clone(), None if cnt is None else cnt.clone())
+            bar.wait()
+            hist.copy_(torch.stack([s[0] for s in slots]).sum(0).to(torch.int32))
+            if cnt is not None:
+                c = torch.stack([s[1] for s in slots])
+                cnt[:2] = c[:, :2].sum(0)
+                cnt[2] = c[:, 2].min(0).values
+                cnt[3] = c[:, 3].max(0).values
+            torch.cuda.current_stream().synchronize()
+            bar.wait()
+        return ex
+
+    def run(i):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                r0, r1 = bands[i]
+                ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                results[i] = g.unproject_band(tdep, timg[r0:r1], H, W, r0, r1, exchange_for(i), density=density,
+                                              depth_scale=12.0, workspace=ws)
+                torch.cuda.current_stream().synchronize()
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(e)
+            bar.abort()
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(parts)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errs, errs
+    xyz = torch.cat([r[0] for r in results]).cpu().numpy()
+    rgb = torch.cat([r[1] for r in results]).cpu().numpy()
+    assert _same_bits(xyz, whole.xyz[0].cpu().numpy()), _first_diff(xyz, whole.xyz[0].cpu().numpy())
+    assert _same_bits(rgb, whole.rgb[0].cpu().numpy())
+    for r in results:
+        assert _same_bits(r[3].cpu().numpy(), whole.stats[0].cpu().numpy())
+    bb = torch.stack([r[2] for r in results]).cpu().numpy()
+    glob = np.empty(6)
+    glob[0::2] = bb[:, 0::2].min(0)
+    glob[1::2] = bb[:, 1::2].max(0)
+    assert _same_bits(glob, whole.bbox[0].cpu().numpy())
