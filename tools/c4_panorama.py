@@ -1,0 +1,102 @@
+"""C4: tile-parallel unprojection of one 8192 x 4096 panorama across the ranks of one node.
+
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P tools/c4_panorama.py [--height 4096 --width 8192 --steps 10]
+
+Each rank holds the model-resolution depth (518 x 1036, the Depth-Anything processor's
+keep-aspect size for 2:1; synthetic smooth field + a NaN) and ONLY its band of
+the image rows; i2pc_unproject_band runs the exact global p2/p98 through three histogram
+all-reduces per selection pass (RCCL when every rank has its own GPU, gloo when ranks share
+one), then unprojects its band.  Rank 0 prints one JSON line (points/s over the job, max
+over ranks), and --check compares every band bit-for-bit with the whole-image unprojection.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from image_to_pointcloud_amd import distributed as D
+from image_to_pointcloud_amd import geometry as G
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--height", type=int, default=4096)
+    ap.add_argument("--width", type=int, default=8192)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--density", default="high")
+    ap.add_argument("--check", action="store_true")
+    a = ap.parse_args()
+    rank, local, world = D.world()
+    ngpu = torch.cuda.device_count()
+    backend = "nccl" if world <= ngpu else "gloo"
+    dev = torch.device("cuda", local % ngpu)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend)
+    H, W = a.height, a.width
+    h, w = 518, 1036
+    rng = np.random.Generator(np.random.PCG64(1))
+    v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    dep = (0.5 + 4.5 * (0.5 + 0.5 * np.sin(6 * np.pi * u / w) * np.cos(4 * np.pi * v / h))
+           + rng.normal(0, 0.05, (h, w))).astype(np.float32)
+    dep[7, 11] = np.nan
+    tdep = torch.from_numpy(dep).to(dev)
+    step = G.DENSITY_STEP[a.density]
+    r0, r1 = G.band_rows(H, world, step)[rank]
+    # this rank's image rows only (row y of the synthetic panorama is seeded 1000 + y)
+    band = np.empty((r1 - r0, W, 3), np.uint8)
+    for y in range(r0, r1):
+        band[y - r0] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
+    timg = torch.from_numpy(band).to(dev)
+    ex = D.band_exchange() if world > 1 else (lambda hist, cnt: None)
+    res = None
+    for _ in range(a.warmup):
+        res = G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = D.max_over_ranks(time.perf_counter() - t0, dev) if world > 1 else time.perf_counter() - t0
+    bbox = D.reduce_bbox(res[2]) if world > 1 else res[2]
+    ok = None
+    if a.check:
+        full = np.empty((H, W, 3), np.uint8)
+        for y in range(H):
+            full[y] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
+        whole = G.unproject_batch(tdep[None], torch.from_numpy(full).to(dev)[None], density=a.density)
+        wn = (W + step - 1) // step
+        p0 = (r0 // step) * wn
+        ok = bool(torch.equal(whole.xyz[0][p0:p0 + res[0].shape[0]], res[0])
+                  and torch.equal(whole.rgb[0][p0:p0 + res[1].shape[0]], res[1])
+                  and torch.equal(whole.stats[0], res[3]) and torch.equal(whole.bbox[0], bbox))
+        if world > 1:
+            t = torch.tensor([int(ok)], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = bool(t.item())
+    n = ((H + step - 1) // step) * ((W + step - 1) // step)
+    if rank == 0:
+        print(json.dumps({"metric": "Mpoints/sec tile-parallel unprojection of one panorama (C4)",
+                          "value": round(n * a.steps / el / 1e6, 1), "unit": "Mpoints/s", "n_ranks": world,
+                          "backend": backend if world > 1 else None, "ms_per_image": round(el / a.steps * 1e3, 3),
+                          "image": [H, W], "depth": [h, w], "density": a.density, "points": n,
+                          "bit_exact_vs_whole_image": ok, "stats": res[3].tolist(), "bbox": bbox.tolist()}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
