@@ -32,7 +32,7 @@ from typing import Any, Dict, Optional
 import numpy as np
 from pydantic import BaseModel
 
-from . import geometry, preview, writers
+from . import geometry, preprocess, preview, writers
 
 logger = logging.getLogger(__name__)
 
@@ -244,9 +244,12 @@ def process_image_pipeline(job_id: str, image_data: bytes, request: ProcessingRe
         model_info = load_model(request.model)
         job.update(progress=20, message="Processing image...")
         image = decode_image(image_data)
-        if max(image.shape[:2]) > MAX_IMAGE_DIM:
-            raise ValueError(f"images above {MAX_IMAGE_DIM} px need the INTER_AREA downscale (app.py:438-445), "
-                             "not implemented in this backend")
+        size = preprocess.reference_downscale_size(image.shape[0], image.shape[1], MAX_IMAGE_DIM)
+        if size is not None:                                # app.py:436-445 (cv2 INTER_AREA)
+            import torch
+            dev = geometry.require_device()
+            image = preprocess.resize_area(torch.from_numpy(np.ascontiguousarray(image)).to(dev), *size).cpu().numpy()
+            logger.info(f"Resized input image to {size[0]}x{size[1]} for processing")
         if model_info.get("type") != "depth":
             raise ValueError(f"model {request.model} has no depth branch in this backend")
         job.update(progress=40, message="Estimating depth with AI...")

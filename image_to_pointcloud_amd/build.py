@@ -32,6 +32,7 @@ SOURCES = [
     "preprocess.hip",
     "sor.hip",
     "head.hip",
+    "area.hip",
     "writers.cpp",
 ]
 HEADERS = ["common.h", "../../include/i2pc.h"]

@@ -105,3 +105,32 @@ class Preprocessor:
         _lib.call("i2pc_preprocess", self._h, bgr.data_ptr(), B, code, out.data_ptr(),
                   torch.cuda.current_stream().cuda_stream)
         return out
+
+
+_lib.register("i2pc_resize_area", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
+
+
+def reference_downscale_size(h: int, w: int, max_dim: int = 3072):
+    """app.py:437-443: (new_w, new_h) when max(h, w) > max_dim, else None."""
+    m = max(h, w)
+    if m <= max_dim:
+        return None
+    scale = max_dim / float(m)
+    return int(round(w * scale)), int(round(h * scale))
+
+
+def resize_area(images, out_w: int, out_h: int, out=None):
+    """cv2.resize(img, (out_w, out_h), interpolation=cv2.INTER_AREA) for uint8 downscaling on the
+    device (i2pc_resize_area).  images: torch.uint8 [H, W, C] or [B, H, W, C] on the device."""
+    import torch
+    x = images if images.dim() == 4 else images.unsqueeze(0)
+    if x.dtype != torch.uint8 or not x.is_cuda:
+        raise TypeError("resize_area expects a device uint8 tensor")
+    x = x.contiguous()
+    B, H, W, C = x.shape
+    if out is None:
+        out = torch.empty((B, out_h, out_w, C), dtype=torch.uint8, device=x.device)
+    _lib.call("i2pc_resize_area", x.data_ptr(), B, H, W, C, out.data_ptr(), out_h, out_w,
+              torch.cuda.current_stream().cuda_stream)
+    return out if images.dim() == 4 else out[0]

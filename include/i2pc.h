@@ -241,6 +241,14 @@ int i2pc_head_out(const void* x, int64_t pixels, int c, const float* w, float bi
 int i2pc_head_upconv(const void* x, int batch, int h, int w, int c, int out_h, int out_w, const void* w2,
                      const float* b2, const float* w4, float b4, float* depth, void* stream);
 
+/* Area-averaging downscale, cv2.resize(image, (out_w, out_h), interpolation=INTER_AREA)
+ * as process_image_pipeline applies it above 3072 px (backend/app.py:436-445); OpenCV's
+ * published algorithm restated (parity against cv2 unpinned: not installed here).
+ * src uint8 [batch, h, w, channels] -> dst uint8 [batch, out_h, out_w, channels];
+ * out_h <= h and out_w <= w (EUNSUPPORTED otherwise). */
+int i2pc_resize_area(const uint8_t* src, int batch, int h, int w, int channels, uint8_t* dst, int out_h, int out_w,
+                     void* stream);
+
 /* ------------------------------------------------------------------------
  * Network input (app.py:103 cvtColor BGR->RGB + app.py:109 DPTImageProcessorPil):
  * Pillow-exact bicubic resample, rescale 1/255, normalise, optional patchify.
