@@ -34,8 +34,10 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 }
 
 __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
-  __bf16 x = (__bf16)a, y = (__bf16)b;
-  return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
+  // one v_cvt_pk_bf16_f32 for the pair (RNE), no shift/or repacking
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
 
 // V^T image: row d (128 B = 64 keys), 8-byte units of 4 keys swizzled by (d >> 1) & 15.
@@ -322,7 +324,9 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[k2][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       const float m_new = fmaxf(m_run, mx);
-      const float alpha = exp2f((m_run - m_new) * c);
+      // raw v_exp_f32 (ocml's exp2f adds 4 VALU ops per call for denormal results, which
+      // only matter for probabilities < 2^-126 of a sum >= 1)
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
       const float mc = m_new * c;
       m_run = m_new;
       float ls = 0.f;
@@ -331,8 +335,8 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
       for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const float p0 = exp2f(__builtin_fmaf(st[k2][r], c, -mc));
-          const float p1 = exp2f(__builtin_fmaf(st[k2][r + 1], c, -mc));
+          const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(st[k2][r], c, -mc));
+          const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(st[k2][r + 1], c, -mc));
           ls += p0 + p1;
           pk[k2][r >> 1] = pack_bf16(p0, p1);
         }
@@ -360,9 +364,7 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
             const int r0 = kb + tq, r1 = kb + 8 + tq;
             const v4s lo = tr_read(sV + r0 * 128 + ((lch ^ v_swz(r0)) << 4) + within);
             const v4s hi = tr_read(sV + r1 * 128 + ((lch ^ v_swz(r1)) << 4) + within);
-            typedef short v8s __attribute__((ext_vector_type(8)));
-            const v8s u = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            const bf16x8 vf = __builtin_bit_cast(bf16x8, u);
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
           }
         }
