@@ -298,13 +298,13 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
         if (k2 == 1 && half) break;
-        for (int i = 0; i < 16; ++i) st[k2][i] = 0.f;
         const int key = 32 * k2 + lq;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int lchunk = 2 * s + hh;
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ (key & 7)) << 4));
-          st[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[k2], 0, 0, 0);
+          // s == 0 starts from an inline-constant zero accumulator (no 16 v_movs per chain)
+          st[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? f32x16{} : st[k2], 0, 0, 0);
         }
       }
       if (half) for (int i = 0; i < 16; ++i) st[1][i] = -INFINITY;
@@ -335,8 +335,11 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
       for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(st[k2][r], c, -mc));
-          const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(st[k2][r + 1], c, -mc));
+          typedef float f32x2 __attribute__((ext_vector_type(2)));
+          const f32x2 e = __builtin_elementwise_fma(f32x2{st[k2][r], st[k2][r + 1]}, f32x2{c, c},
+                                                    f32x2{-mc, -mc});     // one v_pk_fma_f32 per pair
+          const float p0 = __builtin_amdgcn_exp2f(e.x);
+          const float p1 = __builtin_amdgcn_exp2f(e.y);
           ls += p0 + p1;
           pk[k2][r >> 1] = pack_bf16(p0, p1);
         }
