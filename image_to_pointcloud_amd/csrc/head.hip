@@ -34,7 +34,14 @@ __device__ __forceinline__ bf16_t f2bf(float x) {
   __bf16 b = (__bf16)x;
   return *reinterpret_cast<bf16_t*>(&b);
 }
-__device__ __forceinline__ uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 per pair (RNE, as the scalar conversions)
+__device__ __forceinline__ uint32_t pack2(f32x2 v) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2)); }
+// the two bf16 of a dword as floats
+__device__ __forceinline__ f32x2 unpack2(uint32_t u) {
+  return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
 
 __global__ __launch_bounds__(256, 2) void k_head_upconv(const bf16_t* __restrict__ x, int h, int w, int C, int H,
                                                         int W, int tiles_w, int tiles_h,
@@ -100,17 +107,14 @@ __global__ __launch_bounds__(256, 2) void k_head_upconv(const bf16_t* __restrict
         const uint32_t* p11 = reinterpret_cast<const uint32_t*>(&q[u][3]);
         uint4 out;
         uint32_t* po = reinterpret_cast<uint32_t*>(&out);
+        // channel pairs on the packed FP32 pipe (v_pk_mul/v_pk_fma): half the VALU issue
+        const f32x2 vx0 = {lx0, lx0}, vx1 = {lx1, lx1}, vy0 = {ly0, ly0}, vy1 = {ly1, ly1};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          float r[2];
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            auto g = [&](uint32_t v) { return hh ? __uint_as_float(v & 0xffff0000u) : __uint_as_float(v << 16); };
-            const float t0 = lx0 * g(p00[k]) + lx1 * g(p01[k]);
-            const float t1 = lx0 * g(p10[k]) + lx1 * g(p11[k]);
-            r[hh] = ly0 * t0 + ly1 * t1;
-          }
-          po[k] = inside[u] ? pack2(r[0], r[1]) : 0u;
+          const f32x2 t0 = __builtin_elementwise_fma(vx1, unpack2(p01[k]), vx0 * unpack2(p00[k]));
+          const f32x2 t1 = __builtin_elementwise_fma(vx1, unpack2(p11[k]), vx0 * unpack2(p10[k]));
+          const f32x2 r = __builtin_elementwise_fma(vy1, t1, vy0 * t0);
+          po[k] = inside[u] ? pack2(r) : 0u;
         }
         *reinterpret_cast<uint4*>(s_halo + pix * 128 + ((c8 ^ (pix & 7)) << 4)) = out;
       }
