@@ -132,18 +132,18 @@ const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
     const uint32_t* pa = reinterpret_cast<const uint32_t*>(&addv);
     uint4 out;
     uint32_t* po = reinterpret_cast<uint32_t*>(&out);
+    // channel pairs on the packed FP32 pipe; one cvt_pk_bf16 per pair
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    auto g2 = [](uint32_t u) { return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; };
+    const f32x2 vx0 = {lx0, lx0}, vx1 = {lx1, lx1}, vy0 = {ly0, ly0}, vy1 = {ly1, ly1};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float r[2];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        auto g = [&](uint32_t u) { return hh ? __uint_as_float(u & 0xffff0000u) : __uint_as_float(u << 16); };
-        const float t0 = lx0 * g(p00[k]) + lx1 * g(p01[k]);
-        const float t1 = lx0 * g(p10[k]) + lx1 * g(p11[k]);
-        r[hh] = ly0 * t0 + ly1 * t1;
-        if (add) r[hh] += g(pa[k]);
-      }
-      po[k] = pack2(r[0], r[1]);
+      const f32x2 t0 = __builtin_elementwise_fma(vx1, g2(p01[k]), vx0 * g2(p00[k]));
+      const f32x2 t1 = __builtin_elementwise_fma(vx1, g2(p11[k]), vx0 * g2(p10[k]));
+      f32x2 r = __builtin_elementwise_fma(vy1, t1, vy0 * t0);
+      if (add) r += g2(pa[k]);
+      po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
     }
     *reinterpret_cast<uint4*>(y + i * 8) = out;
   }
