@@ -27,6 +27,7 @@ namespace pre {
 
 constexpr int PB = 32 - 8 - 2;     // PRECISION_BITS
 constexpr int kLdsBudget = 60 * 1024;
+constexpr int kStageBytes = 24 * 1024;  // input rows staged per chunk (one 8192-px row fits)
 
 struct Axis {
   int out, ksize;
@@ -95,6 +96,7 @@ static Axis identity(int n) {
 
 struct DevPlan {
   int in_h, in_w, out_h, out_w, kx, ky, R, tiles, patch, pld, lds_bytes;
+  int crows, stage_off;   // input rows staged per chunk, LDS offset of the staging area
   float mean[3], stdv[3];
   const int* hx_min; const int* hx_cnt; const int* hx_k;
   const int* vy_min; const int* vy_cnt; const int* vy_k;
@@ -126,26 +128,44 @@ __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __
   const int nrows = P.tile_n[tile];
   const uint8_t* img = bgr + (int64_t)b * P.in_h * P.in_w * 3;
   const int OW = P.out_w;
-  // horizontal pass: input rows [ylo, ylo + nrows) -> LDS
-  const int hwork = nrows * OW;
-  for (int i = threadIdx.x; i < hwork; i += blockDim.x) {
-    const int r = i / OW;
-    const int xx = i - r * OW;
-    const uint8_t* row = img + (int64_t)(ylo + r) * P.in_w * 3;
-    const int xmin = P.hx_min[xx], cnt = P.hx_cnt[xx];
-    const int* k = P.hx_k + xx * P.kx;
-    int s0 = 1 << (PB - 1), s1 = s0, s2 = s0;
-    for (int x = 0; x < cnt; ++x) {
-      const uint8_t* px = row + (xmin + x) * 3;
-      const int kv = k[x];
-      s0 += px[0] * kv;
-      s1 += px[1] * kv;
-      s2 += px[2] * kv;
+  const int row_bytes = P.in_w * 3;
+  uint8_t* stg = tmp + P.stage_off;
+  const bool vec = (row_bytes & 15) == 0;
+  // horizontal pass: input rows [ylo, ylo + nrows) -> LDS, P.crows input rows at a time
+  // staged through LDS with coalesced 16-B loads (the taps then read LDS, not 3 scattered
+  // global bytes per tap)
+  for (int c0 = 0; c0 < nrows; c0 += P.crows) {
+    const int cr = min(P.crows, nrows - c0);
+    const uint8_t* src = img + (int64_t)(ylo + c0) * row_bytes;
+    const int nbytes = cr * row_bytes;
+    __syncthreads();                       // the previous chunk's taps are read
+    if (vec) {
+      for (int i = threadIdx.x; i < nbytes / 16; i += blockDim.x)
+        reinterpret_cast<uint4*>(stg)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else {
+      for (int i = threadIdx.x; i < nbytes; i += blockDim.x) stg[i] = src[i];
     }
-    uint8_t* t = tmp + (r * OW + xx) * 3;
-    t[0] = clip8(s0);
-    t[1] = clip8(s1);
-    t[2] = clip8(s2);
+    __syncthreads();
+    const int hwork = cr * OW;
+    for (int i = threadIdx.x; i < hwork; i += blockDim.x) {
+      const int rl = i / OW;
+      const int xx = i - rl * OW;
+      const uint8_t* row = stg + rl * row_bytes;
+      const int xmin = P.hx_min[xx], cnt = P.hx_cnt[xx];
+      const int* k = P.hx_k + xx * P.kx;
+      int s0 = 1 << (PB - 1), s1 = s0, s2 = s0;
+      for (int x = 0; x < cnt; ++x) {
+        const uint8_t* px = row + (xmin + x) * 3;
+        const int kv = k[x];
+        s0 += px[0] * kv;
+        s1 += px[1] * kv;
+        s2 += px[2] * kv;
+      }
+      uint8_t* t = tmp + ((c0 + rl) * OW + xx) * 3;
+      t[0] = clip8(s0);
+      t[1] = clip8(s1);
+      t[2] = clip8(s2);
+    }
   }
   __syncthreads();
   // vertical pass + rescale/normalise + layout
@@ -240,7 +260,10 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
   P.in_h = in_h; P.in_w = in_w; P.out_h = out_h; P.out_w = out_w;
   P.kx = hx.ksize; P.ky = vy.ksize; P.R = R; P.tiles = tiles; P.patch = patch;
   P.pld = (3 * patch * patch + 63) / 64 * 64;   // patch-row pitch: the GEMM K axis, padded to 64
-  P.lds_bytes = (int)align_up((size_t)max_rows * row_bytes, 16);
+  P.stage_off = (int)align_up((size_t)max_rows * row_bytes, 16);
+  P.crows = std::max(1, kStageBytes / (in_w * 3));
+  I2PC_REQUIRE(in_w * 3 <= kStageBytes, "input width %d too large for the LDS row stage", in_w);
+  P.lds_bytes = P.stage_off + (int)align_up((size_t)P.crows * in_w * 3, 16);
   for (int c = 0; c < 3; ++c) { P.mean[c] = mean[c]; P.stdv[c] = stdv[c]; }
   const int* base = static_cast<const int*>(dev);
   P.hx_min = base + o0; P.hx_cnt = base + o1; P.hx_k = base + o2;
@@ -262,6 +285,14 @@ extern "C" int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* 
   I2PC_REQUIRE(plan && bgr && out && batch > 0, "bad arguments");
   I2PC_REQUIRE(layout == 0 || (layout == 1 && plan->p.patch > 0), "layout must be 0 (fp32 NCHW) or 1 (bf16 patch rows, plan with patch > 0)");
   const DevPlan& P = plan->p;
+  if (P.lds_bytes > 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_preprocess), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      attr = true;
+    }
+  }
   hipLaunchKernelGGL(k_preprocess, dim3(batch * P.tiles), dim3(256), P.lds_bytes, as_stream(stream), P, bgr, layout, out);
   return check_launch("preprocess");
 }
