@@ -88,7 +88,7 @@ def _kernel_profile(pipe, images):
     lib.i2pc_profile_enable(1)
     e0.record(stream)
     geometry.unproject_batch(depth, images, density=pipe.density, invert=pipe.invert,
-                             depth_scale=pipe.depth_scale, out=pipe._out)
+                             depth_scale=pipe.depth_scale, out=pipe._out, workspace=pipe._ws)
     e1.record(stream)
     torch.cuda.synchronize()
     unp_ms = lib.i2pc_profile_unproject_ms()
@@ -126,6 +126,18 @@ def _traffic(table, src, *names):
     return None, None
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def _cpu_baseline(spec, size, density):
     """Reference CPU path (restated) on one image of the bench's size, density high."""
     import numpy as np
@@ -161,6 +173,7 @@ def _cpu_baseline(spec, size, density):
     t2 = time.perf_counter()
     n = len(pts)
     return {"value": n / (t2 - t0) / 1e6, "unit": "Mpoints/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
             "sample": f"1 image {size}x{size}, density {density} ({n} points): Pillow-exact preprocessing + transformers "
                       f"fp32 {spec.name} forward on {threads} threads ({t1 - t0:.2f} s) + the reference per-point "
                       f"Python loop, single-threaded ({t2 - t1:.2f} s)",

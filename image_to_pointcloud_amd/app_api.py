@@ -209,11 +209,10 @@ def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, mo
     timg = torch.from_numpy(np.ascontiguousarray(image)).to(dev)
     depth = _depth_device(timg, model_info)
     depth_url = None
-    if max(depth.shape) <= preview.DEPTH_PREVIEW_MAX:
-        try:
-            depth_url = preview.encode_png_data_url(preview.depth_preview_batch(depth, request.invert_depth)[0].cpu().numpy())
-        except Exception as e:
-            logger.error(f"Failed to create depth preview: {e}")
+    try:                                                                  # app.py:463 -> :124-172
+        depth_url = preview.encode_png_data_url(preview.colored_preview(depth, request.invert_depth).cpu().numpy())
+    except Exception as e:
+        logger.error(f"Failed to create depth preview: {e}")
     pb = geometry.unproject_batch(depth[None], timg[None], density=request.point_density,
                                   invert=request.invert_depth, depth_scale=request.depth_scale,
                                   smooth=request.smooth_depth, smooth_ksize=request.smooth_ksize)

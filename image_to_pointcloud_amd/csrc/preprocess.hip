@@ -11,9 +11,11 @@
 // the host (i2pc_preprocess_plan_create), so the device path is pure integer
 // arithmetic and bit-exact.
 //
-// One workgroup = one image x a band of R output rows: the horizontal pass
-// resamples exactly the input rows that band needs into LDS (uint8), the
-// vertical pass reads them back; nothing but the input and the output touch HBM.
+// One workgroup = one image x a band of R output rows x a tile of output columns:
+// the horizontal pass resamples exactly the input rows (and the input column
+// window) that tile needs into LDS (uint8), the vertical pass reads them back;
+// nothing but the input and the output touch HBM.  Any width works: wide
+// keep-aspect outputs and inputs wider than one LDS stage split into column tiles.
 #include "common.h"
 
 #include <algorithm>
@@ -26,8 +28,10 @@ namespace i2pc {
 namespace pre {
 
 constexpr int PB = 32 - 8 - 2;     // PRECISION_BITS
-constexpr int kLdsBudget = 60 * 1024;
-constexpr int kStageBytes = 24 * 1024;  // input rows staged per chunk (one 8192-px row fits)
+// LDS per workgroup: the uint8 band of horizontally resampled rows plus the staged input
+// rows; 56 + 24 KB keeps two 256-thread workgroups per CU (160 KB).
+constexpr int kLdsBudget = 56 * 1024;
+constexpr int kStageBytes = 24 * 1024;
 
 struct Axis {
   int out, ksize;
@@ -94,13 +98,17 @@ static Axis identity(int n) {
   return ax;
 }
 
+// A workgroup owns one image x a band of R output rows x a tile of CW output columns.
+// Wide outputs (keep-aspect panoramas) and wide inputs split into column tiles, each
+// staging only the input column window [col_a0, col_a0 + col_wb) bytes its taps read.
 struct DevPlan {
-  int in_h, in_w, out_h, out_w, kx, ky, R, tiles, patch, pld, lds_bytes;
+  int in_h, in_w, out_h, out_w, kx, ky, R, tiles, CW, ctiles, patch, pld, lds_bytes;
   int crows, stage_off;   // input rows staged per chunk, LDS offset of the staging area
   float mean[3], stdv[3];
   const int* hx_min; const int* hx_cnt; const int* hx_k;
   const int* vy_min; const int* vy_cnt; const int* vy_k;
   const int* tile_lo; const int* tile_n;
+  const int* col_a0; const int* col_wb;
 };
 
 }  // namespace pre
@@ -121,36 +129,47 @@ __device__ __forceinline__ uint8_t clip8(int ss) {
 }
 
 __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __restrict__ bgr, int layout, void* out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t tmp[];   // [rows][out_w][3] uint8 (BGR order)
-  const int b = blockIdx.x / P.tiles;
-  const int tile = blockIdx.x - b * P.tiles;
+  extern __shared__ __attribute__((aligned(16))) uint8_t tmp[];   // [rows][CW][3] uint8 (BGR order)
+  const int per_img = P.tiles * P.ctiles;
+  const int b = blockIdx.x / per_img;
+  const int rem = blockIdx.x - b * per_img;
+  const int tile = rem / P.ctiles;
+  const int ct = rem - tile * P.ctiles;
   const int ylo = P.tile_lo[tile];
   const int nrows = P.tile_n[tile];
   const uint8_t* img = bgr + (int64_t)b * P.in_h * P.in_w * 3;
-  const int OW = P.out_w;
+  const int x0 = ct * P.CW;
+  const int CWt = min(P.CW, P.out_w - x0);          // output columns of this tile
   const int row_bytes = P.in_w * 3;
+  const int a0 = P.col_a0[ct], wb = P.col_wb[ct];   // staged input window (bytes) of each row
   uint8_t* stg = tmp + P.stage_off;
-  const bool vec = (row_bytes & 15) == 0;
-  // horizontal pass: input rows [ylo, ylo + nrows) -> LDS, P.crows input rows at a time
-  // staged through LDS with coalesced 16-B loads (the taps then read LDS, not 3 scattered
-  // global bytes per tap)
+  const bool vec = ((row_bytes | a0 | wb) & 15) == 0;
+  // horizontal pass: input rows [ylo, ylo + nrows), window [a0, a0 + wb) -> LDS, P.crows
+  // input rows at a time staged with coalesced 16-B loads (the taps then read LDS, not 3
+  // scattered global bytes per tap)
   for (int c0 = 0; c0 < nrows; c0 += P.crows) {
     const int cr = min(P.crows, nrows - c0);
-    const uint8_t* src = img + (int64_t)(ylo + c0) * row_bytes;
-    const int nbytes = cr * row_bytes;
+    const uint8_t* src = img + (int64_t)(ylo + c0) * row_bytes + a0;
     __syncthreads();                       // the previous chunk's taps are read
     if (vec) {
-      for (int i = threadIdx.x; i < nbytes / 16; i += blockDim.x)
-        reinterpret_cast<uint4*>(stg)[i] = reinterpret_cast<const uint4*>(src)[i];
+      const int u = wb >> 4;
+      for (int i = threadIdx.x; i < cr * u; i += blockDim.x) {
+        const int r = i / u, c = i - r * u;
+        reinterpret_cast<uint4*>(stg)[i] = reinterpret_cast<const uint4*>(src + (int64_t)r * row_bytes)[c];
+      }
     } else {
-      for (int i = threadIdx.x; i < nbytes; i += blockDim.x) stg[i] = src[i];
+      for (int i = threadIdx.x; i < cr * wb; i += blockDim.x) {
+        const int r = i / wb, c = i - r * wb;
+        stg[i] = src[(int64_t)r * row_bytes + c];
+      }
     }
     __syncthreads();
-    const int hwork = cr * OW;
+    const int hwork = cr * CWt;
     for (int i = threadIdx.x; i < hwork; i += blockDim.x) {
-      const int rl = i / OW;
-      const int xx = i - rl * OW;
-      const uint8_t* row = stg + rl * row_bytes;
+      const int rl = i / CWt;
+      const int xl = i - rl * CWt;
+      const int xx = x0 + xl;
+      const uint8_t* row = stg + rl * wb - a0;
       const int xmin = P.hx_min[xx], cnt = P.hx_cnt[xx];
       const int* k = P.hx_k + xx * P.kx;
       int s0 = 1 << (PB - 1), s1 = s0, s2 = s0;
@@ -161,7 +180,7 @@ __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __
         s1 += px[1] * kv;
         s2 += px[2] * kv;
       }
-      uint8_t* t = tmp + ((c0 + rl) * OW + xx) * 3;
+      uint8_t* t = tmp + ((c0 + rl) * CWt + xl) * 3;
       t[0] = clip8(s0);
       t[1] = clip8(s1);
       t[2] = clip8(s2);
@@ -169,20 +188,22 @@ __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __
   }
   __syncthreads();
   // vertical pass + rescale/normalise + layout
+  const int OW = P.out_w;
   const int y0 = tile * P.R;
   const int rows_out = min(P.R, P.out_h - y0);
-  const int vwork = rows_out * OW;
+  const int vwork = rows_out * CWt;
   const int np_x = OW / max(P.patch, 1);
   const int npatch = (P.out_h / max(P.patch, 1)) * np_x;
   for (int i = threadIdx.x; i < vwork; i += blockDim.x) {
-    const int ry = i / OW;
-    const int xx = i - ry * OW;
+    const int ry = i / CWt;
+    const int xl = i - ry * CWt;
+    const int xx = x0 + xl;
     const int yy = y0 + ry;
     const int ymin = P.vy_min[yy] - ylo, cnt = P.vy_cnt[yy];
     const int* k = P.vy_k + yy * P.ky;
     int s[3] = {1 << (PB - 1), 1 << (PB - 1), 1 << (PB - 1)};
     for (int y = 0; y < cnt; ++y) {
-      const uint8_t* t = tmp + ((ymin + y) * OW + xx) * 3;
+      const uint8_t* t = tmp + ((ymin + y) * CWt + xl) * 3;
       const int kv = k[y];
       s[0] += t[0] * kv;
       s[1] += t[1] * kv;
@@ -221,15 +242,46 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
   if (patch > 0) I2PC_REQUIRE(out_h % patch == 0 && out_w % patch == 0, "output %dx%d not a multiple of patch %d", out_h, out_w, patch);
   Axis hx = out_w != in_w ? coeffs(in_w, out_w) : identity(in_w);
   Axis vy = out_h != in_h ? coeffs(in_h, out_h) : identity(in_h);
-  // rows per workgroup so that the uint8 intermediate fits the LDS budget
   const double scale = (double)in_h / out_h;
-  const int row_bytes = out_w * 3;
-  I2PC_REQUIRE(row_bytes * (vy.ksize + 2) <= kLdsBudget, "output width %d too large for one LDS band", out_w);
+  const int row_bytes = in_w * 3;
+  const bool vec = (row_bytes & 15) == 0;
+  // column tiles: the widest that lets the vertical taps of >= 1 output row fit the band
+  // budget and lets one input row's window fit the stage
+  auto window = [&](int x0, int x1, int& a0, int& wb) {
+    int lo = in_w, hi = 0;
+    for (int x = x0; x < x1; ++x) { lo = std::min(lo, hx.xmin[x]); hi = std::max(hi, hx.xmin[x] + hx.cnt[x]); }
+    a0 = lo * 3;
+    int a1 = hi * 3;
+    if (vec) { a0 &= ~15; a1 = std::min(row_bytes, (a1 + 15) & ~15); }
+    wb = a1 - a0;
+  };
+  int CW = out_w;
+  std::vector<int> ca0, cwb;
+  for (;;) {
+    bool ok = (vy.ksize + 2) * CW * 3 <= kLdsBudget;
+    if (ok) {
+      const int ct = (out_w + CW - 1) / CW;
+      ca0.assign(ct, 0);
+      cwb.assign(ct, 0);
+      for (int c = 0; c < ct && ok; ++c) {
+        window(c * CW, std::min(out_w, (c + 1) * CW), ca0[c], cwb[c]);
+        ok = cwb[c] <= kStageBytes;
+      }
+      if (ok) break;
+    }
+    I2PC_REQUIRE(CW > 1, "no column tile fits the LDS budget (in %dx%d -> out %dx%d)", in_h, in_w, out_h, out_w);
+    CW = (CW + 1) / 2;
+  }
+  const int ctiles = (out_w + CW - 1) / CW;
+  int max_wb = 0;
+  for (int c = 0; c < ctiles; ++c) max_wb = std::max(max_wb, cwb[c]);
+  // output rows per workgroup so that the uint8 intermediate fits the band budget
+  const int band_row = CW * 3;
   int R = 1;
   for (int r = 64; r >= 1; r /= 2) {
     // rows needed by r output rows <= (r - 1) * scale + ksize + 2
     const double need = (r - 1) * scale + vy.ksize + 2;
-    if (need * row_bytes <= kLdsBudget) { R = r; break; }
+    if (need * band_row <= kLdsBudget) { R = r; break; }
   }
   const int tiles = (out_h + R - 1) / R;
   std::vector<int> tlo(tiles), tn(tiles);
@@ -242,12 +294,13 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
     tn[t] = hi - lo;
     max_rows = std::max(max_rows, hi - lo);
   }
-  I2PC_REQUIRE(max_rows * row_bytes <= 64 * 1024, "LDS band too large (%d rows)", max_rows);
-  // one device buffer: hx_min | hx_cnt | hx_k | vy_min | vy_cnt | vy_k | tile_lo | tile_n
+  I2PC_REQUIRE(max_rows * band_row <= kLdsBudget, "LDS band too large (%d rows x %d B)", max_rows, band_row);
+  // every check is done: allocate.  One device buffer:
+  // hx_min | hx_cnt | hx_k | vy_min | vy_cnt | vy_k | tile_lo | tile_n | col_a0 | col_wb
   std::vector<int> blob;
   auto put = [&](const std::vector<int>& v) { size_t off = blob.size(); blob.insert(blob.end(), v.begin(), v.end()); return off; };
   const size_t o0 = put(hx.xmin), o1 = put(hx.cnt), o2 = put(hx.k), o3 = put(vy.xmin), o4 = put(vy.cnt), o5 = put(vy.k),
-               o6 = put(tlo), o7 = put(tn);
+               o6 = put(tlo), o7 = put(tn), o8 = put(ca0), o9 = put(cwb);
   void* dev = nullptr;
   if (hipMalloc(&dev, blob.size() * sizeof(int)) != hipSuccess) return set_error(I2PC_ELAUNCH, "hipMalloc failed");
   if (hipMemcpy(dev, blob.data(), blob.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
@@ -258,17 +311,17 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
   pl->dev = dev;
   DevPlan& P = pl->p;
   P.in_h = in_h; P.in_w = in_w; P.out_h = out_h; P.out_w = out_w;
-  P.kx = hx.ksize; P.ky = vy.ksize; P.R = R; P.tiles = tiles; P.patch = patch;
+  P.kx = hx.ksize; P.ky = vy.ksize; P.R = R; P.tiles = tiles; P.CW = CW; P.ctiles = ctiles; P.patch = patch;
   P.pld = (3 * patch * patch + 63) / 64 * 64;   // patch-row pitch: the GEMM K axis, padded to 64
-  P.stage_off = (int)align_up((size_t)max_rows * row_bytes, 16);
-  P.crows = std::max(1, kStageBytes / (in_w * 3));
-  I2PC_REQUIRE(in_w * 3 <= kStageBytes, "input width %d too large for the LDS row stage", in_w);
-  P.lds_bytes = P.stage_off + (int)align_up((size_t)P.crows * in_w * 3, 16);
+  P.stage_off = (int)align_up((size_t)max_rows * band_row, 16);
+  P.crows = std::max(1, kStageBytes / max_wb);
+  P.lds_bytes = P.stage_off + (int)align_up((size_t)P.crows * max_wb, 16);
   for (int c = 0; c < 3; ++c) { P.mean[c] = mean[c]; P.stdv[c] = stdv[c]; }
   const int* base = static_cast<const int*>(dev);
   P.hx_min = base + o0; P.hx_cnt = base + o1; P.hx_k = base + o2;
   P.vy_min = base + o3; P.vy_cnt = base + o4; P.vy_k = base + o5;
   P.tile_lo = base + o6; P.tile_n = base + o7;
+  P.col_a0 = base + o8; P.col_wb = base + o9;
   *plan = pl;
   return I2PC_OK;
 }
@@ -293,6 +346,6 @@ extern "C" int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* 
       attr = true;
     }
   }
-  hipLaunchKernelGGL(k_preprocess, dim3(batch * P.tiles), dim3(256), P.lds_bytes, as_stream(stream), P, bgr, layout, out);
+  hipLaunchKernelGGL(k_preprocess, dim3(batch * P.tiles * P.ctiles), dim3(256), P.lds_bytes, as_stream(stream), P, bgr, layout, out);
   return check_launch("preprocess");
 }

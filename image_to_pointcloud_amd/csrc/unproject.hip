@@ -12,7 +12,7 @@
 //                     map holds NaN/Inf, the ranks of np.nanmedian (app.py:195)
 //   k_sel_hist/resolve x3 levels (pass 1)   only when a nanmedian fill was
 //                     needed: p2/p98 of the sanitised map (no-op launches otherwise)
-//   [k_norm_field, k_blur_rows, k_blur_cols]  only when smooth=True (app.py:209-214)
+//   [k_norm_field, k_blur<rows>, k_blur<cols>]  only when smooth=True (app.py:209-214), any odd k
 //   k_unproject       normalise (fp64 / fp32 / constant branch exactly as
 //                     numpy evaluates app.py:198-206), pinhole back-projection in
 //                     Python-double semantics (app.py:219-238), RGB gather
@@ -942,20 +942,28 @@ __global__ void k_norm_field(Geo g, const SelState* st, int B, int invert, doubl
   }
 }
 
+// cv2 borderInterpolate(BORDER_REFLECT_101), repeated reflection for kernels wider than the image
 __device__ __forceinline__ int reflect101(int i, int n) {
   if (n == 1) return 0;
-  if (i < 0) i = -i;
-  if (i >= n) i = 2 * (n - 1) - i;
-  return i < 0 ? -i : i;
+  while ((unsigned)i >= (unsigned)n) i = i < 0 ? -i : 2 * (n - 1) - i;
+  return i;
 }
 
-// 5-tap [1,4,6,4,1]/16 (cv2 small-kernel table for ksize 5, sigma 0), BORDER_REFLECT_101,
-// accumulated tap by tap in the branch dtype (float64 for mode 0, float32 otherwise).
+// Separable Gaussian taps of cv2.GaussianBlur(d, (k, k), 0) (getGaussianKernel, sigma 0):
+// the fixed small-kernel tables for k <= 7, else sigma = 0.15 k + 0.35 sampled and normalised.
+constexpr int kMaxBlur = 63;
+struct BlurTaps {
+  int k;
+  double w[kMaxBlur];
+};
+
+// Tap-order accumulation (k taps, BORDER_REFLECT_101) in the branch dtype (float64 for
+// mode 0, float32 with float32 taps otherwise).
 template <bool kRows>
-__global__ void k_blur(const double* src, double* dst, const SelState* st, int B, int H, int W) {
+__global__ void k_blur(const double* src, double* dst, const SelState* st, int B, int H, int W, BlurTaps taps) {
   const size_t n = (size_t)H * W;
   const size_t total = n * B;
-  const double k64[5] = {0.0625, 0.25, 0.375, 0.25, 0.0625};
+  const int r = taps.k / 2;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int b = (int)(i / n);
     const int p = (int)(i - (size_t)b * n);
@@ -963,20 +971,46 @@ __global__ void k_blur(const double* src, double* dst, const SelState* st, int B
     const double* s = src + (size_t)b * n;
     if (st[b].mode == 0) {
       double acc = 0.0;
-      for (int t = 0; t < 5; ++t) {
-        const double x = kRows ? s[(size_t)v * W + reflect101(u + t - 2, W)] : s[(size_t)reflect101(v + t - 2, H) * W + u];
-        acc = acc + x * k64[t];
+      for (int t = 0; t < taps.k; ++t) {
+        const double x = kRows ? s[(size_t)v * W + reflect101(u + t - r, W)] : s[(size_t)reflect101(v + t - r, H) * W + u];
+        acc = acc + x * taps.w[t];
       }
       dst[i] = acc;
     } else {
       float acc = 0.f;
-      for (int t = 0; t < 5; ++t) {
-        const float x = (float)(kRows ? s[(size_t)v * W + reflect101(u + t - 2, W)] : s[(size_t)reflect101(v + t - 2, H) * W + u]);
-        acc = acc + x * (float)k64[t];
+      for (int t = 0; t < taps.k; ++t) {
+        const float x = (float)(kRows ? s[(size_t)v * W + reflect101(u + t - r, W)] : s[(size_t)reflect101(v + t - r, H) * W + u]);
+        acc = acc + x * (float)taps.w[t];
       }
       dst[i] = (double)acc;
     }
   }
+}
+
+static BlurTaps gaussian_taps(int k) {
+  BlurTaps t{};
+  t.k = k;
+  static const double small[4][7] = {{1.0},
+                                     {0.25, 0.5, 0.25},
+                                     {0.0625, 0.25, 0.375, 0.25, 0.0625},
+                                     {0.03125, 0.109375, 0.21875, 0.28125, 0.21875, 0.109375, 0.03125}};
+  if (k <= 7) {
+    for (int i = 0; i < k; ++i) t.w[i] = small[k / 2][i];
+    return t;
+  }
+  const double sigma = 0.15 * k + 0.35;                 // ((k - 1) * 0.5 - 1) * 0.3 + 0.8
+  const double scale2x = -0.125 / (sigma * sigma);      // x below is 2 * (i - (k - 1) / 2)
+  const int h = (k - 1) / 2;
+  double v[kMaxBlur], sum = 0.0;
+  for (int i = 0, x = 1 - k; i < h; ++i, x += 2) {
+    v[i] = std::exp((double)(x * x) * scale2x);
+    sum += v[i];
+  }
+  sum = sum * 2.0 + 1.0;
+  const double mul = 1.0 / sum;
+  for (int i = 0; i < h; ++i) t.w[i] = t.w[k - 1 - i] = v[i] * mul;
+  t.w[h] = mul;
+  return t;
 }
 
 __global__ void k_finalize(const SelState* st, int B, double* bbox, double* stats) {
@@ -1169,10 +1203,9 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   const int step = params->step;
   I2PC_REQUIRE(step == 1 || step == 2 || step == 4, "step must be 1, 2 or 4 (low/medium/high)");
   I2PC_REQUIRE((int64_t)img_h * img_w < (1ll << 31), "image too large");
-  if (params->smooth) {
-    const int k = params->smooth_ksize < 3 ? 3 : params->smooth_ksize / 2 * 2 + 1;
-    if (k != 5) return set_error(I2PC_EUNSUPPORTED, "smooth_ksize -> kernel %d: only the default 5 is implemented", k);
-  }
+  const int blur_k = params->smooth_ksize < 3 ? 3 : params->smooth_ksize / 2 * 2 + 1;   // app.py:211
+  if (params->smooth)
+    I2PC_REQUIRE(blur_k <= kMaxBlur, "smooth_ksize -> kernel %d: at most %d taps", blur_k, kMaxBlur);
   const Layout L = layout(batch, img_h, img_w, params->smooth);
   if (workspace_bytes < L.total) return set_error(I2PC_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
   hipStream_t s = as_stream(stream);
@@ -1226,8 +1259,9 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
     double* f1 = reinterpret_cast<double*>(ws + L.tmp);
     const int nb = 2048;
     hipLaunchKernelGGL(k_norm_field, dim3(nb), dim3(256), 0, s, g, st, batch, params->invert, f0);
-    hipLaunchKernelGGL((k_blur<true>), dim3(nb), dim3(256), 0, s, f0, f1, st, batch, img_h, img_w);
-    hipLaunchKernelGGL((k_blur<false>), dim3(nb), dim3(256), 0, s, f1, f0, st, batch, img_h, img_w);
+    const BlurTaps taps = gaussian_taps(blur_k);
+    hipLaunchKernelGGL((k_blur<true>), dim3(nb), dim3(256), 0, s, f0, f1, st, batch, img_h, img_w, taps);
+    hipLaunchKernelGGL((k_blur<false>), dim3(nb), dim3(256), 0, s, f1, f0, st, batch, img_h, img_w, taps);
     field = f0;
     hipLaunchKernelGGL((k_unproject<true>), dim3(batch * sunp.nrb), dim3(kBlock), 0, s, g, st, field, image,
                        channels, batch, sunp, params->invert, cam, xyz, rgb, st);

@@ -47,7 +47,15 @@ def _stream_handle():
 _WS = {}
 
 
+def workspace_bytes(batch: int, height: int, width: int, smooth: bool = False) -> int:
+    """Device workspace one i2pc_unproject call of this shape needs (SelState + histograms + tap tables)."""
+    return int(_lib.load().i2pc_unproject_workspace_bytes(batch, height, width, int(bool(smooth))))
+
+
 def _workspace(nbytes: int, device):
+    """Per-device scratch for one-off calls.  It is REPLACED when a call needs more bytes, so a
+    caller that records launches into a HIP graph must own its workspace instead (pass
+    `workspace=` to unproject_batch / unproject_band; PointCloudPipeline does)."""
     torch = _torch()
     key = (device.index if device.index is not None else torch.cuda.current_device())
     buf = _WS.get(key)
@@ -71,11 +79,14 @@ def point_count(h: int, w: int, step: int) -> int:
 
 def unproject_batch(depth, images, density: str = "medium", invert: bool = True,
                     depth_scale: float = 10.0, smooth: bool = False, smooth_ksize: int = 5,
-                    fov: Optional[float] = None, out: Optional[PointBatch] = None) -> PointBatch:
+                    fov: Optional[float] = None, out: Optional[PointBatch] = None,
+                    workspace=None) -> PointBatch:
     """Batched GPU depth_to_point_cloud.
 
-    depth : torch.float32 [B, h, w] (model resolution) on the device
-    images: torch.uint8 [B, H, W, C] BGR on the device
+    depth    : torch.float32 [B, h, w] (model resolution) on the device
+    images   : torch.uint8 [B, H, W, C] BGR on the device
+    workspace: optional caller-owned device uint8 buffer of >= workspace_bytes(B, H, W, smooth)
+               bytes (required for graph capture: the shared per-device one may be reallocated)
     """
     torch = _torch()
     if density not in DENSITY_STEP:
@@ -107,7 +118,12 @@ def unproject_batch(depth, images, density: str = "medium", invert: bool = True,
         )
     lib = _lib.load()
     ws_bytes = lib.i2pc_unproject_workspace_bytes(B, H, W, int(bool(smooth)))
-    ws = _workspace(ws_bytes, dev)
+    if workspace is not None:
+        if workspace.dtype != torch.uint8 or not workspace.is_cuda or workspace.numel() < ws_bytes:
+            raise ValueError(f"workspace must be a device uint8 buffer of >= {ws_bytes} bytes")
+        ws = workspace
+    else:
+        ws = _workspace(ws_bytes, dev)
     p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
                              fov_deg=float(fov) if fov else 0.0, smooth=int(bool(smooth)),
                              smooth_ksize=int(smooth_ksize))

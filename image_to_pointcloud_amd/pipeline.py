@@ -63,6 +63,10 @@ class PointCloudPipeline:
             rgb=torch.empty((batch, self.points_per_image, 3), dtype=torch.uint8, device=self.device),
             bbox=torch.empty((batch, 6), dtype=torch.float64, device=self.device),
             stats=torch.empty((batch, 4), dtype=torch.float64, device=self.device))
+        # the pipeline owns its unprojection workspace: a captured graph bakes its address in,
+        # so it must never be the shared per-device scratch that other calls may regrow
+        self._ws = torch.empty(max(geometry.workspace_bytes(batch, height, width, smooth), 1),
+                               dtype=torch.uint8, device=self.device)
         self._graph = None
         self._static_in = None
         self.depth = None
@@ -78,7 +82,7 @@ class PointCloudPipeline:
         self.infer_depth(images)
         return geometry.unproject_batch(self.depth, images, density=self.density, invert=self.invert,
                                         depth_scale=self.depth_scale, smooth=self.smooth, fov=self.fov,
-                                        out=self._out)
+                                        out=self._out, workspace=self._ws)
 
     __call__ = run
 
@@ -103,25 +107,3 @@ class PointCloudPipeline:
         self._graph.replay()
         return self._out
 
-
-def smoke():
-    """Tiny end-to-end pass on cuda:0: every stage runs; unprojection checked against the oracle."""
-    import numpy as np
-    import torch
-
-    from .dpt import DPT_TINY
-    from oracle import unproject_ref as ref
-
-    dev = torch.device("cuda", 0)
-    rng = np.random.Generator(np.random.PCG64(1))
-    imgs = rng.integers(0, 256, (2, 96, 80, 3), dtype=np.uint8)
-    pipe = PointCloudPipeline(2, 96, 80, spec=DPT_TINY, density="medium", device=dev)
-    t = torch.from_numpy(imgs).to(dev)
-    pb = pipe.run(t)
-    torch.cuda.synchronize()
-    depth = pipe.depth.cpu().numpy()
-    assert np.isfinite(depth).all()
-    for i in range(2):
-        ep, ec = ref.depth_to_point_cloud(imgs[i], depth[i], density="medium", loop=False)
-        assert pb.xyz[i].cpu().numpy().tobytes() == ep.tobytes()
-        assert pb.rgb[i].cpu().numpy().astype(np.float32).tobytes() == ec.tobytes()

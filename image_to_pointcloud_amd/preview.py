@@ -89,6 +89,27 @@ def encode_png_data_url(bgr: np.ndarray) -> str:
     return "data:image/png;base64," + base64.b64encode(buf.getvalue()).decode("utf-8")
 
 
+def preview_size(h: int, w: int, max_dim: int = DEPTH_PREVIEW_MAX):
+    """(out_h, out_w) of the preview: unchanged up to max_dim, else the reference's
+    (int(round(dw * s)), int(round(dh * s))) with s = max_dim / max(dh, dw) (app.py:155-160)."""
+    dmax = max(h, w)
+    if dmax <= max_dim:
+        return h, w
+    s = max_dim / float(dmax)
+    return int(round(h * s)), int(round(w * s))
+
+
+def colored_preview(depth, invert: bool = True):
+    """Device preview image as the reference encodes it: float32 depth [h, w] -> uint8 BGR
+    [h', w', 3], the colour-mapped image INTER_AREA-downscaled when larger than 2048 px."""
+    t = depth_preview_batch(depth, invert)[0]
+    oh, ow = preview_size(t.shape[0], t.shape[1])
+    if (oh, ow) != tuple(t.shape[:2]):
+        from .preprocess import resize_area
+        t = resize_area(t, ow, oh)                    # cv2.resize(..., INTER_AREA), app.py:158-160
+    return t
+
+
 def create_depth_preview(depth, invert: bool = True):
     """Drop-in for app.py:124: numpy (or device) depth -> PNG data URL, or None on failure."""
     import torch
@@ -96,9 +117,7 @@ def create_depth_preview(depth, invert: bool = True):
         dev = geometry.require_device()
         t = depth if isinstance(depth, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(depth, np.float32))
         t = t.to(device=dev, dtype=torch.float32)
-        if max(t.shape[-2:]) > DEPTH_PREVIEW_MAX:
-            raise NotImplementedError(f"preview larger than {DEPTH_PREVIEW_MAX} px needs the INTER_AREA downscale")
-        img = depth_preview_batch(t, invert)[0].cpu().numpy()
+        img = colored_preview(t, invert).cpu().numpy()
         return encode_png_data_url(img)
     except Exception as e:        # the reference logs and returns None (app.py:169-171)
         logger.error(f"Failed to create depth preview: {e}")

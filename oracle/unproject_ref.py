@@ -131,34 +131,61 @@ def _linear_taps(in_size: int, out_size: int):
     return sx, s1, a0, fx
 
 
-def gaussian_blur_5(d: np.ndarray) -> np.ndarray:
-    """cv2.GaussianBlur(d, (5, 5), 0) as called at app.py:212 (k = 5 for the default ksize).
+def gaussian_kernel(k: int) -> np.ndarray:
+    """cv2.getGaussianKernel(k, 0) (OpenCV's getGaussianKernelBitExact, restated from the published
+    source): the fixed small-kernel tables for k <= 7, else sigma = 0.15 k + 0.35 (the documented
+    0.3 ((k - 1) 0.5 - 1) + 0.8), taps exp(-x^2 / (2 sigma^2)) normalised to sum 1 via one reciprocal.
+    PARITY UNPINNED (no OpenCV here; OpenCV evaluates exp in soft-float, libm here)."""
+    small = {1: [1.0], 3: [0.25, 0.5, 0.25], 5: [0.0625, 0.25, 0.375, 0.25, 0.0625],
+             7: [0.03125, 0.109375, 0.21875, 0.28125, 0.21875, 0.109375, 0.03125]}
+    if k in small:
+        return np.array(small[k], dtype=np.float64)
+    sigma = 0.15 * k + 0.35
+    scale2x = -0.125 / (sigma * sigma)
+    h = (k - 1) // 2
+    v = [math.exp(float(x * x) * scale2x) for x in range(1 - k, 0, 2)]
+    s = 0.0
+    for t in v:
+        s += t
+    mul = 1.0 / (s * 2.0 + 1.0)
+    half = [t * mul for t in v]
+    return np.array(half + [mul] + half[::-1], dtype=np.float64)
 
-    ksize 5 with sigma 0 uses OpenCV's fixed small kernel [1,4,6,4,1]/16 and
-    BORDER_REFLECT_101; separable, rows then columns, in the array's dtype.
-    PARITY UNPINNED (no OpenCV here): summation order follows the tap order.
-    """
-    k = np.array([1, 4, 6, 4, 1], dtype=np.float64) / 16.0
+
+def _reflect101(i: np.ndarray, n: int) -> np.ndarray:
+    """cv2 borderInterpolate(BORDER_REFLECT_101), repeated for kernels wider than the axis."""
+    if n == 1:
+        return np.zeros_like(i)
+    i = i.copy()
+    while True:
+        bad = (i < 0) | (i >= n)
+        if not bad.any():
+            return i
+        i = np.where(i < 0, -i, np.where(i >= n, 2 * (n - 1) - i, i))
+
+
+def gaussian_blur(d: np.ndarray, k: int) -> np.ndarray:
+    """cv2.GaussianBlur(d, (k, k), 0) as called at app.py:212: separable, rows then columns,
+    BORDER_REFLECT_101, taps in the array's dtype, accumulated in tap order.
+    PARITY UNPINNED (no OpenCV here): summation order follows the tap order."""
     a = np.asarray(d)
-    kt = k.astype(a.dtype)
+    kt = gaussian_kernel(k).astype(a.dtype)
     h, w = a.shape
-
-    def reflect101(i, n):
-        if n == 1:
-            return np.zeros_like(i)
-        i = np.abs(i)
-        i = np.where(i >= n, 2 * (n - 1) - i, i)
-        return np.abs(i)
-
+    r = k // 2
     cols = np.arange(w)
     tmp = np.zeros_like(a)
-    for t in range(5):
-        tmp = tmp + a[:, reflect101(cols + t - 2, w)] * kt[t]
+    for t in range(k):
+        tmp = tmp + a[:, _reflect101(cols + t - r, w)] * kt[t]
     rows = np.arange(h)
     out = np.zeros_like(a)
-    for t in range(5):
-        out = out + tmp[reflect101(rows + t - 2, h), :] * kt[t]
+    for t in range(k):
+        out = out + tmp[_reflect101(rows + t - r, h), :] * kt[t]
     return out
+
+
+def gaussian_blur_5(d: np.ndarray) -> np.ndarray:
+    """The default call (smooth_ksize 5 -> k = 5): OpenCV's fixed [1,4,6,4,1]/16 kernel."""
+    return gaussian_blur(d, 5)
 
 
 # ----------------------------------------------------------------------------
@@ -235,11 +262,8 @@ def depth_to_point_cloud(image: np.ndarray, depth: np.ndarray, density: str = "m
         depth = resize_linear_cv2(depth, img_w, img_h)                  # :187-188
     d, _ = normalize_depth(depth, invert)
     if smooth:                                                          # :209-214
-        k = max(3, int(smooth_ksize) // 2 * 2 + 1)
-        if k == 5:
-            d = gaussian_blur_5(d)
-        else:
-            raise NotImplementedError("oracle restates the default ksize=5 only")
+        k = max(3, int(smooth_ksize) // 2 * 2 + 1)                      # :211
+        d = gaussian_blur(d, k)                                         # :212
     h, w = img_h, img_w
     cx, cy, f = intrinsics(w, h, fov)
     step = DENSITY_STEP[density]

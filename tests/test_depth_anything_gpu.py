@@ -3,7 +3,8 @@ DepthAnythingForDepthEstimation on the same seeded weights and the same
 preprocessed input (keep-aspect, multiple-of-14 resize; app.py:78-82, 109-116).
 
 Tolerance, as for DPT (bf16 operands / fp32 accumulation vs an fp32 network,
-SURVEY §8c D9): relative L2 error of the depth <= 2e-2 and max |err| <= 6e-2 * max |ref|.
+SURVEY §8c D9): relative L2 error of the depth <= 1e-2 and max |err| <= 4e-2 * max |ref|;
+the achieved error is printed (pytest -rP) and logged to $I2PC_PARITY_LOG.
 Non-square inputs exercise the bicubic position-embedding interpolation and the
 non-square neck/fusion/head sizes.
 """
@@ -64,7 +65,9 @@ def test_depth_anything_matches_transformers_fp32(which, B, hw):
     rel = (err.norm() / exp.norm()).item()
     mx = (err.abs().max() / exp.abs().max()).item()
     assert exp.abs().max() > 0 and exp.std() > 1e-3 * exp.abs().max(), "degenerate reference depth"
-    assert rel <= 2e-2 and mx <= 6e-2, f"rel L2 {rel:.3e} max {mx:.3e}"
+    from test_dpt_gpu import _report
+    _report(f"depth-anything-v2 {tuple(depth.shape)}", rel_l2=rel, max_rel=mx)
+    assert rel <= 1e-2 and mx <= 4e-2, f"rel L2 {rel:.3e} max {mx:.3e}"
 
 
 @pytest.mark.parametrize("B,h,w,c,oh,ow,ac", [(2, 19, 19, 64, 37, 37, True), (1, 296, 296, 64, 518, 518, True),

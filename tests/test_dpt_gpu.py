@@ -1,10 +1,21 @@
 """Depth network parity: the bf16 HIP DPT against transformers' fp32 DPTForDepthEstimation.
 
 Same seeded weights (transformers key layout), same preprocessed input.
-Tolerance (bf16 operands / fp32 accumulation vs an fp32 network):
-relative L2 error of the predicted depth <= 2e-2 and max |err| <= 6e-2 * max |ref|.
-The preprocessing itself is checked bit-exact against DPTImageProcessorPil.
+Tolerance (bf16 operands / fp32 accumulation vs an fp32 network): relative L2
+error of the predicted depth <= 1e-2 (SURVEY §8c's bound) and max |err| <= 4e-2 * max |ref| for
+the tiny config; the 24-layer DPT-Large accumulates more bf16 rounding (measured r02: rel L2
+0.97e-2 at 384^2 and 1.12e-2 at 1024^2 input, max 1.6-1.8e-2), so its bound is rel L2 <= 1.5e-2.
+Every case prints the error it reached.  The preprocessing itself is checked bit-exact against
+DPTImageProcessorPil.
+
+End to end (`test_end_to_end_points_vs_fp32_reference`): transformers-fp32 depth -> oracle
+unprojection against HIP bf16 depth -> HIP unprojection.  The north star's 1e-4 relative XYZ
+bound holds for the unprojection given identical depth (bit-exact, test_unproject_gpu.py); with a
+bf16 network in front it cannot hold point for point (D9), so this test measures and prints the
+fraction of points within 1e-4 and the median / p99 relative XYZ error, and bounds the median.
 """
+import json
+import os
 import numpy as np
 import pytest
 
@@ -72,4 +83,80 @@ def test_dpt_forward_matches_transformers_fp32(which, B, hw):
     rel = (err.norm() / exp.norm()).item()
     mx = (err.abs().max() / exp.abs().max()).item()
     assert exp.abs().max() > 0 and exp.std() > 1e-3 * exp.abs().max(), "degenerate reference depth"
-    assert rel <= 2e-2 and mx <= 6e-2, f"rel L2 {rel:.3e} max {mx:.3e}"
+    _report(f"dpt-{which} B={B} {hw[0]}x{hw[1]}", rel_l2=rel, max_rel=mx)
+    bound = 1.5e-2 if which == "large" else 1e-2
+    assert rel <= bound and mx <= 4e-2, f"rel L2 {rel:.3e} max {mx:.3e}"
+
+
+def _report(case, **vals):
+    """Print the achieved error (pytest -rP shows it) and append it to $I2PC_PARITY_LOG if set."""
+    line = {"case": case, **{k: float(v) for k, v in vals.items()}}
+    print("parity", json.dumps(line))
+    path = os.environ.get("I2PC_PARITY_LOG")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps(line) + "\n")
+
+
+def test_end_to_end_points_vs_fp32_reference():
+    """bf16 HIP depth -> HIP points vs transformers-fp32 depth -> oracle points (DPT-Large, 2 x 384^2)."""
+    from image_to_pointcloud_amd import geometry
+    from image_to_pointcloud_amd.dpt import DPT_LARGE, DPTDepthModel, synthetic_state_dict
+    from image_to_pointcloud_amd.preprocess import Preprocessor, ProcessorSpec
+    from oracle import unproject_ref as oref
+    spec, B, hw = DPT_LARGE, 2, (384, 384)
+    dev = torch.device("cuda")
+    sd = synthetic_state_dict(spec, seed=0)
+    ours = DPTDepthModel(spec, sd, dev)
+    ref = _hf_model(spec, sd, dev)
+    imgs = _images(B, hw[0], hw[1], 11)
+    prep = Preprocessor(hw[0], hw[1], ProcessorSpec(size=(spec.image, spec.image)), patch=spec.patch)
+    timgs = torch.from_numpy(imgs).to(dev)
+    with torch.no_grad():
+        exp_depth = ref(pixel_values=prep(timgs, layout="nchw")).predicted_depth.float().cpu().numpy()
+    depth = ours(prep(timgs, layout="patches"), B)
+    pb = geometry.unproject_batch(depth, timgs, density="high")
+    torch.cuda.synchronize()
+    fracs, meds, p99s = [], [], []
+    for i in range(B):
+        ep, ec = oref.depth_to_point_cloud(imgs[i], exp_depth[i], density="high", loop=False)
+        got = pb.xyz[i].cpu().numpy().astype(np.float64)
+        assert np.array_equal(pb.rgb[i].cpu().numpy().astype(np.float32), ec)   # integer outputs: exact
+        scale = np.maximum(np.abs(ep).max(axis=1), 10.0 * 1e-5)                  # floor: depth_scale * 1e-5
+        rel = (np.abs(got - ep).max(axis=1) / scale)
+        fracs.append(float((rel <= 1e-4).mean()))
+        meds.append(float(np.median(rel)))
+        p99s.append(float(np.quantile(rel, 0.99)))
+    _report("e2e dpt-large 2x384^2 high: bf16 network + HIP unproject vs fp32 network + oracle",
+            frac_within_1e4=np.mean(fracs), median_rel=np.mean(meds), p99_rel=np.mean(p99s))
+    assert np.mean(meds) <= 5e-2, (fracs, meds, p99s)
+
+
+def test_captured_pipeline_survives_workspace_regrow():
+    """A captured pipeline owns its unprojection workspace: a later, larger one-off call that
+    regrows the shared per-device scratch must not change what replay() writes."""
+    from image_to_pointcloud_amd import geometry
+    from image_to_pointcloud_amd.dpt import DPT_TINY
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    from oracle import unproject_ref as oref
+    dev = torch.device("cuda")
+    imgs = _images(2, 96, 80, 3)
+    timgs = torch.from_numpy(imgs).to(dev)
+    pipe = PointCloudPipeline(2, 96, 80, spec=DPT_TINY, density="high", device=dev)
+    pipe.capture(timgs)
+    big_b, big = 64, 256
+    need = geometry.workspace_bytes(big_b, big, big)
+    held = geometry._WS.get(dev.index if dev.index is not None else torch.cuda.current_device())
+    assert held is None or held.numel() < need, "the one-off call below must force a regrow"
+    bd = torch.rand((big_b, 32, 32), device=dev)
+    bi = torch.randint(0, 256, (big_b, big, big, 3), dtype=torch.uint8, device=dev)
+    geometry.unproject_batch(bd, bi, density="high")          # regrows (and frees) the shared scratch
+    torch.cuda.synchronize()
+    torch.empty(need * 4, dtype=torch.uint8, device=dev).fill_(0xA5)   # recycle the freed block
+    out = pipe.replay()
+    torch.cuda.synchronize()
+    depth = pipe.depth.cpu().numpy()
+    for i in range(2):
+        ep, ec = oref.depth_to_point_cloud(imgs[i], depth[i], density="high", loop=False)
+        assert out.xyz[i].cpu().numpy().tobytes() == ep.tobytes()
+        assert out.rgb[i].cpu().numpy().astype(np.float32).tobytes() == ec.tobytes()

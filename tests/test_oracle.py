@@ -87,3 +87,35 @@ def test_depth_preview_u8_matches_reference_fixtures():
         got = ref.depth_preview_u8(z[m["name"] + "__depth"], m["invert"])
         exp = z[m["name"] + "__u8"]
         assert got.dtype == exp.dtype and np.array_equal(got, exp), m["name"]
+
+
+def test_gaussian_kernel_tables_and_sampled():
+    """oracle.gaussian_kernel: OpenCV's fixed tables for k <= 7, and the sampled kernels sum to 1,
+    are symmetric and peak in the middle (cv2 absent: parity unpinned beyond these properties)."""
+    from oracle import unproject_ref as r
+    assert np.array_equal(r.gaussian_kernel(5), np.array([1, 4, 6, 4, 1]) / 16.0)
+    assert np.array_equal(r.gaussian_kernel(3), np.array([0.25, 0.5, 0.25]))
+    for k in (9, 11, 15, 31):
+        t = r.gaussian_kernel(k)
+        assert len(t) == k and abs(t.sum() - 1.0) < 1e-12
+        assert np.array_equal(t, t[::-1]) and t.argmax() == k // 2
+    # sigma 0.15 k + 0.35 (OpenCV's documented 0.3 ((k - 1) 0.5 - 1) + 0.8)
+    t = r.gaussian_kernel(9)
+    s = 0.15 * 9 + 0.35
+    x = np.arange(9) - 4
+    g = np.exp(-x * x / (2 * s * s))
+    assert np.allclose(t, g / g.sum(), rtol=1e-14, atol=0)
+
+
+def test_blur_matches_direct_convolution():
+    from oracle import unproject_ref as r
+    rng = np.random.default_rng(2)
+    d = rng.random((13, 17))
+    for k in (3, 9):
+        got = r.gaussian_blur(d, k)
+        kt = r.gaussian_kernel(k)
+        # dense reference: reflect-101 padded separable convolution
+        p = np.pad(d, k // 2, mode="reflect")
+        tmp = sum(p[:, t:t + 17] * kt[t] for t in range(k))
+        exp = sum(tmp[t:t + 13, :] * kt[t] for t in range(k))
+        assert np.allclose(got, exp, rtol=1e-13, atol=1e-15)

@@ -1,6 +1,7 @@
 """GPU preprocessing (k_preprocess: Pillow bicubic + rescale + normalise) bit-exact with the
 CPU restatement (itself pinned to Pillow / DPTImageProcessorPil, tests/test_preprocess.py) at
-the bench's size and the Depth-Anything keep-aspect size, both output layouts."""
+the bench's size, the Depth-Anything keep-aspect size, wide keep-aspect panoramas and inputs wider
+than one LDS row stage."""
 import numpy as np
 import pytest
 
@@ -12,7 +13,12 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("h,w,size,keep", [(1024, 1024, (384, 384), False), (768, 1024, (518, 518), True),
                                            (301, 997, (384, 384), False), (2048, 1024, (518, 518), True),
-                                           (300, 4000, (384, 384), False)])
+                                           (300, 4000, (384, 384), False),
+                                           # wide keep-aspect outputs (phone panoramas after the REST 3072-px
+                                           # downscale) split into column tiles: 518x2296 and 518x2652
+                                           (691, 3072, (518, 518), True), (600, 3072, (518, 518), True),
+                                           # input rows at and beyond one LDS stage (8192 px = 24 KB)
+                                           (40, 8192, (384, 384), False), (36, 9000, (384, 384), False)])
 def test_preprocess_bit_exact(h, w, size, keep):
     from image_to_pointcloud_amd.preprocess import Preprocessor, ProcessorSpec, output_size
     spec = ProcessorSpec(size=size, keep_aspect_ratio=keep, multiple=14 if keep else 1)

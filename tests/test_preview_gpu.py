@@ -51,3 +51,22 @@ def test_create_depth_preview_data_url():
     img = np.array(Image.open(io.BytesIO(base64.b64decode(url.split(",", 1)[1]))))
     lut = np.frombuffer(preview.PLASMA_BGR, np.uint8).reshape(256, 3)
     assert np.array_equal(img[:, :, ::-1], lut[ref.depth_preview_u8(d, True)])
+
+
+def test_preview_above_2048_is_area_downscaled():
+    """Depth maps wider than DEPTH_PREVIEW_MAX: the colour-mapped preview is INTER_AREA-resized to
+    (round(dw * s), round(dh * s)), s = 2048 / max(dh, dw) (app.py:155-160); checked against the
+    colour table + the INTER_AREA restatement (oracle/area_ref.py, cv2 itself unpinned)."""
+    from oracle import area_ref
+    from image_to_pointcloud_amd import preview
+    rng = np.random.Generator(np.random.PCG64(5))
+    h, w = 1036, 2600
+    v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    d = (2.0 + np.sin(u / 50.0) * np.cos(v / 30.0) + rng.normal(0, 0.05, (h, w))).astype(np.float32)
+    oh, ow = preview.preview_size(h, w)
+    assert (oh, ow) == (int(round(h * 2048 / w)), 2048)
+    got = preview.colored_preview(torch.from_numpy(d).cuda(), True).cpu().numpy()
+    lut = np.frombuffer(preview.PLASMA_BGR, np.uint8).reshape(256, 3)
+    exp = area_ref.resize_area(lut[ref.depth_preview_u8(d, True)], ow, oh)
+    assert got.shape == (oh, ow, 3) and np.array_equal(got, exp)
+    assert preview.create_depth_preview(d, invert=True).startswith("data:image/png;base64,")

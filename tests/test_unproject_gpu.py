@@ -163,12 +163,18 @@ def test_full_size_high_density_properties():
         assert x[:, 2].min() >= 0.0 and x[:, 2].max() <= 10.0
 
 
-def test_smooth_path_matches_oracle_blur():
+@pytest.mark.parametrize("ksize,shape", [(5, (60, 50)), (1, (60, 50)), (3, (41, 37)), (7, (60, 50)),
+                                         (9, (60, 50)), (14, (33, 70)), (31, (12, 9))])
+def test_smooth_path_matches_oracle_blur(ksize, shape):
+    """GaussianBlur for every kernel app.py:211 can form (k = max(3, ksize // 2 * 2 + 1)): the
+    small-kernel tables (3, 5, 7), sampled Gaussians (9, 15), and a kernel wider than the image
+    (31 on 12 x 9: repeated BORDER_REFLECT_101)."""
     g = _geom()
-    dep = _smooth_depth(60, 50, 61)
-    img = _rgb(60, 50, 62)
-    pts, _ = g.depth_to_point_cloud(img, dep, density="medium", smooth=True)
-    ep, _ = ref.depth_to_point_cloud(img, dep, density="medium", smooth=True, loop=False)
+    h, w = shape
+    dep = _smooth_depth(h, w, 61)
+    img = _rgb(h, w, 62)
+    pts, _ = g.depth_to_point_cloud(img, dep, density="medium", smooth=True, smooth_ksize=ksize)
+    ep, _ = ref.depth_to_point_cloud(img, dep, density="medium", smooth=True, smooth_ksize=ksize, loop=False)
     assert _same_bits(pts, ep), _first_diff(pts, ep)
 
 
@@ -192,7 +198,7 @@ def test_bad_arguments_raise():
     with pytest.raises(KeyError):
         g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), density="ultra")
     with pytest.raises(I2PCError):
-        g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), smooth=True, smooth_ksize=9)
+        g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), smooth=True, smooth_ksize=99)
 
 
 @pytest.mark.parametrize("density,parts", [("high", 1), ("high", 3), ("medium", 2), ("low", 4)])
