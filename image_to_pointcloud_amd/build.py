@@ -33,9 +33,10 @@ SOURCES = [
     "sor.hip",
     "head.hip",
     "area.hip",
+    "fp8.hip",
     "writers.cpp",
 ]
-HEADERS = ["common.h", "../../include/i2pc.h"]
+HEADERS = ["common.h", "mx.h", "../../include/i2pc.h"]
 
 
 def hipcc() -> str:

@@ -20,6 +20,7 @@
 // (8-/16-byte epilogue stores). XCD-aware tile order: consecutive tiles (which
 // share an activation panel) go to one XCD.
 #include "common.h"
+#include "mx.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -77,6 +78,11 @@ struct Args {
   int tiles_m, tiles_n;
   int group_m;
   uint32_t a_bytes, w_bytes;   // buffer ranges of A and W (persistent engine)
+  // MX fp8 engine: E8M0 scale dwords [rows][K / 128] (byte b = 32-k block b of the 128-k step)
+  const uint32_t* As; int64_t ldas;    // A scales, dwords per row (conv: per pixel, Cin / 128)
+  const uint32_t* Ws; int64_t ldws;    // W scales
+  uint32_t* Cs; int64_t ldcs;          // fp8 output scales (EPI_Q8), dwords per row
+  uint32_t as_bytes, ws_bytes;
 };
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
@@ -514,11 +520,15 @@ static void launch(const Args& p, hipStream_t s) {
 // makes the counted waits exact.
 namespace pers {
 
-enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4 };
+using namespace ::i2pc::mx;
+
+enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4, EPI_Q8 = 5 };
 constexpr int OOB = 0x7FFFFFF0;   // buffer range; offsets >= OOB are dropped / read as 0
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 template <int I, int N, class F>
@@ -585,17 +595,18 @@ __device__ __forceinline__ int out_elem(const Args& p, int m, int n, int64_t ld,
 
 template <int EPI> struct EpiCount {
   static constexpr int loads = EPI == EPI_RESF32 || EPI == EPI_RESBF16 ? 4 : EPI == EPI_RES2 ? 8 : 0;
-  static constexpr int stores = EPI == EPI_RESF32 ? 4 : 2;
+  static constexpr int stores = EPI == EPI_RESF32 ? 4 : EPI == EPI_Q8 ? 5 : 2;
 };
 
 // Register-direct tile epilogue of the persistent engines for one wave: rows mw0 + i*16 + (lane & 15),
-// columns ncol + j*16 + (lane >> 4)*4 (the swapped 16x16x32 MFMA layout).  Issues exactly
-// RM * (loads + stores) vector-memory instructions (EpiCount), all unconditional.
-template <int RM, int EPI>
-__device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][4], int mw0, int ncol, const float* bias_lds,
-                                           rsrc_t c_rs, rsrc_t r_rs, rsrc_t r2_rs) {
-    constexpr int RN = 4;
+// columns ncol + j*16 + (lane >> 4)*4 (the swapped 16x16 MFMA layout), j < RN.  Issues exactly
+// RM * (loads + stores) vector-memory instructions (EpiCount), all unconditional -- plus, only in
+// the fp8 engine, plain row-bias / table loads the counted waits tolerate (extra, older-first).
+template <int RM, int RN, int EPI, bool F8>
+__device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], int mw0, int ncol, const float* bias_lds,
+                                           rsrc_t c_rs, rsrc_t r_rs, rsrc_t r2_rs, rsrc_t cs_rs) {
     constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
+    static_assert(RN == 2 || RN == 4, "RN");
     const int lane = threadIdx.x & 63;
     const int frow = lane & 15, fq = lane >> 4;
     float4 bias4[RN];
@@ -636,28 +647,51 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][4], i
       constexpr int slot = i & 1;
       if constexpr (NRL > 0) {
         if constexpr (i + 1 < RM) load_res(i + 1, slot ^ 1);
-        constexpr int after = (i + 1 < RM ? NRL : 0) + (i > 0 ? NS : 0);
-        if constexpr (EPI == EPI_RESF32)
-          asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rf[slot][0]), "+v"(rf[slot][1]), "+v"(rf[slot][2]), "+v"(rf[slot][3])
-                       : "i"(after) : "memory");
-        else if constexpr (EPI == EPI_RESBF16)
-          asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb[slot][2]), "+v"(rb[slot][3])
-                       : "i"(after) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(%c8)"
-                       : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb[slot][2]), "+v"(rb[slot][3]),
-                         "+v"(rb2[slot][0]), "+v"(rb2[slot][1]), "+v"(rb2[slot][2]), "+v"(rb2[slot][3])
-                       : "i"(after) : "memory");
+        constexpr int after = (i + 1 < RM ? NRL * RN / 4 : 0) + (i > 0 ? NS : 0);
+        if constexpr (EPI == EPI_RESF32) {
+          if constexpr (RN == 4)
+            asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rf[slot][0]), "+v"(rf[slot][1]), "+v"(rf[slot][2]), "+v"(rf[slot][3])
+                         : "i"(after) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%c2)" : "+v"(rf[slot][0]), "+v"(rf[slot][1]) : "i"(after) : "memory");
+        } else if constexpr (EPI == EPI_RESBF16) {
+          if constexpr (RN == 4)
+            asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb[slot][2]), "+v"(rb[slot][3])
+                         : "i"(after) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%c2)" : "+v"(rb[slot][0]), "+v"(rb[slot][1]) : "i"(after) : "memory");
+        } else {
+          if constexpr (RN == 4)
+            asm volatile("s_waitcnt vmcnt(%c8)"
+                         : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb[slot][2]), "+v"(rb[slot][3]),
+                           "+v"(rb2[slot][0]), "+v"(rb2[slot][1]), "+v"(rb2[slot][2]), "+v"(rb2[slot][3])
+                         : "i"(after) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb2[slot][0]), "+v"(rb2[slot][1])
+                         : "i"(after) : "memory");
+        }
       }
       const int m = mrow + i * 16;
       const bool ok = m < p.M;
+      const int mc = ok ? m : p.M - 1;
       float v[RN][4];
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        v[j][0] = act_f<ACT>(acc[i][j][0] + bias4[j].x);
-        v[j][1] = act_f<ACT>(acc[i][j][1] + bias4[j].y);
-        v[j][2] = act_f<ACT>(acc[i][j][2] + bias4[j].z);
-        v[j][3] = act_f<ACT>(acc[i][j][3] + bias4[j].w);
+        float t[4] = {acc[i][j][0] + bias4[j].x, acc[i][j][1] + bias4[j].y, acc[i][j][2] + bias4[j].z,
+                      acc[i][j][3] + bias4[j].w};
+        if constexpr (F8 && (EPI == EPI_PLAIN || EPI == EPI_Q8)) {   // per-image row bias (DPT readout CLS half), position table
+          const int n = ncol + j * 16 + fq * 4;
+          if (p.rbias) {
+            const float4 bb = *reinterpret_cast<const float4*>(p.rbias + (int64_t)(mc / p.rb_g) * p.N + n);
+            t[0] += bb.x; t[1] += bb.y; t[2] += bb.z; t[3] += bb.w;
+          }
+          if (p.tbl) {
+            const float4 bb = *reinterpret_cast<const float4*>(p.tbl + (int64_t)(mc % p.tbl_rows) * p.N + n);
+            t[0] += bb.x; t[1] += bb.y; t[2] += bb.z; t[3] += bb.w;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][e] = act_f<ACT>(t[e]);
         if constexpr (EPI == EPI_RESF32) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[j][e] += rf[slot][j][e];
@@ -671,7 +705,37 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][4], i
           v[j][2] += __uint_as_float(rb2[slot][j].y << 16); v[j][3] += __uint_as_float(rb2[slot][j].y & 0xffff0000u);
         }
       }
-      if constexpr (OUTF) {
+      if constexpr (EPI == EPI_Q8) {
+        // MX fp8 output: blocks of 32 columns = j pair (2q, 2q+1) x the 4 lanes fq of one row
+        constexpr int NB = RN / 2;
+        uint32_t sbytes = 0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          float am = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) am = fmaxf(am, fmaxf(fabsf(v[2 * q][e]), fabsf(v[2 * q + 1][e])));
+          am = fmaxf(am, __shfl_xor(am, 16));
+          am = fmaxf(am, __shfl_xor(am, 32));
+          const int ex = mx_exponent(am);
+          const float mul = exp2i(-ex);
+          sbytes |= (uint32_t)(ex + 127) << (8 * q);
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const int j = 2 * q + jj;
+            const uint32_t d = pack_e4m3(v[j][0] * mul, v[j][1] * mul, v[j][2] * mul, v[j][3] * mul);
+            const int off = ok ? remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldc + ncol + j * 16 + fq * 4 : OOB;
+            __builtin_amdgcn_raw_buffer_store_b32(d, c_rs, off, 0, 0);
+          }
+        }
+        if constexpr (RN == 2) {   // keep the per-i store count at 5 (RN / 2 = 1 data pair -> pad)
+          __builtin_amdgcn_raw_buffer_store_b32(0u, c_rs, OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(0u, c_rs, OOB, 0, 0);
+        }
+        // scale bytes of the row's blocks ncol/32 .. + NB - 1, by the fq == 0 lane
+        const int soff = (ok && fq == 0) ? remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldcs * 4 + ncol / 32 : OOB;
+        if constexpr (NB == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)sbytes, cs_rs, soff, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sbytes, cs_rs, soff, 0, 0);
+      } else if constexpr (OUTF) {
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
           const int off = ok ? out_elem(p, m, ncol + j * 16 + fq * 4, p.ldc, false) * 4 : OOB;
@@ -679,11 +743,15 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][4], i
                            __float_as_uint(v[j][3])};
           __builtin_amdgcn_raw_buffer_store_b128(d, c_rs, off, 0, 0);
         }
+        if constexpr (RN == 2) {   // 4 stores per i whatever RN (EpiCount)
+          __builtin_amdgcn_raw_buffer_store_b32(0u, c_rs, OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(0u, c_rs, OOB, 0, 0);
+        }
       } else {
         // pairs (2p, 2p+1): after the swap lane fq holds 8 consecutive columns at
         // 32p + (fq & 1) * 16 + (fq >> 1) * 8
 #pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
+        for (int pp = 0; pp < RN / 2; ++pp) {
           uint32_t x0 = pack_bf16(v[2 * pp][0], v[2 * pp][1]), x1 = pack_bf16(v[2 * pp][2], v[2 * pp][3]);
           uint32_t y0 = pack_bf16(v[2 * pp + 1][0], v[2 * pp + 1][1]), y1 = pack_bf16(v[2 * pp + 1][2], v[2 * pp + 1][3]);
           const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
@@ -693,6 +761,7 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][4], i
           const u32x4 d = {s0[0], s1[0], s0[1], s1[1]};
           __builtin_amdgcn_raw_buffer_store_b128(d, c_rs, off, 0, 0);
         }
+        if constexpr (RN == 2) __builtin_amdgcn_raw_buffer_store_b32(0u, c_rs, OOB, 0, 0);
       }
     });
     };
@@ -701,17 +770,30 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][4], i
     else epilogue(std::integral_constant<int, 0>{});
 }
 
-template <int BM, bool CONV, bool RELU_A, int EPI>
+// F8: MX fp8 operands (e4m3fn data + one E8M0 scale per 32 k) on
+// v_mfma_scale_f32_16x16x128_f8f6f4: a K-step is 128 fp8 = the same 128-B LDS row as 64 bf16,
+// so the tile geometry, swizzle and pipeline are the bf16 engine's; per stage each row also
+// brings one scale dword (its four 32-k blocks) into LDS (waves 0-3: A rows, 4-7: W rows).
+// The MFMA's k order inside a lane is (bytes 0-15: k = 16 g + j, bytes 16-31: k = 64 + 16 g + j)
+// for lane group g = lane >> 4, and the scale a lane passes covers k in [32 g, 32 g + 32)
+// (tools/probes/probe_mx.hip), so lane group g reads 16-B chunks g and 4 + g of the row and
+// passes byte g of the row's scale dword.
+template <int BM, bool CONV, bool RELU_A, int EPI, int BN = 256, bool F8 = false>
 __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
-  constexpr int BN = 256, TM = BM / 2, RM = TM / 16, RN = 4;
+  constexpr int TM = BM / 2, RM = TM / 16, RN = BN / 64;
   constexpr int ROWB = 128, RPI = 8;
+  constexpr int ESZ = F8 ? 1 : 2;          // operand bytes
+  constexpr int KSTEP = ROWB / ESZ;        // k per LDS stage
   constexpr int A_LOADS = BM / 64, W_LOADS = BN / 64;
-  constexpr int A_BYTES = BM * ROWB;
-  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int A_BYTES = BM * ROWB, W_BYTES = BN * ROWB;
+  constexpr int SC_BYTES = F8 ? (BM + BN) * 4 : 0;
+  constexpr int STAGE = A_BYTES + W_BYTES + SC_BYTES;
   constexpr int BIAS_OFF = 2 * STAGE;
-  constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
+  constexpr int NRL = EpiCount<EPI>::loads * RN / 4, NS = EpiCount<EPI>::stores;
   constexpr int E_ALL = RM * (NRL + NS);
   static_assert(BM == 256 || BM == 320, "BM");
+  static_assert(BN == 256 || BN == 128, "BN");
+  static_assert(!F8 || BM == 256, "fp8 engine: BM 256 (scale loads: one wave per 64 rows)");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
   const int lane = threadIdx.x & 63;
@@ -731,75 +813,111 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   const rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, p.a_bytes, 0x00020000);
   const rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W), 0, p.w_bytes, 0x00020000);
   const rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias), 0, p.bias ? p.N * 4 : 0, 0x00020000);
+  const rsrc_t as_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p.As), 0, F8 ? p.as_bytes : 0, 0x00020000);
+  const rsrc_t ws_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p.Ws), 0, F8 ? p.ws_bytes : 0, 0x00020000);
   const int chunk16 = (pchunk ^ lrow) << 4;           // swizzled 16-B chunk (row & 7 == lrow)
   const int a_row0 = wid * A_LOADS * RPI + lrow;      // + j * RPI
   const int w_row0 = wid * W_LOADS * RPI + lrow;
-  const int a_sstep = RPI * (int)p.lda * 2, w_sstep = RPI * (int)p.ldw * 2;
+  const int a_sstep = RPI * (int)p.lda * ESZ, w_sstep = RPI * (int)p.ldw * ESZ;
+  // fp8 scale rows: waves 0..BM/64-1 load A rows 64 w + lane, waves 4..4+BN/64-1 W rows
+  const bool sc_a = F8 && wid < BM / 64;
+  const bool sc_w = F8 && wid >= 4 && wid < 4 + BN / 64;
+  const int sc_row = (wid & 3) * 64 + lane;
 
   uint32_t a_off;                 // dense A: byte offset of this lane's slab-0 row
   uint32_t w_off;
+  uint32_t s_off;                 // dense A / W scale: byte offset of this lane's scale row
   int cpix[CONV ? A_LOADS : 1], cyx[CONV ? A_LOADS : 1];
+  int spix = 0, syx = 0;          // conv: pixel of this lane's scale row
   int nm0, nn0;   // coordinates of the tile the offsets point at
+  auto conv_row = [&](int m, int& pix, int& yx) {
+    const int hw = p.coh * p.cow;
+    const int b = m / hw;
+    const int rem = m - b * hw;
+    const int oy = rem / p.cow;
+    const int ox = rem - oy * p.cow;
+    // rows past M: an out-of-image y so every tap reads zero
+    pix = b * p.ch * p.cw;
+    yx = m < p.M ? ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff) : (int)(0x4000u << 16);
+  };
   auto setup = [&](int tile) {
     int tm, tn;
     grouped(p, tile, tm, tn);
     nm0 = tm * BM;
     nn0 = tn * BN;
     if constexpr (!CONV) {
-      a_off = (uint32_t)(nm0 + a_row0) * (uint32_t)(p.lda * 2) + chunk16;
+      a_off = (uint32_t)(nm0 + a_row0) * (uint32_t)(p.lda * ESZ) + chunk16;
     } else {
 #pragma unroll
-      for (int j = 0; j < A_LOADS; ++j) {
-        const int m = nm0 + a_row0 + j * RPI;
-        const int hw = p.coh * p.cow;
-        const int b = m / hw;
-        const int rem = m - b * hw;
-        const int oy = rem / p.cow;
-        const int ox = rem - oy * p.cow;
-        // rows past M: an out-of-image y so every tap reads zero
-        cpix[j] = b * p.ch * p.cw;
-        cyx[j] = m < p.M ? ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff) : (int)(0x4000u << 16);
+      for (int j = 0; j < A_LOADS; ++j) conv_row(nm0 + a_row0 + j * RPI, cpix[j], cyx[j]);
+    }
+    w_off = (uint32_t)(nn0 + w_row0) * (uint32_t)(p.ldw * ESZ) + chunk16;
+    if constexpr (F8) {
+      if (sc_a) {
+        if constexpr (CONV) conv_row(nm0 + sc_row, spix, syx);
+        else s_off = (uint32_t)(nm0 + sc_row) * (uint32_t)(p.ldas * 4);
+      } else {
+        s_off = (uint32_t)(nn0 + sc_row) * (uint32_t)(p.ldws * 4);
       }
     }
-    w_off = (uint32_t)(nn0 + w_row0) * (uint32_t)(p.ldw * 2) + chunk16;
   };
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  // one K-stage (A BM x 64, W 256 x 64) into LDS buffer `buf`; with `bias_par` >= 0
-  // wave 0 first stages the tile's 256 bias values into bias slot bias_par
+  // one K-stage (A BM x KSTEP, W BN x KSTEP [+ their scale dwords]) into LDS buffer `buf`;
+  // with `bias_par` >= 0 wave 0 first stages the tile's BN bias values into bias slot bias_par
   auto stage = [&](int buf, int k0, int bias_par) {
     uint8_t* sA = smem + buf * STAGE;
     uint8_t* sW = sA + A_BYTES;
-    if (bias_par >= 0 && wid == 0)
+    if (bias_par >= 0 && wid == 0 && lane < BN / 4)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, (lds_ptr_t)(smem + BIAS_OFF + bias_par * 1024), 16,
                                                 (nn0 + lane * 4) * 4, 0, 0, 0);
+    int kk = 0, ky = 0, kx = 0, ci0 = 0;
+    if constexpr (CONV) {
+      kk = k0 / p.cc;
+      ky = kk / p.ck;
+      kx = kk - ky * p.ck;
+      ci0 = k0 - kk * p.cc;
+    }
     if constexpr (!CONV) {
 #pragma unroll
       for (int j = 0; j < A_LOADS; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid * A_LOADS + j) * RPI * ROWB), 16,
-                                                  a_off + j * a_sstep, k0 * 2, 0, 0);   // row part in voffset: range-checked
+                                                  a_off + j * a_sstep, k0 * ESZ, 0, 0);   // row part in voffset: range-checked
     } else {
-      const int kk = k0 / p.cc;
-      const int ky = kk / p.ck;
-      const int kx = kk - ky * p.ck;
-      const int ci0 = k0 - kk * p.cc;
 #pragma unroll
       for (int j = 0; j < A_LOADS; ++j) {
         const int yi = (cyx[j] >> 16) + ky, xi = ((int)(short)(cyx[j] & 0xffff)) + kx;
         const bool ok = (unsigned)yi < (unsigned)p.ch && (unsigned)xi < (unsigned)p.cw;
-        const int off = ok ? ((cpix[j] + yi * p.cw + xi) * p.cc + ci0) * 2 + chunk16 : OOB;
+        const int off = ok ? ((cpix[j] + yi * p.cw + xi) * p.cc + ci0) * ESZ + chunk16 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid * A_LOADS + j) * RPI * ROWB), 16, off, 0, 0, 0);
       }
     }
 #pragma unroll
     for (int j = 0; j < W_LOADS; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rs, (lds_ptr_t)(sW + (wid * W_LOADS + j) * RPI * ROWB), 16, w_off,
-                                                j * w_sstep + k0 * 2, 0, 0);
+                                                j * w_sstep + k0 * ESZ, 0, 0);
+    if constexpr (F8) {
+      uint8_t* sS = sW + W_BYTES;                    // [BM] A scale dwords | [BN] W scale dwords
+      if (sc_a) {
+        if constexpr (!CONV) {
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(as_rs, (lds_ptr_t)(sS + (wid & 3) * 256), 4, s_off, (k0 / 128) * 4, 0, 0);
+        } else {
+          const int yi = (syx >> 16) + ky, xi = ((int)(short)(syx & 0xffff)) + kx;
+          const bool ok = (unsigned)yi < (unsigned)p.ch && (unsigned)xi < (unsigned)p.cw;
+          const int off = ok ? ((spix + yi * p.cw + xi) * (p.cc / 128) + ci0 / 128) * 4 : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(as_rs, (lds_ptr_t)(sS + (wid & 3) * 256), 4, off, 0, 0, 0);
+        }
+      } else if (sc_w) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ws_rs, (lds_ptr_t)(sS + BM * 4 + (wid & 3) * 256), 4, s_off,
+                                                  (k0 / 128) * 4, 0, 0);
+      }
+    }
   };
 
   const rsrc_t c_rs = make_rsrc(p.C);
   const rsrc_t r_rs = make_rsrc(p.res);
   const rsrc_t r2_rs = make_rsrc(p.res2);
-  const int nk = p.K / BK;
+  const rsrc_t cs_rs = make_rsrc(p.Cs);
+  const int nk = p.K / KSTEP;
 
   setup(t);
   int m0 = nm0, n0 = nn0;
@@ -843,29 +961,63 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
 #endif
       if (kt == 0) PSTAMP(tord, 1);
       if (kt + 1 < nk) {
-        stage((g + 1) & 1, (kt + 1) * BK, -1);
+        stage((g + 1) & 1, (kt + 1) * KSTEP, -1);
       } else if (has_next) {
         setup(t_next);
         stage((g + 1) & 1, 0, tpar ^ 1);
       }
       const uint8_t* sA = smem + (g & 1) * STAGE;
       const uint8_t* sW = sA + A_BYTES;
+      if constexpr (!F8) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 wf[RN];
-        const int lchunk = 4 * s + fq;
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 wf[RN];
+          const int lchunk = 4 * s + fq;
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            const int row = wn * (BN / 4) + j * 16 + frow;
+            wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * ROWB + ((lchunk ^ (row & 7)) << 4));
+          }
+#pragma unroll
+          for (int i = 0; i < RM; ++i) {
+            const int row = wm * TM + i * 16 + frow;
+            bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((lchunk ^ (row & 7)) << 4));
+            if (RELU_A) af = relu8(af);
+#pragma unroll
+            for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
+          }
+        }
+      } else {
+        const uint32_t* sS = reinterpret_cast<const uint32_t*>(sW + W_BYTES);
+        i32x8 wf[RN];
+        int wsc[RN];
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
-          const int row = wn * 64 + j * 16 + frow;
-          wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * ROWB + ((lchunk ^ (row & 7)) << 4));
+          const int row = wn * (BN / 4) + j * 16 + frow;
+          const uint8_t* r = sW + row * ROWB;
+          const i32x4 lo = *reinterpret_cast<const i32x4*>(r + ((fq ^ (row & 7)) << 4));
+          const i32x4 hi = *reinterpret_cast<const i32x4*>(r + (((4 + fq) ^ (row & 7)) << 4));
+          wf[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          wsc[j] = (int)(sS[BM + row] >> (8 * fq));
         }
 #pragma unroll
         for (int i = 0; i < RM; ++i) {
           const int row = wm * TM + i * 16 + frow;
-          bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((lchunk ^ (row & 7)) << 4));
-          if (RELU_A) af = relu8(af);
+          const uint8_t* r = sA + row * ROWB;
+          const i32x4 lo = *reinterpret_cast<const i32x4*>(r + ((fq ^ (row & 7)) << 4));
+          const i32x4 hi = *reinterpret_cast<const i32x4*>(r + (((4 + fq) ^ (row & 7)) << 4));
+          i32x8 af = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (RELU_A) {          // ReLU on e4m3 bytes: negative values (sign bit) -> +0
 #pragma unroll
-          for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t u = (uint32_t)af[e];
+              af[e] = (int)(u & ~(((u >> 7) & 0x01010101u) * 0xffu));
+            }
+          }
+          const int asc = (int)(sS[row] >> (8 * fq));
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[j], af, acc[i][j], 0, 0, 0, wsc[j], 0, asc);
         }
       }
       ++g;
@@ -876,8 +1028,9 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     if (threadIdx.x == 0 && tord < 8) g_stamps[(blockIdx.x * 8 + tord) * 8 + 4] = st_wait;
 #endif
     // ---- epilogue of tile (m0, n0): register-direct, counted
-    epilogue_p<RM, EPI>(p, acc, m0 + wm * TM, n0 + wn * 64,
-                        reinterpret_cast<const float*>(smem + BIAS_OFF + tpar * 1024) + wn * 64, c_rs, r_rs, r2_rs);
+    epilogue_p<RM, RN, EPI, F8>(p, acc, m0 + wm * TM, n0 + wn * (BN / 4),
+                                reinterpret_cast<const float*>(smem + BIAS_OFF + tpar * 1024) + wn * (BN / 4), c_rs, r_rs,
+                                r2_rs, cs_rs);
     PSTAMP(tord, 3);
     ++tord;
     if (!has_next) break;
@@ -909,22 +1062,27 @@ static int num_cus() {
   return n;
 }
 
-template <int BM, bool CONV, bool RELU_A, int EPI>
+template <int BM, bool CONV, bool RELU_A, int EPI, int BN = 256, bool F8 = false>
 static void launch_p(const Args& p, hipStream_t s) {
+  constexpr int ESZ = F8 ? 1 : 2;
   Args q = p;
   if (!CONV) {                        // dense rows: fold the row offset into the base
-    q.A = p.A + (int64_t)p.a_o * p.lda;
+    q.A = reinterpret_cast<const bf16_t*>(reinterpret_cast<const uint8_t*>(p.A) + (int64_t)p.a_o * p.lda * ESZ);
+    if (F8) q.As = p.As + (int64_t)p.a_o * p.ldas;
     q.a_o = 0;
-    q.a_bytes = (uint32_t)((int64_t)p.M * p.lda * 2);
+    q.a_bytes = (uint32_t)((int64_t)p.M * p.lda * ESZ);
+    q.as_bytes = (uint32_t)((int64_t)p.M * p.ldas * 4);
   } else {
-    q.a_bytes = (uint32_t)((int64_t)p.cb * p.ch * p.cw * p.cc * 2);
+    q.a_bytes = (uint32_t)((int64_t)p.cb * p.ch * p.cw * p.cc * ESZ);
+    q.as_bytes = (uint32_t)((int64_t)p.cb * p.ch * p.cw * (p.cc / 128) * 4);
   }
-  q.w_bytes = (uint32_t)((int64_t)p.N * p.ldw * 2);
+  q.w_bytes = (uint32_t)((int64_t)p.N * p.ldw * ESZ);
+  q.ws_bytes = (uint32_t)((int64_t)p.N * p.ldws * 4);
   q.tiles_m = (p.M + BM - 1) / BM;
-  q.tiles_n = p.N / 256;
+  q.tiles_n = p.N / BN;
   q.group_m = group_m_for(q.tiles_m);
-  const int smem = 2 * (BM + 256) * 128 + 2048;
-  auto kern = pers::k_gemm_p<BM, CONV, RELU_A, EPI>;
+  const int smem = 2 * ((BM + BN) * 128 + (F8 ? (BM + BN) * 4 : 0)) + 2048;
+  auto kern = pers::k_gemm_p<BM, CONV, RELU_A, EPI, BN, F8>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
@@ -1075,6 +1233,73 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu) {
   return buf;
 }
 
+// ---------------------------------------------------------------------------
+// MX fp8 GEMM (i2pc_gemm_fp8): always the persistent engine, BM 256, BN 256 (N % 256 == 0)
+// or 128 (N % 128 == 0).  Epilogues: bf16 out (+ bf16 residual(s)), fp32 out + fp32
+// residual, MX fp8 out (EPI_Q8); conv A (implicit im2col, Cin % 128 == 0) optionally with
+// ReLU on load.
+struct Plan8 { int bn, epi; };
+
+static int plan8(const Args& p, bool conv, bool relu, bool q8, Plan8& pl) {
+  pl.bn = p.N % 256 == 0 ? 256 : p.N % 128 == 0 ? 128 : 0;
+  if (!pl.bn) return set_error(I2PC_EUNSUPPORTED, "gemm_fp8: N=%d must be a multiple of 128", p.N);
+  if (p.ct_s > 0) return set_error(I2PC_EUNSUPPORTED, "gemm_fp8: no ConvTranspose store");
+  int epi = -1;
+  if ((p.rbias || p.tbl) && (p.res || p.res2 || p.c_f32))
+    return set_error(I2PC_EUNSUPPORTED, "gemm_fp8: row bias / table only with a bf16 or fp8 output and no residual");
+  if (q8) epi = (!p.res && !p.res2) ? pers::EPI_Q8 : -1;
+  else if (!p.res && !p.res2 && !p.c_f32) epi = pers::EPI_PLAIN;
+  else if (p.res && p.res_f32 && p.c_f32 && !p.res2) epi = pers::EPI_RESF32;
+  else if (p.res && !p.res_f32 && !p.c_f32 && !p.res2) epi = pers::EPI_RESBF16;
+  else if (p.res && !p.res_f32 && !p.c_f32 && p.res2) epi = pers::EPI_RES2;
+  // instantiated combinations
+  const bool ok = conv ? (pl.bn == 256 ? (epi == pers::EPI_PLAIN && !relu) || epi == pers::EPI_Q8 ||
+                                             ((epi == pers::EPI_RESBF16 || epi == pers::EPI_RES2) && !relu)
+                                       : epi == pers::EPI_PLAIN && !relu)
+                       : !relu && pl.bn == 256 && (epi == pers::EPI_PLAIN || epi == pers::EPI_RESF32 || epi == pers::EPI_Q8);
+  if (!ok) return set_error(I2PC_EUNSUPPORTED, "gemm_fp8: epilogue %d (conv %d relu %d bn %d) not instantiated", epi, conv, relu, pl.bn);
+  if (!conv && p.a_g != 0) return set_error(I2PC_EUNSUPPORTED, "gemm_fp8: no A row groups");
+  const int64_t esz = q8 ? 1 : p.c_f32 ? 4 : 2;
+  const int64_t abytes = conv ? (int64_t)p.cb * p.ch * p.cw * p.cc : (int64_t)(p.M + 256) * p.lda;
+  const int64_t cbytes = (max_row(p) * p.ldc + p.N) * esz;
+  int64_t rbytes = 0;
+  if (p.res) rbytes = std::max(rbytes, (max_row(p) * p.ldr + p.N) * (p.res_f32 ? 4 : 2));
+  if (p.res2) rbytes = std::max(rbytes, (max_row(p) * p.ldr2 + p.N) * 2);
+  if (abytes >= pers::OOB || (int64_t)p.N * p.ldw >= pers::OOB || cbytes >= pers::OOB || rbytes >= pers::OOB)
+    return set_error(I2PC_EUNSUPPORTED, "gemm_fp8: operand beyond the 31-bit buffer range");
+  pl.epi = epi;
+  return I2PC_OK;
+}
+
+static int run8(const Plan8& pl, const Args& p, bool conv, bool relu, hipStream_t s) {
+  using namespace pers;
+  if (!conv) {
+    if (pl.epi == EPI_PLAIN) launch_p<256, false, false, EPI_PLAIN, 256, true>(p, s);
+    else if (pl.epi == EPI_RESF32) launch_p<256, false, false, EPI_RESF32, 256, true>(p, s);
+    else launch_p<256, false, false, EPI_Q8, 256, true>(p, s);
+  } else if (pl.bn == 128) {
+    launch_p<256, true, false, EPI_PLAIN, 128, true>(p, s);
+  } else if (pl.epi == EPI_Q8) {
+    if (relu) launch_p<256, true, true, EPI_Q8, 256, true>(p, s);
+    else launch_p<256, true, false, EPI_Q8, 256, true>(p, s);
+  } else if (pl.epi == EPI_PLAIN) {
+    launch_p<256, true, false, EPI_PLAIN, 256, true>(p, s);
+  } else if (pl.epi == EPI_RESBF16) {
+    launch_p<256, true, false, EPI_RESBF16, 256, true>(p, s);
+  } else {
+    launch_p<256, true, false, EPI_RES2, 256, true>(p, s);
+  }
+  return check_launch("gemm_fp8");
+}
+
+static const char* plan8_name(const Plan8& pl, bool conv, bool relu) {
+  static thread_local char buf[96];
+  static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8"};
+  snprintf(buf, sizeof buf, "k_gemm_f8<%d, %s, %s, %s>", pl.bn, conv ? "true" : "false", relu ? "true" : "false",
+           epis[pl.epi]);
+  return buf;
+}
+
 }  // namespace gemm
 }  // namespace i2pc
 
@@ -1126,6 +1351,49 @@ extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) {
   const gemm::Plan pl = gemm::plan_for(p, conv, relu);
   if (conv) return relu ? gemm::run_plan<true, true>(pl, p, s) : gemm::run_plan<true, false>(pl, p, s);
   return relu ? gemm::run_plan<false, true>(pl, p, s) : gemm::run_plan<false, false>(pl, p, s);
+}
+
+static int make_args8(const i2pc_gemm_fp8_desc* d8, gemm::Args& p) {
+  I2PC_REQUIRE(d8 != nullptr, "desc is NULL");
+  const i2pc_gemm_desc* d = &d8->g;
+  I2PC_REQUIRE(d->a && d->w && d->c && d8->a_scale && d8->w_scale, "NULL operand");
+  I2PC_REQUIRE(d->m > 0 && d->n > 0 && d->k > 0, "empty gemm");
+  I2PC_REQUIRE(d->k % 128 == 0, "gemm_fp8: K=%d must be a multiple of 128", d->k);
+  I2PC_REQUIRE(!d8->c_fp8 || (d8->c_scale && d->ldc % 16 == 0 && d->n % 32 == 0), "gemm_fp8: fp8 output needs c_scale, ldc %% 16, n %% 32");
+  I2PC_REQUIRE(d->lda % 16 == 0 && d->ldw % 16 == 0, "gemm_fp8: lda/ldw must be multiples of 16 bytes");
+  if (d->conv) I2PC_REQUIRE(d->conv_c % 128 == 0, "gemm_fp8 conv: Cin=%d must be a multiple of 128", d->conv_c);
+  gemm::Args q;
+  i2pc_gemm_desc dd = *d;
+  if (d->conv) dd.conv_c = d->conv_c;   // (make_args checks Cin % 64, implied)
+  const int rc = make_args(&dd, q);
+  if (rc != I2PC_OK) return rc;
+  p = q;
+  p.As = static_cast<const uint32_t*>(d8->a_scale); p.ldas = d8->lda_scale;
+  p.Ws = static_cast<const uint32_t*>(d8->w_scale); p.ldws = d8->ldw_scale;
+  p.Cs = static_cast<uint32_t*>(d8->c_scale); p.ldcs = d8->ldc_scale;
+  I2PC_REQUIRE(d->conv || p.ldas >= d->k / 128, "gemm_fp8: lda_scale < K/128");
+  I2PC_REQUIRE(p.ldws >= d->k / 128, "gemm_fp8: ldw_scale < K/128");
+  return I2PC_OK;
+}
+
+extern "C" int i2pc_gemm_fp8(const i2pc_gemm_fp8_desc* d8, void* stream) {
+  clear_error();
+  gemm::Args p;
+  int rc = make_args8(d8, p);
+  if (rc != I2PC_OK) return rc;
+  const i2pc_gemm_desc* d = &d8->g;
+  gemm::Plan8 pl;
+  rc = gemm::plan8(p, d->conv != 0, d->conv_relu_in != 0, d8->c_fp8 != 0, pl);
+  if (rc != I2PC_OK) return rc;
+  return gemm::run8(pl, p, d->conv != 0, d->conv_relu_in != 0, as_stream(stream));
+}
+
+extern "C" const char* i2pc_gemm_fp8_kernel_name(const i2pc_gemm_fp8_desc* d8) {
+  gemm::Args p;
+  if (make_args8(d8, p) != I2PC_OK) return "invalid";
+  gemm::Plan8 pl;
+  if (gemm::plan8(p, d8->g.conv != 0, d8->g.conv_relu_in != 0, d8->c_fp8 != 0, pl) != I2PC_OK) return "invalid";
+  return gemm::plan8_name(pl, d8->g.conv != 0, d8->g.conv_relu_in != 0);
 }
 
 extern "C" const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* d) {

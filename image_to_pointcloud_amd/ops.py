@@ -295,3 +295,198 @@ def head_out(x, w, bias: float, out=None):
     with _Timed("k_head_out", 2.0 * B * H * W * C, B * H * W * (2.0 * C + 4)):
         _lib.call("i2pc_head_out", _p(x), B * H * W, C, _p(w), float(bias), _p(out), _stream())
     return out
+
+
+# ------------------------------------------------------------------ MX fp8 (DPT-Hybrid fp8 path)
+class GemmFp8Desc(ctypes.Structure):
+    _fields_ = [("g", GemmDesc), ("a_scale", c_void_p), ("lda_scale", c_int64), ("w_scale", c_void_p),
+                ("ldw_scale", c_int64), ("c_scale", c_void_p), ("ldc_scale", c_int64), ("c_fp8", c_int32)]
+
+
+_lib.register("i2pc_gemm_fp8", ctypes.c_int, [ctypes.POINTER(GemmFp8Desc), c_void_p])
+_lib.register("i2pc_gemm_fp8_kernel_name", ctypes.c_char_p, [ctypes.POINTER(GemmFp8Desc)])
+_lib.register("i2pc_quant_fp8", ctypes.c_int, [c_void_p, ctypes.c_int, c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p,
+                                               c_int64, c_void_p])
+_lib.register("i2pc_layernorm_fp8", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float, ctypes.c_int,
+                                                   ctypes.c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p])
+
+
+class Fp8:
+    """An MX fp8 operand: `data` uint8 e4m3fn [..., K] (rows or NHWC pixels) and `scale` uint8
+    [..., K / 32] (E8M0 exponent + 127 of each 32-element block; viewed by the kernels as
+    uint32 [..., K / 128])."""
+
+    def __init__(self, data, scale):
+        self.data, self.scale = data, scale
+
+    @property
+    def shape(self):
+        return self.data.shape
+
+    def rows(self):
+        return self.data.numel() // self.data.shape[-1]
+
+    def view(self, *shape):
+        k = self.data.shape[-1]
+        return Fp8(self.data.view(*shape), self.scale.view(*shape[:-1], k // 32))
+
+    def dequantize(self):
+        """fp32 values (test helper)."""
+        torch = _torch()
+        v = self.data.view(torch.float8_e4m3fn).float()
+        e = (self.scale.to(torch.int32) - 127).repeat_interleave(32, dim=-1)
+        return v * exp2i(e)
+
+
+def empty_fp8(shape, device):
+    torch = _torch()
+    shape = tuple(shape)
+    return Fp8(torch.empty(shape, dtype=torch.uint8, device=device),
+               torch.empty(shape[:-1] + (shape[-1] // 32,), dtype=torch.uint8, device=device))
+
+
+def mx_exponent(amax):
+    """E8M0 exponent of blocks with max |v| = amax (torch, any device): the smallest e with
+    amax / 2^e <= 448 -- the same rule as csrc/mx.h."""
+    torch = _torch()
+    m, ex = torch.frexp(amax)                 # amax = m * 2^ex, m in [0.5, 1)
+    e = (ex - 1) - 8 + (m > 0.875).to(ex.dtype)
+    e = torch.where(amax == 0, torch.full_like(e, -127), e)
+    return e.clamp(-127, 127)
+
+
+def exp2i(e):
+    """Exact 2^e (float32) for an integer tensor e in [-127, 127], built from the exponent bits
+    (torch's pow / ldexp on the device are not exact)."""
+    torch = _torch()
+    e = e.to(torch.int32)
+    bits = ((e.clamp(min=-126) + 127) << 23).view(torch.float32)
+    return torch.where(e >= -126, bits, torch.full_like(bits, 2.0 ** -127))
+
+
+def round_e4m3(q):
+    """Round fp32 values with |q| <= 448 to the e4m3fn grid, nearest, ties to even (what
+    v_cvt_pk_fp8_f32 does; torch's own float8 cast does not break ties to even here)."""
+    torch = _torch()
+    a = q.abs()
+    _, ex = torch.frexp(a)                                  # a = m * 2^ex, m in [0.5, 1)
+    ulp_exp = torch.clamp(ex - 1, min=-6) - 3               # normal: 2^(E-3); subnormal: 2^-9
+    # exact powers of two (exp2i): torch's device pow / ldexp are off by an ulp and move ties
+    return torch.round(q * exp2i(-ulp_exp)) * exp2i(ulp_exp)            # round: half to even
+
+
+def quantize_mx(w):
+    """fp32 [..., K] -> Fp8 on w's device (weights: done once at load; K % 32 == 0).
+    Same block rule and round-to-nearest-even as the device producers."""
+    torch = _torch()
+    w = w.float()
+    K = w.shape[-1]
+    blocks = w.reshape(*w.shape[:-1], K // 32, 32)
+    e = mx_exponent(blocks.abs().amax(dim=-1))
+    q = round_e4m3((blocks * exp2i(-e).unsqueeze(-1)).clamp(-448.0, 448.0))
+    data = q.to(torch.float8_e4m3fn).view(torch.uint8).reshape(w.shape).contiguous()
+    return Fp8(data, (e + 127).to(torch.uint8).contiguous())
+
+
+def quant_fp8(x, relu=False, rows=None, a_map=(0, 0, 0), out=None):
+    """bf16 / fp32 device rows [*, K] -> Fp8 [rows, K] (row r reads input row a_map(r))."""
+    torch = _torch()
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    R = rows if rows is not None else x2.shape[0]
+    if out is None:
+        out = empty_fp8(tuple(x.shape) if rows is None else (R, K), x.device)
+    with _Timed("k_quant_rows", 0.0, R * K * (x.element_size() + 1.0)):
+        _lib.call("i2pc_quant_fp8", _p(x2), int(x.dtype == torch.float32), x2.stride(0), R, K, int(bool(relu)),
+                  a_map[0], a_map[1], a_map[2], _p(out.data), out.data.shape[-1], _p(out.scale),
+                  out.scale.shape[-1] // 4, _stream())
+    return out
+
+
+def layernorm_fp8(x, gamma, beta, eps, out=None):
+    torch = _torch()
+    _check(x, torch.float32, "x")
+    rows, dim = x.shape
+    if out is None:
+        out = empty_fp8((rows, dim), x.device)
+    with _Timed("k_layernorm_fp8", 0.0, rows * dim * 5.0):
+        _lib.call("i2pc_layernorm_fp8", _p(x), x.stride(0), _p(gamma), _p(beta), float(eps), rows, dim,
+                  _p(out.data), out.data.shape[-1], _p(out.scale), out.scale.shape[-1] // 4, _stream())
+    return out
+
+
+def gemm_fp8(d: GemmFp8Desc) -> None:
+    if profile is None:
+        _lib.call("i2pc_gemm_fp8", ctypes.byref(d), _stream())
+        return
+    label = _lib.load().i2pc_gemm_fp8_kernel_name(ctypes.byref(d)).decode()
+    with _Timed(label, 2.0 * d.g.m * d.g.n * d.g.k):
+        _lib.call("i2pc_gemm_fp8", ctypes.byref(d), _stream())
+
+
+def _fp8_out(d, out, out_fp8, M, N, device, shape=None):
+    torch = _torch()
+    if out_fp8:
+        if out is None:
+            out = empty_fp8(shape or (M, N), device)
+        d.g.c, d.g.c_f32, d.g.ldc = _p(out.data), 0, out.data.shape[-1]
+        d.c_scale, d.ldc_scale, d.c_fp8 = _p(out.scale), out.scale.shape[-1] // 4, 1
+    else:
+        if out is None:
+            out = torch.empty(shape or (M, N), dtype=torch.bfloat16, device=device)
+        d.g.c, d.g.c_f32, d.g.ldc = _p(out), int(out.dtype == torch.float32), out.shape[-1]
+    return out
+
+
+def linear_fp8(x: Fp8, w: Fp8, bias=None, act=None, res=None, out=None, out_fp8=False, row_bias=None,
+               row_bias_group=1, table=None, table_rows=1):
+    """out = act(x @ w.T + bias + row_bias + table) [+ res fp32] on MX fp8 operands.
+    x: Fp8 [M, K]; w: Fp8 [N, K]; out bf16 [M, N], fp32 (with an fp32 res), or Fp8 (out_fp8)."""
+    torch = _torch()
+    M, K = x.rows(), x.shape[-1]
+    N = w.shape[0]
+    d = GemmFp8Desc()
+    d.g.a, d.g.lda, d.g.m, d.g.n, d.g.k = _p(x.data), K, M, N, K
+    d.a_scale, d.lda_scale = _p(x.scale), K // 128
+    d.g.w, d.g.ldw = _p(w.data), w.shape[-1]
+    d.w_scale, d.ldw_scale = _p(w.scale), w.shape[-1] // 128
+    d.g.bias = _p(bias)
+    d.g.row_bias, d.g.row_bias_group = _p(row_bias), row_bias_group
+    d.g.table, d.g.table_rows = _p(table), table_rows
+    d.g.act = ACT[act]
+    if res is not None:
+        d.g.res, d.g.res_f32, d.g.ldr = _p(res), int(res.dtype == torch.float32), res.stride(0)
+    if out is None and res is not None and res.dtype == torch.float32:
+        out = res
+    out = _fp8_out(d, out, out_fp8, M, N, x.data.device)
+    gemm_fp8(d)
+    return out
+
+
+def conv2d_fp8(x: Fp8, w: Fp8, bias=None, k=3, stride=1, pad=1, relu_in=False, act=None, res=None, res2=None,
+               out=None, out_fp8=False):
+    """NHWC implicit-GEMM conv on MX fp8: x Fp8 [B, H, W, C] (C % 128 == 0), w Fp8 [Co, k*k*C]
+    packed (ky, kx, ci); out bf16 NHWC (+ bf16 residuals) or Fp8 NHWC (out_fp8)."""
+    B, H, W, C = x.shape
+    Co = w.shape[0]
+    OH = (H + 2 * pad - k) // stride + 1
+    OW = (W + 2 * pad - k) // stride + 1
+    d = GemmFp8Desc()
+    d.g.a, d.g.lda, d.g.m, d.g.n, d.g.k = _p(x.data), C, B * OH * OW, Co, k * k * C
+    d.a_scale, d.lda_scale = _p(x.scale), C // 128
+    if not (k == 1 and stride == 1 and pad == 0):
+        d.g.conv, d.g.conv_batch, d.g.conv_h, d.g.conv_w, d.g.conv_c = 1, B, H, W, C
+        d.g.conv_oh, d.g.conv_ow, d.g.conv_k, d.g.conv_stride, d.g.conv_pad = OH, OW, k, stride, pad
+    d.g.conv_relu_in = int(relu_in)
+    d.g.w, d.g.ldw = _p(w.data), w.shape[-1]
+    d.w_scale, d.ldw_scale = _p(w.scale), w.shape[-1] // 128
+    d.g.bias = _p(bias)
+    d.g.act = ACT[act]
+    if res is not None:
+        d.g.res, d.g.res_f32, d.g.ldr = _p(res), 0, Co
+    if res2 is not None:
+        d.g.res2, d.g.ldr2 = _p(res2), Co
+    out = _fp8_out(d, out, out_fp8, B * OH * OW, Co, x.data.device, shape=(B, OH, OW, Co))
+    gemm_fp8(d)
+    return out

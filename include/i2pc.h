@@ -191,6 +191,40 @@ typedef struct i2pc_gemm_desc {
 
 int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
 
+/* MX fp8 GEMM / implicit-GEMM convolution (the DPT-Hybrid fp8 path, BASELINE configs[4]):
+ * the same contract as i2pc_gemm with A and W in OCP e4m3fn (1 byte per element; lda, ldw
+ * and ldc in ELEMENTS = bytes) and one E8M0 scale per 32 consecutive k:
+ *   a_scale: uint32 [rows][lda_scale] -- dword kt of row m holds the scales of k-blocks
+ *            4 kt .. 4 kt + 3 (byte b = block 4 kt + b), i.e. the bytes [rows][K / 32];
+ *            for a conv, rows are input PIXELS (NHWC) and lda_scale = Cin / 128;
+ *   w_scale: uint32 [n][ldw_scale], same layout over W's k;
+ *   value(m, k) = e4m3(A[m][k]) * 2^(scale byte - 127).
+ * Runs on v_mfma_scale_f32_16x16x128_f8f6f4 (fp32 accumulation).  Output: bf16 / fp32 as
+ * i2pc_gemm, or (c_fp8 = 1) MX fp8 C [m][ldc] bytes + c_scale uint32 [m][ldc_scale] with
+ * each 32-column block scaled so that max |v| / 2^e <= 448 (no saturation), e4m3 round to
+ * nearest even.  Requires k % 128 == 0, n % 128 == 0 (256 for dense A / fp8 output),
+ * conv_c % 128 == 0; no ConvTranspose store, no A row groups. */
+typedef struct i2pc_gemm_fp8_desc {
+  i2pc_gemm_desc g;
+  const void* a_scale; int64_t lda_scale;
+  const void* w_scale; int64_t ldw_scale;
+  void* c_scale; int64_t ldc_scale;
+  int32_t c_fp8;
+} i2pc_gemm_fp8_desc;
+
+int i2pc_gemm_fp8(const i2pc_gemm_fp8_desc* desc, void* stream);
+const char* i2pc_gemm_fp8_kernel_name(const i2pc_gemm_fp8_desc* desc);
+
+/* MX fp8 producers (operand format of i2pc_gemm_fp8).  quant_fp8: y[r] = fp8 of x[src(r)]
+ * (x bf16 or fp32 [*][ldx], optional ReLU; src(r) = (r / g) * gs + r % g + o, g = 0: r + o --
+ * e.g. skip the CLS row of every image); layernorm_fp8: nn.LayerNorm of fp32 rows written as
+ * fp8 rows (dim % 256 == 0).  y: bytes [rows][ldy]; y_scale: uint32 [rows][ldy_scale]. */
+int i2pc_quant_fp8(const void* x, int x_f32, int64_t ldx, int rows, int k, int relu, int row_group,
+                   int row_group_stride, int row_offset, void* y, int64_t ldy, void* y_scale, int64_t ldy_scale,
+                   void* stream);
+int i2pc_layernorm_fp8(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps, int rows,
+                       int dim, void* y, int64_t ldy, void* y_scale, int64_t ldy_scale, void* stream);
+
 /* Name of the kernel instance i2pc_gemm would launch for `desc` (profiling labels;
  * no device work).  Returns "invalid" for a descriptor i2pc_gemm would reject. */
 const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* desc);

@@ -1,10 +1,13 @@
 // Probe of v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3) operand and scale lane maps on gfx950.
-// Hypothesis checked (what csrc/gemm_fp8.hip relies on):
-//   A: lane l holds A[row = l & 15][k = 32 * (l >> 4) + j], j = byte 0..31 of its 8 VGPRs
-//   B: lane l holds B[k = 32 * (l >> 4) + j][col = l & 15]
-//   D: lane l, reg r = D[row = 4 * (l >> 4) + r][col = l & 15]
-//   scale_a (opsel 0): byte 0 of lane l's VGPR = E8M0 scale of A row (l & 15), k-block (l >> 4);
-//   scale_b likewise for B column (l & 15), k-block (l >> 4).
+// What csrc/gemm.hip's fp8 engine relies on (measured r02, "MX LAYOUT OK"):
+//   byte j of lane l's 8 A VGPRs pairs with byte j of lane l' in the same 16-lane group
+//   g = l >> 4 (A row l & 15, B column l' & 15), and the MFMA's k index of that pair is
+//   kh(g, j) = j < 16 ? 16 g + j : 64 + 16 g + (j - 16);
+//   D: lane l, reg r = D[row = 4 * (l >> 4) + r][col = l & 15];
+//   scale_a (opsel 0): byte 0 of lane l's VGPR = E8M0 scale of A row (l & 15) over
+//   kh in [32 (l >> 4), 32 (l >> 4) + 32); scale_b likewise for B column (l & 15).
+// So a lane of group g loads 16-B chunks g and 4 + g of a 128-k row and passes the scale of
+// 32-k block g: memory k order = kh, scale block b = memory k [32 b, 32 b + 32).
 //   hipcc --offload-arch=gfx950 -O2 tools/probes/probe_mx.hip -o /tmp/probe_mx && /tmp/probe_mx
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -75,8 +78,9 @@ int main() {
         const float e1 = m == row ? (float)(1 + ((k & 31) % 16)) : 0.f;
         const float e2 = m == row ? (float)(1 + (k >> 5) * 2 + ((k & 31) >> 4)) : 0.f;
         float sc = 1.f;
-        if (row == 5 && (k >> 5) == 1) sc *= 2.f;        // A lane 21
-        if (n == 5 && (k >> 5) == 2) sc *= 4.f;          // B lane 37
+        const int g = L >> 4, kh = J < 16 ? 16 * g + J : 64 + 16 * g + (J - 16);
+        if (row == 5 && (kh >> 5) == 1) sc *= 2.f;       // A lane 21: row 5, block 1
+        if (n == 5 && (kh >> 5) == 2) sc *= 4.f;         // B lane 37: column 5, block 2
         const float e3 = e2 * sc;
         if (v1 != e1 || v2 != e2 || v3 != e3) {
           if (bad < 10) printf("mismatch A(l=%d,j=%d) D[%d][%d]: %g %g %g expected %g %g %g\n", L, J, m, n, v1, v2, v3, e1, e2, e3);
@@ -84,6 +88,22 @@ int main() {
         }
       }
   }
+  // observed scale factors per k: A lane 21 (x2) seen at row 5 / col != 5, B lane 37 (x4) at col 5 / row != 5
+  printf("A-scale k:");
+  for (int pos = 0; pos < 2048; ++pos) {
+    const int L = pos >> 5, J = pos & 31, row = L & 15, k = 32 * (L >> 4) + J;
+    if (row != 5) continue;
+    const float f = o3[pos * 256 + 5 * 16 + 0] / o2[pos * 256 + 5 * 16 + 0];
+    if (f != 1.f) printf(" %d(x%g)", k, f);
+  }
+  printf("\nB-scale k (row 0):");
+  for (int pos = 0; pos < 2048; ++pos) {
+    const int L = pos >> 5, J = pos & 31, row = L & 15, k = 32 * (L >> 4) + J;
+    if (row != 0) continue;
+    const float f = o3[pos * 256 + 0 * 16 + 5] / o2[pos * 256 + 0 * 16 + 5];
+    if (f != 1.f) printf(" %d(x%g)", k, f);
+  }
+  printf("\n");
   printf(bad ? "MX LAYOUT MISMATCH: %d\n" : "MX LAYOUT OK (%d mismatches)\n", bad);
   return bad != 0;
 }
