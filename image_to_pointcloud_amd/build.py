@@ -34,6 +34,7 @@ SOURCES = [
     "head.hip",
     "area.hip",
     "fp8.hip",
+    "bit.hip",
     "writers.cpp",
 ]
 HEADERS = ["common.h", "mx.h", "../../include/i2pc.h"]

@@ -163,19 +163,24 @@ def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=Fal
     return out
 
 
-def conv2d(x, w, bias=None, k=3, stride=1, pad=1, relu_in=False, act=None, res=None, res2=None, out=None):
-    """NHWC bf16 conv via implicit GEMM.  w: bf16 [Co, k*k*Ci] in (ky, kx, ci) order."""
+def conv2d(x, w, bias=None, k=3, stride=1, pad=1, relu_in=False, act=None, res=None, res2=None, out=None,
+           out_hw=None):
+    """NHWC bf16 conv via implicit GEMM.  w: bf16 [Co, k*k*Ci] in (ky, kx, ci) order.
+    pad = top/left padding; out_hw overrides the output size (TF "SAME" stride-2 convs pad
+    less on the top/left than on the bottom/right: the missing bottom/right taps read zero)."""
     torch = _torch()
     _check(x, torch.bfloat16, "x")
     B, H, W, C = x.shape
     Co = w.shape[0]
     OH = (H + 2 * pad - k) // stride + 1
     OW = (W + 2 * pad - k) // stride + 1
+    if out_hw is not None:
+        OH, OW = out_hw
     if out is None:
         out = torch.empty((B, OH, OW, Co), dtype=torch.bfloat16, device=x.device)
     d = GemmDesc()
     d.a, d.lda, d.m, d.n, d.k = _p(x), C, B * OH * OW, Co, k * k * C
-    if k == 1 and stride == 1 and pad == 0:
+    if k == 1 and stride == 1 and pad == 0 and (OH, OW) == (H, W):
         pass    # a 1x1 conv is a plain GEMM over pixels
     else:
         d.conv, d.conv_batch, d.conv_h, d.conv_w, d.conv_c = 1, B, H, W, C
@@ -489,4 +494,84 @@ def conv2d_fp8(x: Fp8, w: Fp8, bias=None, k=3, stride=1, pad=1, relu_in=False, a
         d.g.res2, d.g.ldr2 = _p(res2), Co
     out = _fp8_out(d, out, out_fp8, B * OH * OW, Co, x.data.device, shape=(B, OH, OW, Co))
     gemm_fp8(d)
+    return out
+
+
+# ------------------------------------------------------------------ BiT stem (DPT-Hybrid)
+_lib.register("i2pc_bit_stem_im2col", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     c_void_p, c_void_p])
+_lib.register("i2pc_groupnorm_stats", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     c_void_p, c_void_p])
+_lib.register("i2pc_groupnorm_apply", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                     c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.c_float, ctypes.c_int, c_void_p, c_void_p])
+_lib.register("i2pc_maxpool3s2", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p])
+
+
+def same_pad(size: int, k: int, s: int):
+    """DynamicPad2d (modeling_bit.py:171-196): (output size, top/left pad) of TF "SAME" padding."""
+    out = -(-size // s)
+    total = max((out - 1) * s + k - size, 0)
+    return out, total // 2
+
+
+def stem_im2col(pixels, ksize=7, stride=2, k_pitch=None, out=None):
+    """fp32 NCHW [B, 3, H, W] -> bf16 [B * OH * OW, k_pitch] rows of the stem conv (SAME pad)."""
+    torch = _torch()
+    _check(pixels, torch.float32, "pixels")
+    assert stride == 2
+    B, _, H, W = pixels.shape
+    OH, pt = same_pad(H, ksize, stride)
+    OW, pl = same_pad(W, ksize, stride)
+    kp = k_pitch or (ksize * ksize * 3 + 63) // 64 * 64
+    if out is None:
+        out = torch.empty((B * OH * OW, kp), dtype=torch.bfloat16, device=pixels.device)
+    with _Timed("k_stem_im2col", 0.0, pixels.numel() * 4.0 + out.numel() * 2.0):
+        _lib.call("i2pc_bit_stem_im2col", _p(pixels), B, H, W, OH, OW, pt, pl, ksize, kp, _p(out), _stream())
+    return out, (OH, OW)
+
+
+def group_norm(x, gamma, beta, groups=32, eps=1e-5, relu=False, shortcut=None, acc=None, out=None):
+    """act(GroupNorm(x) + shortcut) on NHWC bf16; shortcut = None | bf16 tensor | (tensor, gamma, beta)
+    (normalised with its own statistics).  Returns bf16 NHWC."""
+    torch = _torch()
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    hw = H * W
+
+    def stats(t):
+        a = torch.empty((B, groups, 2), dtype=torch.float64, device=t.device)
+        with _Timed("k_gn_stats", 0.0, t.numel() * 2.0):
+            _lib.call("i2pc_groupnorm_stats", _p(t), B, hw, C, groups, _p(a), _stream())
+        return a
+
+    a = acc if acc is not None else stats(x)
+    r = ra = rg = rb = None
+    if isinstance(shortcut, tuple):
+        r, rg, rb = shortcut
+        ra = stats(r)
+    elif shortcut is not None:
+        r = shortcut
+    if out is None:
+        out = torch.empty_like(x)
+    nbytes = x.numel() * 4.0 + (r.numel() * 2.0 if r is not None else 0.0)
+    with _Timed("k_gn_apply", 0.0, nbytes):
+        _lib.call("i2pc_groupnorm_apply", _p(x), _p(a), _p(gamma), _p(beta), _p(r), _p(ra), _p(rg), _p(rb), B, hw, C,
+                  groups, float(eps), int(bool(relu)), _p(out), _stream())
+    return out
+
+
+def maxpool3s2(x, out=None):
+    """BitMaxPool2d(3, 2, dynamic SAME padding with 0) on NHWC bf16."""
+    torch = _torch()
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    OH, pt = same_pad(H, 3, 2)
+    OW, pl = same_pad(W, 3, 2)
+    if out is None:
+        out = torch.empty((B, OH, OW, C), dtype=torch.bfloat16, device=x.device)
+    with _Timed("k_maxpool", 0.0, x.numel() * 2.0 + out.numel() * 2.0):
+        _lib.call("i2pc_maxpool3s2", _p(x), B, H, W, C, OH, OW, pt, pl, _p(out), _stream())
     return out

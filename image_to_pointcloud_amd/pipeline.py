@@ -22,10 +22,18 @@ from .dpt import DPT_LARGE, DPTSpec
 from .preprocess import DEPTH_ANYTHING_PROCESSOR, DPT_LARGE_PROCESSOR, Preprocessor, ProcessorSpec
 
 
-def model_for(spec, state_dict=None, device=None, seed: int = 0):
-    """The network of a spec's family (DPT or Depth-Anything); seeded synthetic weights when none are given."""
-    if getattr(spec, "family", "dpt") == "depth-anything":
+def model_for(spec, state_dict=None, device=None, seed: int = 0, dtype: str = "bf16"):
+    """The network of a spec's family (DPT, DPT-Hybrid or Depth-Anything); seeded synthetic
+    weights when none are given.  dtype "fp8" selects the MX fp8 engine (DPT-Hybrid only)."""
+    family = getattr(spec, "family", "dpt")
+    if dtype not in ("bf16", "fp8") or (dtype == "fp8" and family != "dpt-hybrid"):
+        raise ValueError(f"dtype {dtype!r} is not available for {family}")
+    if family == "depth-anything":
         from .depth_anything import DepthAnythingModel as Model, synthetic_state_dict
+    elif family == "dpt-hybrid":
+        from .dpt_hybrid import DPTHybridModel, synthetic_state_dict
+        sd = state_dict if state_dict is not None else synthetic_state_dict(spec, seed)
+        return DPTHybridModel(spec, sd, device, dtype=dtype)
     else:
         from .dpt import DPTDepthModel as Model, synthetic_state_dict
     return Model(spec, state_dict if state_dict is not None else synthetic_state_dict(spec, seed), device)
@@ -39,25 +47,32 @@ class PointCloudPipeline:
     def __init__(self, batch: int, height: int, width: int, spec: DPTSpec = DPT_LARGE,
                  state_dict: Optional[dict] = None, processor: Optional[ProcessorSpec] = None,
                  density: str = "high", invert: bool = True, depth_scale: float = 10.0,
-                 smooth: bool = False, fov: Optional[float] = None, device=None, seed: int = 0, model=None):
+                 smooth: bool = False, fov: Optional[float] = None, device=None, seed: int = 0, model=None,
+                 dtype: str = "bf16"):
         import torch
         self.device = torch.device(device) if device is not None else geometry.require_device()
         self.batch, self.height, self.width = batch, height, width
         self.spec = spec
         self.density, self.invert, self.depth_scale, self.smooth, self.fov = density, invert, depth_scale, smooth, fov
         if model is None:
-            model = model_for(spec, state_dict, self.device, seed)
+            model = model_for(spec, state_dict, self.device, seed, dtype)
         self.model = model
         processor = processor or default_processor(spec)
-        if getattr(spec, "family", "dpt") == "dpt":
+        if getattr(spec, "family", "dpt") in ("dpt", "dpt-hybrid"):
             processor = ProcessorSpec(size=(spec.image, spec.image), mean=processor.mean, std=processor.std,
                                       keep_aspect_ratio=processor.keep_aspect_ratio, multiple=processor.multiple)
         self.pre = Preprocessor(height, width, processor, patch=spec.patch)
         self.gh, self.gw = self.pre.out_h // spec.patch, self.pre.out_w // spec.patch
         step = geometry.DENSITY_STEP[density]
         self.points_per_image = geometry.point_count(height, width, step)
-        self._patches = torch.zeros((batch * self.gh * self.gw, self.pre.patch_pitch), dtype=torch.bfloat16,
-                                    device=self.device)
+        # network input: bf16 patch rows (ViT patch embedding) or fp32 NCHW pixels (BiT stem)
+        self.layout = getattr(model, "input_layout", "patches")
+        if self.layout == "patches":
+            self._patches = torch.zeros((batch * self.gh * self.gw, self.pre.patch_pitch), dtype=torch.bfloat16,
+                                        device=self.device)
+        else:
+            self._patches = torch.zeros((batch, 3, self.pre.out_h, self.pre.out_w), dtype=torch.float32,
+                                        device=self.device)
         self._out = geometry.PointBatch(
             xyz=torch.empty((batch, self.points_per_image, 3), dtype=torch.float32, device=self.device),
             rgb=torch.empty((batch, self.points_per_image, 3), dtype=torch.uint8, device=self.device),
@@ -73,7 +88,7 @@ class PointCloudPipeline:
 
     def infer_depth(self, images):
         """images: uint8 [B,H,W,3] BGR on the device -> model-resolution depth fp32 [B, h', w']."""
-        self.pre(images, layout="patches", out=self._patches)
+        self.pre(images, layout=self.layout, out=self._patches)
         self.depth = self.model(self._patches, self.batch, self.gh, self.gw)
         return self.depth
 

@@ -225,6 +225,25 @@ int i2pc_quant_fp8(const void* x, int x_f32, int64_t ldx, int rows, int k, int r
 int i2pc_layernorm_fp8(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps, int rows,
                        int dim, void* y, int64_t ldy, void* y_scale, int64_t ldy_scale, void* stream);
 
+/* BiT-ResNet stem of DPT-Hybrid (transformers modeling_bit.py; bf16 NHWC maps).
+ * bit_stem_im2col: fp32 NCHW pixel_values -> bf16 GEMM rows [b*out_h*out_w][k_pitch], k =
+ *   (ky*ksize + kx)*3 + c (zero past ksize^2*3), input pixel (oy*2 - pad_top + ky, ox*2 -
+ *   pad_left + kx), zero outside (DynamicPad2d "SAME", modeling_bit.py:148-196).
+ * groupnorm_stats: acc fp64 [batch][groups][2] = per-group sum, sum of squares (zeroed here).
+ * groupnorm_apply: y = relu?(gn(x) + shortcut); gn(x) = (x - mean) * rstd * gamma + beta with
+ *   biased variance (nn.functional.group_norm); acc NULL = x raw; shortcut r NULL = none,
+ *   r with r_acc NULL = raw bf16, else gn(r) with its own statistics.
+ * maxpool3s2: 3x3 stride-2 max pool, zero padding pad_top/pad_left and past the bottom/right
+ *   edge (BitMaxPool2d with DynamicPad2d, modeling_bit.py:199-223). */
+int i2pc_bit_stem_im2col(const float* pixels, int batch, int h, int w, int out_h, int out_w, int pad_top,
+                         int pad_left, int ksize, int k_pitch, void* out, void* stream);
+int i2pc_groupnorm_stats(const void* x, int batch, int hw, int c, int groups, double* acc, void* stream);
+int i2pc_groupnorm_apply(const void* x, const double* acc, const float* gamma, const float* beta, const void* r,
+                         const double* r_acc, const float* r_gamma, const float* r_beta, int batch, int hw, int c,
+                         int groups, float eps, int relu, void* y, void* stream);
+int i2pc_maxpool3s2(const void* x, int batch, int h, int w, int c, int out_h, int out_w, int pad_top, int pad_left,
+                    void* y, void* stream);
+
 /* Name of the kernel instance i2pc_gemm would launch for `desc` (profiling labels;
  * no device work).  Returns "invalid" for a descriptor i2pc_gemm would reject. */
 const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* desc);

@@ -35,3 +35,35 @@ def test_depth_anything_sizes():
     from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL
     assert DA_V2_SMALL.sizes(37, 37) == [(148, 148), (74, 74), (37, 37), (19, 19)]
     assert DA_V2_SMALL.sizes(37, 49) == [(148, 196), (74, 98), (37, 49), (19, 25)]
+
+
+@pytest.mark.parametrize("which", ["tiny", "full"])
+def test_dpt_hybrid_state_dict_layout(which):
+    """Every tensor of DPTForDepthEstimation(is_hybrid=True) (BiT-R50 stem + ViT-B/16), same names and shapes."""
+    from transformers import DPTConfig, DPTForDepthEstimation
+    from image_to_pointcloud_amd.dpt_hybrid import DPT_HYBRID, DPT_HYBRID_TINY, state_dict_keys
+    spec = DPT_HYBRID if which == "full" else DPT_HYBRID_TINY
+    m = DPTForDepthEstimation(DPTConfig(**spec.hf_config_kwargs()))
+    assert {k: tuple(v.shape) for k, v in m.state_dict().items()} == state_dict_keys(spec)
+
+
+def test_dpt_hybrid_flops_match_flop_counter():
+    """HybridSpec.flops_per_image (conv + linear part) against torch's FlopCounter on the
+    transformers model (attention is added analytically, as for DPT-Large)."""
+    import torch
+    from torch.utils.flop_counter import FlopCounterMode
+    from transformers import DPTConfig, DPTForDepthEstimation
+    from image_to_pointcloud_amd.dpt_hybrid import DPT_HYBRID_TINY as spec
+    m = DPTForDepthEstimation(DPTConfig(**spec.hf_config_kwargs())).eval()
+    x = torch.zeros(1, 3, spec.image, spec.image)
+    with torch.no_grad(), FlopCounterMode(display=False) as fc:
+        m(pixel_values=x)
+    T = spec.grid ** 2 + 1
+    attn = spec.layers * 4.0 * T * T * spec.hidden
+    counted = fc.get_total_flops()
+    # the fusion 1x1 projections run here BEFORE the 2x upsample (they commute): 4x fewer FLOPs
+    g, F = spec.grid, spec.fusion
+    moved = sum(3 * 2.0 * s * s * F * F for s in (4 * g, 2 * g, g, (g + 1) // 2))
+    # FlopCounter counts SDPA on CPU as 0 or as bmm depending on the backend: accept either
+    ours = spec.flops_per_image() + moved
+    assert abs(counted - ours) <= 0.01 * ours or abs(counted + attn - ours) <= 0.01 * ours, (counted, ours)
