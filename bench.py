@@ -37,6 +37,12 @@ if ROOT not in sys.path:
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (AMD's 5 PF headline is 2:1 sparse)
+FP8_PEAK_TFLOPS = 5000.0       # dense MX fp8 (v_mfma_scale_f32_*_f8f6f4, 2x bf16 per clock)
+
+
+def _peak(label: str) -> float:
+    """Dense MFMA peak of the dtype a kernel computes in (fp8 engine labels: k_gemm_f8<...>)."""
+    return FP8_PEAK_TFLOPS if label.startswith("k_gemm_f8") else BF16_PEAK_TFLOPS
 
 
 def _args():
@@ -50,16 +56,26 @@ def _args():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-profile", action="store_true")
-    ap.add_argument("--all-gather", action="store_true",
-                    help="C3 layout: all-gather every rank's point buffers (RCCL over xGMI) inside each step")
-    ap.add_argument("--model", default="dpt-large", choices=["dpt-large", "depth-anything-v2"])
-    return ap.parse_args()
+    ap.add_argument("--no-all-gather", action="store_true",
+                    help="world > 1: skip the C3 all-gather of every rank's point buffers (RCCL over xGMI), "
+                         "which by default runs inside every step, overlapped with the next step's compute")
+    ap.add_argument("--model", default="dpt-large", choices=["dpt-large", "dpt-hybrid", "depth-anything-v2"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp8"],
+                    help="network arithmetic (fp8 = MX e4m3 on the scaled MFMA; DPT-Hybrid only). "
+                         "Default: fp8 for dpt-hybrid (BASELINE configs[4]), bf16 otherwise")
+    a = ap.parse_args()
+    if a.dtype is None:
+        a.dtype = "fp8" if a.model == "dpt-hybrid" else "bf16"
+    return a
 
 
 def _spec(name):
     if name == "depth-anything-v2":
         from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL
         return DA_V2_SMALL
+    if name == "dpt-hybrid":
+        from image_to_pointcloud_amd.dpt_hybrid import DPT_HYBRID
+        return DPT_HYBRID
     from image_to_pointcloud_amd.dpt import DPT_LARGE
     return DPT_LARGE
 
@@ -82,7 +98,7 @@ def _kernel_profile(pipe, images):
     stream = torch.cuda.current_stream()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    pipe.pre(images, layout="patches", out=pipe._patches)
+    pipe.pre(images, layout=pipe.layout, out=pipe._patches)
     depth = pipe.model(pipe._patches, pipe.batch)
     lib = _lib.load()
     lib.i2pc_profile_enable(1)
@@ -107,12 +123,12 @@ def _kernel_profile(pipe, images):
     return per, geo_t, (unp_ms * 1e-3 if unp_ms > 0 else None)
 
 
-def _pmc_traffic():
-    """HBM bytes per launch by kernel label from the newest profiles/r*_pmc_traffic.json
-    (tools/gpu_pmc_bench.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench,
+def _pmc_traffic(tag: str):
+    """HBM bytes per launch by kernel label from the newest profiles/r*_<tag>_pmc_traffic.json
+    (tools/gpu_profile.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench,
     gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or ({}, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc_traffic.json")))
     if not files:
         return {}, None
     with open(files[-1]) as fh:
@@ -152,6 +168,9 @@ def _cpu_baseline(spec, size, density):
     if spec.family == "depth-anything":
         from transformers import DepthAnythingConfig as Cfg, DepthAnythingForDepthEstimation as Net
         from image_to_pointcloud_amd.depth_anything import synthetic_state_dict
+    elif spec.family == "dpt-hybrid":
+        from transformers import DPTConfig as Cfg, DPTForDepthEstimation as Net
+        from image_to_pointcloud_amd.dpt_hybrid import synthetic_state_dict
     else:
         from transformers import DPTConfig as Cfg, DPTForDepthEstimation as Net
         from image_to_pointcloud_amd.dpt import synthetic_state_dict
@@ -198,24 +217,31 @@ def main():
     spec = _spec(a.model)
 
     B, S = a.batch, a.size
-    pipe = PointCloudPipeline(B, S, S, spec=spec, density=a.density, device=device, seed=0)
+    pipe = PointCloudPipeline(B, S, S, spec=spec, density=a.density, device=device, seed=0, dtype=a.dtype)
     images = _images(B, S, rank, device)
-    if a.no_graph:
+    gather = world > 1 and not a.no_all_gather
+    finish = lambda: None                   # noqa: E731
+    if gather:
+        # C3: two point-buffer sets (a second pipeline sharing the model), gather k under step k+1
+        pipe2 = PointCloudPipeline(B, S, S, spec=spec, density=a.density, device=device, model=pipe.model,
+                                   dtype=a.dtype)
+        if a.no_graph:
+            runs = [lambda: pipe.run(images), lambda: pipe2.run(images)]
+        else:
+            pipe.capture(images)
+            pipe2.capture(images)
+            runs = [pipe.replay, pipe2.replay]
+        og = D.OverlappedGather(runs, world, B, pipe.points_per_image, device)
+        step, finish = og.step, og.finish
+    elif a.no_graph:
         step = lambda: pipe.run(images)     # noqa: E731
         step()
     else:
         pipe.capture(images)
         step = pipe.replay
-    if a.all_gather and world > 1:
-        gx = torch.empty((world * B, pipe.points_per_image, 3), dtype=torch.float32, device=device)
-        gr = torch.empty((world * B, pipe.points_per_image, 3), dtype=torch.uint8, device=device)
-        inner = step
-
-        def step():
-            out = inner()
-            D.gather_points(out.xyz, out.rgb, out_xyz=gx, out_rgb=gr)
     for _ in range(a.warmup):
         step()
+    finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -223,6 +249,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    finish()                                # the last step's gather is part of the job
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -235,13 +262,14 @@ def main():
     kernels = None
     if rank == 0 and not a.no_kernel_profile:
         per, geo_t, unp_t = _kernel_profile(pipe, images)
-        pmc, pmc_src = _pmc_traffic()
+        pmc, pmc_src = _pmc_traffic(f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}"))
         dom = max(per.items(), key=lambda kv: kv[1]["t"])
         name, d = dom
         if d["flops"] > 0:
             ach = d["flops"] / d["n"] / (d["t"] / d["n"]) / 1e12
-            roofline = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": BF16_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(ach / BF16_PEAK_TFLOPS, 4), "traffic": None,
+            pk = _peak(name)
+            roofline = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": pk,
+                        "unit": "TFLOP/s", "frac": round(ach / pk, 4), "traffic": None,
                         "launches": d["n"], "avg_us": round(d["t"] / d["n"] * 1e6, 2),
                         "flops_per_launch": d["flops"] / d["n"],
                         "share_of_step": round(d["t"] / (ms * 1e-3), 3)}
@@ -270,11 +298,17 @@ def main():
             rooflines["unproject_kernel"].update(traffic=t, traffic_source=src)
         net_t = sum(v["t"] for v in per.values())
         net_f = sum(v["flops"] for v in per.values())
+        # mixed-precision networks: the peak is the FLOP-weighted harmonic mean of the kernels'
+        # dtype peaks (time at peak = sum flops_k / peak_k)
+        t_peak = sum(v["flops"] / (_peak(k) * 1e12) for k, v in per.items())
+        mix_peak = net_f / t_peak / 1e12 if t_peak > 0 else BF16_PEAK_TFLOPS
         rooflines["dpt_blocks"] = {"kernel": "all network launches (GEMM/conv/attention/LN/resize/head)",
                                    "bound": "mfma", "achieved": round(net_f / net_t / 1e12, 1),
-                                   "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                   "frac": round(net_f / net_t / 1e12 / BF16_PEAK_TFLOPS, 4), "traffic": None,
-                                   "ms": round(net_t * 1e3, 3)}
+                                   "peak": round(mix_peak, 1), "unit": "TFLOP/s",
+                                   "frac": round(t_peak / net_t, 4), "traffic": None,
+                                   "ms": round(net_t * 1e3, 3),
+                                   "fp8_flop_share": round(sum(v["flops"] for k, v in per.items()
+                                                               if k.startswith("k_gemm_f8")) / max(net_f, 1.0), 4)}
         kernels = {k: {"launches": v["n"], "ms": round(v["t"] * 1e3, 3),
                        "tflops": round(v["flops"] / v["t"] / 1e12, 1) if v["flops"] else None}
                    for k, v in sorted(per.items(), key=lambda kv: -kv[1]["t"])}
@@ -294,9 +328,10 @@ def main():
             "metric": "Mpoints/sec end-to-end (depth+unproject), 1024² batch",
             "value": round(value, 2), "unit": "Mpoints/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16", "data": f"synthetic (uint8 RGB uniform, PCG64 seeds 1000+i; seeded random {spec.name} weights)",
-            "config": {"workload": f"{spec.name} bf16 depth + unproject, batch {B} x {S}x{S} per GPU, density {a.density}"
-                                   + (", all-gather of points" if a.all_gather and world > 1 else ""),
+            "dtype": a.dtype, "data": f"synthetic (uint8 RGB uniform, PCG64 seeds 1000+i; seeded random {spec.name} weights)",
+            "config": {"workload": f"{spec.name} {a.dtype} depth + unproject, batch {B} x {S}x{S} per GPU, density {a.density}"
+                                   + (", RCCL all-gather of every rank's points overlapped with the next step"
+                                      if gather else ""),
                        "model": spec.name, "network_input": [pipe.pre.out_h, pipe.pre.out_w], "global_batch": B * world,
                        "image": [S, S], "points_per_image": pipe.points_per_image, "parallelism": f"dp{world}",
                        "hip_graph": not a.no_graph},

@@ -52,7 +52,11 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int qtiles = (T + kQ - 1) / kQ;
-  int bid = blockIdx.x;
+  // XCD-aware order: workgroups b and b + 8 share an XCD, so give each XCD a contiguous range
+  // of (image, head, q-tile) indices (bijective for any count): the q-tiles of one head then
+  // read its K / V through one L2 instead of up to five
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, xq = nwg >> 3, xr = nwg & 7;
+  int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (blockIdx.x >> 3);
   const int qt = bid % qtiles;
   bid /= qtiles;
   const int h = bid % NH;
@@ -239,7 +243,11 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int qtiles = (T + kQ - 1) / kQ;
-  int bid = blockIdx.x;
+  // XCD-aware order: workgroups b and b + 8 share an XCD, so give each XCD a contiguous range
+  // of (image, head, q-tile) indices (bijective for any count): the q-tiles of one head then
+  // read its K / V through one L2 instead of up to five
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, xq = nwg >> 3, xr = nwg & 7;
+  int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (blockIdx.x >> 3);
   const int qt = bid % qtiles;
   bid /= qtiles;
   const int h = bid % NH;

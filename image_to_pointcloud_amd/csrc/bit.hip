@@ -5,8 +5,8 @@
 //   k_stem_im2col : 7x7 stride-2 "SAME" stem conv input (BitEmbeddings.convolution,
 //                   modeling_bit.py:234-241, DynamicPad2d :148-196) as bf16 GEMM rows
 //                   [pixel][(ky, kx, c) padded to a multiple of 64]
-//   k_gn_stats    : GroupNorm statistics (nn.functional.group_norm, modeling_bit.py:142-146):
-//                   per (image, group) sum and sum of squares, fp32 per workgroup, fp64 atomics
+//   k_gn_partial / k_gn_finalize : GroupNorm statistics (nn.functional.group_norm,
+//                   modeling_bit.py:142-146): per-tile fp32 sums, fp64 combine -> (mean, rstd)
 //   k_gn_apply    : y = act(gn(x) + shortcut), shortcut = none | bf16 | gn(r) of a second map
 //                   (BitBottleneckLayer.forward, modeling_bit.py:429-447)
 //   k_maxpool     : 3x3 stride-2 max pool after dynamic SAME padding with value 0
@@ -60,108 +60,180 @@ __global__ __launch_bounds__(256) void k_stem_im2col(const float* __restrict__ x
   }
 }
 
-// One workgroup = one image x PIX pixels; thread t owns 8 consecutive channels of pixels
-// t / (C / 8) + j * (256 / (C / 8)).  Per-channel partial sums reduce through LDS, then one
-// thread per group adds them to the fp64 accumulators acc[b][g][2].
-constexpr int PIX = 128;
-__global__ __launch_bounds__(256) void k_gn_stats(const bf16_t* __restrict__ x, int HW, int C, int G,
-                                                  double* __restrict__ acc) {
-  __shared__ float ss[2][1024];
+// GroupNorm statistics in two launches, no atomics:
+//  k_gn_partial: one workgroup = one image x PIX pixels; thread t owns 8 consecutive channels
+//    of pixel lane t / (C / 8) and accumulates their sums / sums of squares over the tile in
+//    registers (fp32); the pixel lanes reduce through LDS and the workgroup writes one
+//    (sum, sumsq) pair per group to part[b][tile][g].
+//  k_gn_finalize: one thread per (image, group) adds the tile partials in fp64 and writes
+//    (mean, rstd) as float: stats[b][g] (biased variance, as nn.functional.group_norm).
+// pixels per workgroup: up to 512, fewer when that would leave < ~8 workgroups per CU
+static int gn_pix(int batch, int hw) {
+  const int64_t want = ((int64_t)batch * hw + 2047) / 2048;
+  return (int)std::max<int64_t>(32, std::min<int64_t>(512, (want + 31) / 32 * 32));
+}
+
+__global__ __launch_bounds__(256) void k_gn_partial(const bf16_t* __restrict__ x, int HW, int C, int G, int tiles,
+                                                    int PIX, float* __restrict__ part) {
+  __shared__ float red[2][2048];
   const int chunks = C / 8;
-  const int per_it = 256 / chunks;                 // pixels per iteration (C <= 2048)
-  const int tiles = (HW + PIX - 1) / PIX;
+  const int per_it = 256 / chunks;                 // pixel lanes (C <= 2048)
   const int b = blockIdx.x / tiles;
-  const int p0 = (blockIdx.x - b * tiles) * PIX;
-  const int ch = (threadIdx.x % chunks) * 8;
+  const int tile = blockIdx.x - b * tiles;
+  const int p0 = tile * PIX;
+  const int cc = threadIdx.x % chunks;
   const int pl = threadIdx.x / chunks;
   float s[8] = {}, q[8] = {};
   if (pl < per_it) {
-    const bf16_t* xb = x + (int64_t)b * HW * C;
-    for (int p = p0 + pl; p < min(p0 + PIX, HW); p += per_it) {
-      const uint4 u = *reinterpret_cast<const uint4*>(xb + (int64_t)p * C + ch);
-      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    const bf16_t* xb = x + (int64_t)b * HW * C + cc * 8;
+    const int p1 = min(p0 + PIX, HW);
+    constexpr int U = 8;                           // 8 independent 16-B loads in flight
+    for (int pb = p0 + pl; pb < p1; pb += U * per_it) {
+      uint4 u[U];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = __uint_as_float(w[e] << 16), c = __uint_as_float(w[e] & 0xffff0000u);
-        s[2 * e] += a; q[2 * e] += a * a;
-        s[2 * e + 1] += c; q[2 * e + 1] += c * c;
+      for (int k = 0; k < U; ++k) {
+        const int p = pb + k * per_it;
+        u[k] = p < p1 ? *reinterpret_cast<const uint4*>(xb + (int64_t)p * C) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t w[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float a = __uint_as_float(w[e] << 16), c = __uint_as_float(w[e] & 0xffff0000u);
+          s[2 * e] += a; q[2 * e] = fmaf(a, a, q[2 * e]);
+          s[2 * e + 1] += c; q[2 * e + 1] = fmaf(c, c, q[2 * e + 1]);
+        }
       }
     }
   }
-  for (int i = threadIdx.x; i < 2 * 1024; i += 256) (&ss[0][0])[i] = 0.f;
-  __syncthreads();
+  // per channel: sum over the pixel lanes through the lane-major LDS image [per_it][C]
+  // (per_it * C <= 2048 because per_it = 256 / (C / 8))
   if (pl < per_it) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      atomicAdd(&ss[0][ch + e], s[e]);
-      atomicAdd(&ss[1][ch + e], q[e]);
+      red[0][pl * C + cc * 8 + e] = s[e];
+      red[1][pl * C + cc * 8 + e] = q[e];
     }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f, d = 0.f;
+    for (int l = 0; l < per_it; ++l) { a += red[0][l * C + c]; d += red[1][l * C + c]; }
+    red[0][c] = a;            // (only this thread reads column c, and row 0 is its own slot)
+    red[1][c] = d;
   }
   __syncthreads();
   const int cg = C / G;
   for (int g = threadIdx.x; g < G; g += 256) {
-    double a = 0.0, c = 0.0;
-    for (int k = 0; k < cg; ++k) { a += ss[0][g * cg + k]; c += ss[1][g * cg + k]; }
-    atomicAdd(&acc[((int64_t)b * G + g) * 2], a);
-    atomicAdd(&acc[((int64_t)b * G + g) * 2 + 1], c);
+    float a = 0.f, d = 0.f;
+    for (int k = 0; k < cg; ++k) { a += red[0][g * cg + k]; d += red[1][g * cg + k]; }
+    part[(((int64_t)b * tiles + tile) * G + g) * 2] = a;
+    part[(((int64_t)b * tiles + tile) * G + g) * 2 + 1] = d;
   }
+}
+
+__global__ void k_gn_finalize(const float* __restrict__ part, int B, int G, int tiles, double inv_n, float eps,
+                              float* __restrict__ stats) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * G) return;
+  const int b = i / G, g = i - (i / G) * G;
+  double a = 0.0, d = 0.0;
+  for (int t = 0; t < tiles; ++t) {
+    a += part[(((int64_t)b * tiles + t) * G + g) * 2];
+    d += part[(((int64_t)b * tiles + t) * G + g) * 2 + 1];
+  }
+  const double mean = a * inv_n;
+  const double var = fmax(d * inv_n - mean * mean, 0.0);
+  stats[2 * i] = (float)mean;
+  stats[2 * i + 1] = 1.0f / sqrtf((float)var + eps);
 }
 
 struct GnOperand {
   const bf16_t* x;
-  const double* acc;        // [B][G][2] sums (null: x is used raw)
+  const float* stats;       // [B][G] (mean, rstd) (null: x is used raw)
   const float* gamma;
   const float* beta;
 };
 
-__device__ __forceinline__ void gn_load(const GnOperand& o, int64_t off, int b, int c0, int C, int G, float inv_n,
-                                        float eps, float v[8]) {
-  const uint4 u = *reinterpret_cast<const uint4*>(o.x + off);
+// per-channel affine of one operand for image b: v * sc + sh (identity when raw)
+__device__ __forceinline__ void gn_coeffs(const GnOperand& o, int b, int c0, int C, int G, float sc[8], float sh[8]) {
+  if (!o.stats) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+    return;
+  }
+  const int cg = C / G;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e;
+    const float2 st = *reinterpret_cast<const float2*>(o.stats + ((int64_t)b * G + c / cg) * 2);
+    sc[e] = st.y * o.gamma[c];
+    sh[e] = o.beta[c] - st.x * sc[e];
+  }
+}
+
+__device__ __forceinline__ void unpack8(const uint4& u, float v[8]) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     v[2 * e] = __uint_as_float(w[e] << 16);
     v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
   }
-  if (!o.acc) return;
-  const int cg = C / G;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int c = c0 + e;
-    const int g = c / cg;
-    const double sum = o.acc[((int64_t)b * G + g) * 2], sq = o.acc[((int64_t)b * G + g) * 2 + 1];
-    const double mean = sum * inv_n;
-    const double var = fmax(sq * inv_n - mean * mean, 0.0);
-    const float rstd = 1.0f / sqrtf((float)var + eps);
-    v[e] = (v[e] - (float)mean) * rstd * o.gamma[c] + o.beta[c];
-  }
 }
 
-__global__ __launch_bounds__(256) void k_gn_apply(GnOperand a, GnOperand r, int has_r, int B, int HW, int C, int G,
-                                                  float eps, int relu, bf16_t* __restrict__ y) {
-  const int64_t total = (int64_t)B * HW * (C / 8);
-  const float inv_n = 1.0f / ((float)HW * (float)(C / G));
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t off = i * 8;
-    const int c0 = (int)(off % C);
-    const int b = (int)(off / ((int64_t)HW * C));
-    float v[8], w[8];
-    gn_load(a, off, b, c0, C, G, inv_n, eps, v);
-    if (has_r) {
-      gn_load(r, off, b, c0, C, G, inv_n, eps, w);
+// One workgroup = one image x PIX pixels; thread = (channel chunk, pixel lane) as in
+// k_gn_partial, so every thread derives its 8 channels' scale / shift once.
+// (x - mean) * rstd * gamma + beta is evaluated as x * (rstd * gamma) + (beta - mean * rstd * gamma).
+__global__ __launch_bounds__(256) void k_gn_apply(GnOperand a, GnOperand r, int has_r, int HW, int C, int G, int tiles,
+                                                  int PIX, int relu, bf16_t* __restrict__ y) {
+  const int chunks = C / 8;
+  const int per_it = 256 / chunks;
+  const int b = blockIdx.x / tiles;
+  const int p0 = (blockIdx.x - b * tiles) * PIX;
+  const int cc = threadIdx.x % chunks;
+  const int pl = threadIdx.x / chunks;
+  if (pl >= per_it) return;
+  const int c0 = cc * 8;
+  float as[8], ah[8], rs[8], rh[8];
+  gn_coeffs(a, b, c0, C, G, as, ah);
+  if (has_r) gn_coeffs(r, b, c0, C, G, rs, rh);
+  const int64_t base = (int64_t)b * HW * C + c0;
+  const int p1 = min(p0 + PIX, HW);
+  constexpr int U = 4;
+  for (int pb = p0 + pl; pb < p1; pb += U * per_it) {
+    uint4 ux[U], ur[U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += w[e];
+    for (int k = 0; k < U; ++k) {
+      const int p = pb + k * per_it;
+      const int64_t off = base + (int64_t)min(p, p1 - 1) * C;
+      ux[k] = *reinterpret_cast<const uint4*>(a.x + off);
+      if (has_r) ur[k] = *reinterpret_cast<const uint4*>(r.x + off);
     }
-    if (relu) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    for (int k = 0; k < U; ++k) {
+      const int p = pb + k * per_it;
+      if (p >= p1) break;
+      float v[8], w[8];
+      unpack8(ux[k], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaf(v[e], as[e], ah[e]);
+      if (has_r) {
+        unpack8(ur[k], w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += fmaf(w[e], rs[e], rh[e]);
+      }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      uint4 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+      o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      *reinterpret_cast<uint4*>(y + base + (int64_t)p * C) = o;
     }
-    uint4 o;
-    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    *reinterpret_cast<uint4*>(y + off) = o;
   }
 }
 
@@ -225,29 +297,43 @@ extern "C" int i2pc_bit_stem_im2col(const float* pixels, int batch, int h, int w
   return check_launch("bit_stem_im2col");
 }
 
-extern "C" int i2pc_groupnorm_stats(const void* x, int batch, int hw, int c, int groups, double* acc, void* stream) {
+extern "C" size_t i2pc_groupnorm_workspace_bytes(int batch, int hw, int groups) {
+  const int pix = gn_pix(batch, hw);
+  return sizeof(float) * 2 * (size_t)batch * ((hw + pix - 1) / pix) * groups;
+}
+
+extern "C" int i2pc_groupnorm_stats(const void* x, int batch, int hw, int c, int groups, float eps, float* stats,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
-  I2PC_REQUIRE(x && acc && batch > 0 && hw > 0, "bad arguments");
-  I2PC_REQUIRE(c % 8 == 0 && c <= 1024 && groups > 0 && c % groups == 0, "groupnorm: C=%d (%% 8, <= 1024) / groups %d", c, groups);
+  I2PC_REQUIRE(x && stats && workspace && batch > 0 && hw > 0, "bad arguments");
+  I2PC_REQUIRE(c % 8 == 0 && c <= 2048 && groups > 0 && c % groups == 0, "groupnorm: C=%d (%% 8, <= 2048) / groups %d", c, groups);
+  const int pix = gn_pix(batch, hw);
+  const int tiles = (hw + pix - 1) / pix;
+  I2PC_REQUIRE(workspace_bytes >= i2pc_groupnorm_workspace_bytes(batch, hw, groups), "groupnorm: workspace too small");
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(acc, 0, sizeof(double) * 2 * batch * groups, s) != hipSuccess) return set_error(I2PC_ELAUNCH, "memset failed");
-  const int tiles = (hw + PIX - 1) / PIX;
-  hipLaunchKernelGGL(k_gn_stats, dim3(batch * tiles), dim3(256), 0, s, static_cast<const bf16_t*>(x), hw, c, groups, acc);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(k_gn_partial, dim3(batch * tiles), dim3(256), 0, s, static_cast<const bf16_t*>(x), hw, c, groups,
+                     tiles, pix, part);
+  const int n = batch * groups;
+  hipLaunchKernelGGL(k_gn_finalize, dim3((n + 255) / 256), dim3(256), 0, s, part, batch, groups, tiles,
+                     1.0 / ((double)hw * (c / groups)), eps, stats);
   return check_launch("groupnorm_stats");
 }
 
-extern "C" int i2pc_groupnorm_apply(const void* x, const double* acc, const float* gamma, const float* beta,
-                                    const void* r, const double* r_acc, const float* r_gamma, const float* r_beta,
-                                    int batch, int hw, int c, int groups, float eps, int relu, void* y, void* stream) {
+extern "C" int i2pc_groupnorm_apply(const void* x, const float* stats, const float* gamma, const float* beta,
+                                    const void* r, const float* r_stats, const float* r_gamma, const float* r_beta,
+                                    int batch, int hw, int c, int groups, int relu, void* y, void* stream) {
   clear_error();
   I2PC_REQUIRE(x && y && batch > 0 && hw > 0 && c % 8 == 0 && groups > 0 && c % groups == 0, "bad arguments");
-  I2PC_REQUIRE(!acc || (gamma && beta), "groupnorm: gamma/beta required with statistics");
-  I2PC_REQUIRE(!r_acc || (r && r_gamma && r_beta), "groupnorm: shortcut gamma/beta required with its statistics");
-  GnOperand a{static_cast<const bf16_t*>(x), acc, gamma, beta};
-  GnOperand rr{static_cast<const bf16_t*>(r), r_acc, r_gamma, r_beta};
-  const int64_t work = (int64_t)batch * hw * (c / 8);
-  hipLaunchKernelGGL(k_gn_apply, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), a, rr, r ? 1 : 0, batch, hw, c,
-                     groups, eps, relu, static_cast<bf16_t*>(y));
+  I2PC_REQUIRE(!stats || (gamma && beta), "groupnorm: gamma/beta required with statistics");
+  I2PC_REQUIRE(!r_stats || (r && r_gamma && r_beta), "groupnorm: shortcut gamma/beta required with its statistics");
+  I2PC_REQUIRE(c <= 2048, "groupnorm: C=%d > 2048", c);
+  GnOperand a{static_cast<const bf16_t*>(x), stats, gamma, beta};
+  GnOperand rr{static_cast<const bf16_t*>(r), r_stats, r_gamma, r_beta};
+  const int pix = gn_pix(batch, hw);
+  const int tiles = (hw + pix - 1) / pix;
+  hipLaunchKernelGGL(k_gn_apply, dim3(batch * tiles), dim3(256), 0, as_stream(stream), a, rr, r ? 1 : 0, hw, c, groups,
+                     tiles, pix, relu, static_cast<bf16_t*>(y));
   return check_launch("groupnorm_apply");
 }
 

@@ -4,9 +4,10 @@ Every image is independent (percentiles, intrinsics and bbox are per image,
 backend/app.py:197-223), so ranks own contiguous slices of the global batch and
 compute without any data-path collective (weak scaling).  The north star's C3
 configuration additionally gathers every rank's fixed-size point buffers onto
-every rank (`gather_points`, one RCCL all-gather per tensor over xGMI); the
-result is image-major, i.e. exactly the concatenation of the per-image
-reference outputs.
+every rank (`gather_points`, one RCCL all-gather per tensor over xGMI;
+`OverlappedGather` runs it under the next step's compute); the result is
+image-major, i.e. exactly the concatenation of the per-image reference outputs
+(SURVEY §8e).
 """
 from __future__ import annotations
 
@@ -42,6 +43,53 @@ def gather_points(xyz, rgb, group=None, out_xyz=None, out_rgb=None):
     dist.all_gather_into_tensor(out_xyz, xyz.contiguous(), group=group)
     dist.all_gather_into_tensor(out_rgb, rgb.contiguous(), group=group)
     return out_xyz, out_rgb
+
+
+class OverlappedGather:
+    """The C3 layout: every step's point buffers all-gathered onto every rank, gather k
+    overlapped with compute k + 1.
+
+    `runs` are two step callables that write into two different point-buffer sets (slot 0 / 1,
+    e.g. two graph-captured PointCloudPipelines sharing one model) and return them as a
+    PointBatch.  step() computes into slot k % 2 on the current stream, then launches the two
+    RCCL all-gathers of that slot asynchronously (torch.distributed async_op: the collective
+    waits for the compute on its own stream, the current stream goes on with step k + 1).
+    Before a slot is overwritten, the current stream waits for the gather that read it."""
+
+    def __init__(self, runs, world: int, batch: int, points: int, device, group=None):
+        import torch
+        if len(runs) != 2:
+            raise ValueError("OverlappedGather needs two step callables (double-buffered point sets)")
+        self.runs, self.group = runs, group
+        self.gx = [torch.empty((world * batch, points, 3), dtype=torch.float32, device=device) for _ in range(2)]
+        self.gr = [torch.empty((world * batch, points, 3), dtype=torch.uint8, device=device) for _ in range(2)]
+        self.works = [None, None]
+        self.k = 0
+
+    def step(self):
+        import torch.distributed as dist
+        slot = self.k & 1
+        self._wait(slot)                      # the gather that read this slot's buffers is done
+        out = self.runs[slot]()
+        self.works[slot] = (dist.all_gather_into_tensor(self.gx[slot], out.xyz, group=self.group, async_op=True),
+                            dist.all_gather_into_tensor(self.gr[slot], out.rgb, group=self.group, async_op=True))
+        self.k += 1
+        return slot
+
+    def _wait(self, slot):
+        w = self.works[slot]
+        if w is not None:
+            for x in w:
+                x.wait()
+            self.works[slot] = None
+
+    def finish(self):
+        """Make the current stream wait for every outstanding gather."""
+        self._wait(0)
+        self._wait(1)
+
+    def gathered(self, slot):
+        return self.gx[slot], self.gr[slot]
 
 
 def max_over_ranks(seconds: float, device=None) -> float:

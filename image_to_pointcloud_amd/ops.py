@@ -501,11 +501,12 @@ def conv2d_fp8(x: Fp8, w: Fp8, bias=None, k=3, stride=1, pad=1, relu_in=False, a
 _lib.register("i2pc_bit_stem_im2col", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                      c_void_p, c_void_p])
+_lib.register("i2pc_groupnorm_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int])
 _lib.register("i2pc_groupnorm_stats", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                                     c_void_p, c_void_p])
+                                                     ctypes.c_float, c_void_p, c_void_p, ctypes.c_size_t, c_void_p])
 _lib.register("i2pc_groupnorm_apply", ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                                      c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                                     ctypes.c_float, ctypes.c_int, c_void_p, c_void_p])
+                                                     ctypes.c_int, c_void_p, c_void_p])
 _lib.register("i2pc_maxpool3s2", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p])
 
@@ -542,9 +543,11 @@ def group_norm(x, gamma, beta, groups=32, eps=1e-5, relu=False, shortcut=None, a
     hw = H * W
 
     def stats(t):
-        a = torch.empty((B, groups, 2), dtype=torch.float64, device=t.device)
+        a = torch.empty((B, groups, 2), dtype=torch.float32, device=t.device)
+        nb = _lib.load().i2pc_groupnorm_workspace_bytes(B, hw, groups)
+        ws = torch.empty(max(nb, 4), dtype=torch.uint8, device=t.device)
         with _Timed("k_gn_stats", 0.0, t.numel() * 2.0):
-            _lib.call("i2pc_groupnorm_stats", _p(t), B, hw, C, groups, _p(a), _stream())
+            _lib.call("i2pc_groupnorm_stats", _p(t), B, hw, C, groups, float(eps), _p(a), _p(ws), nb, _stream())
         return a
 
     a = acc if acc is not None else stats(x)
@@ -559,7 +562,7 @@ def group_norm(x, gamma, beta, groups=32, eps=1e-5, relu=False, shortcut=None, a
     nbytes = x.numel() * 4.0 + (r.numel() * 2.0 if r is not None else 0.0)
     with _Timed("k_gn_apply", 0.0, nbytes):
         _lib.call("i2pc_groupnorm_apply", _p(x), _p(a), _p(gamma), _p(beta), _p(r), _p(ra), _p(rg), _p(rb), B, hw, C,
-                  groups, float(eps), int(bool(relu)), _p(out), _stream())
+                  groups, int(bool(relu)), _p(out), _stream())
     return out
 
 

@@ -229,18 +229,22 @@ int i2pc_layernorm_fp8(const float* x, int64_t ldx, const float* gamma, const fl
  * bit_stem_im2col: fp32 NCHW pixel_values -> bf16 GEMM rows [b*out_h*out_w][k_pitch], k =
  *   (ky*ksize + kx)*3 + c (zero past ksize^2*3), input pixel (oy*2 - pad_top + ky, ox*2 -
  *   pad_left + kx), zero outside (DynamicPad2d "SAME", modeling_bit.py:148-196).
- * groupnorm_stats: acc fp64 [batch][groups][2] = per-group sum, sum of squares (zeroed here).
- * groupnorm_apply: y = relu?(gn(x) + shortcut); gn(x) = (x - mean) * rstd * gamma + beta with
- *   biased variance (nn.functional.group_norm); acc NULL = x raw; shortcut r NULL = none,
- *   r with r_acc NULL = raw bf16, else gn(r) with its own statistics.
+ * groupnorm_stats: stats fp32 [batch][groups][2] = (mean, 1 / sqrt(var + eps)), biased variance
+ *   (nn.functional.group_norm): per-tile fp32 sums into `workspace`
+ *   (>= i2pc_groupnorm_workspace_bytes), combined in fp64.
+ * groupnorm_apply: y = relu?(gn(x) + shortcut); gn(x) = (x - mean) * rstd * gamma + beta;
+ *   stats NULL = x raw; shortcut r NULL = none, r with r_stats NULL = raw bf16, else gn(r)
+ *   with its own statistics.
  * maxpool3s2: 3x3 stride-2 max pool, zero padding pad_top/pad_left and past the bottom/right
  *   edge (BitMaxPool2d with DynamicPad2d, modeling_bit.py:199-223). */
 int i2pc_bit_stem_im2col(const float* pixels, int batch, int h, int w, int out_h, int out_w, int pad_top,
                          int pad_left, int ksize, int k_pitch, void* out, void* stream);
-int i2pc_groupnorm_stats(const void* x, int batch, int hw, int c, int groups, double* acc, void* stream);
-int i2pc_groupnorm_apply(const void* x, const double* acc, const float* gamma, const float* beta, const void* r,
-                         const double* r_acc, const float* r_gamma, const float* r_beta, int batch, int hw, int c,
-                         int groups, float eps, int relu, void* y, void* stream);
+size_t i2pc_groupnorm_workspace_bytes(int batch, int hw, int groups);
+int i2pc_groupnorm_stats(const void* x, int batch, int hw, int c, int groups, float eps, float* stats,
+                         void* workspace, size_t workspace_bytes, void* stream);
+int i2pc_groupnorm_apply(const void* x, const float* stats, const float* gamma, const float* beta, const void* r,
+                         const float* r_stats, const float* r_gamma, const float* r_beta, int batch, int hw, int c,
+                         int groups, int relu, void* y, void* stream);
 int i2pc_maxpool3s2(const void* x, int batch, int h, int w, int c, int out_h, int out_w, int pad_top, int pad_left,
                     void* y, void* stream);
 

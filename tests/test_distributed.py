@@ -110,3 +110,58 @@ def test_band_exchange_protocol():
         assert hist.tolist() == [3 * i for i in range(8)]
         assert cnt[:, 0].tolist() == [3, 10, 99, 8]
         assert bb.tolist() == [0.0, 6.0, -1.0, 2.0, 0.0, 2.0]
+
+
+def _overlap_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from image_to_pointcloud_amd.geometry import PointBatch
+        B, N = 2, 4
+        bufs = [PointBatch(torch.zeros(B, N, 3), torch.zeros(B, N, 3, dtype=torch.uint8), None, None) for _ in range(2)]
+        state = {"k": 0}
+
+        def make(slot):
+            def run():
+                k = state["k"]                      # step k writes (rank, k)-coded values into its slot
+                bufs[slot].xyz.fill_(1000 * rank + k)
+                bufs[slot].rgb.fill_((10 * rank + k) % 256)
+                state["k"] += 1
+                return bufs[slot]
+            return run
+
+        og = D.OverlappedGather([make(0), make(1)], ws, B, N, "cpu")
+        seen = []
+        for k in range(5):
+            slot = og.step()
+            if k >= 1:                              # step k-1's gather (other slot) may be read now
+                og._wait(slot ^ 1)
+                gx, gr = og.gathered(slot ^ 1)
+                seen.append((k - 1, gx[:, 0, 0].tolist(), gr[:, 0, 0].tolist()))
+        og.finish()
+        gx, gr = og.gathered(4 & 1)
+        seen.append((4, gx[:, 0, 0].tolist(), gr[:, 0, 0].tolist()))
+        q.put((rank, seen))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_gather_double_buffers():
+    """C3: gather k (async) overlaps step k+1; each step's gathered buffer holds exactly that
+    step's points from every rank, image-major, although the next step already overwrote
+    the other slot."""
+    ws, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(ws)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, seen in out:
+        assert [k for k, _, _ in seen] == [0, 1, 2, 3, 4]
+        for k, xs, rs in seen:
+            assert xs == [float(k), float(k), 1000.0 + k, 1000.0 + k]
+            assert rs == [k, k, 10 + k, 10 + k]

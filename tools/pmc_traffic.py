@@ -15,14 +15,17 @@ import re
 import sys
 from collections import defaultdict
 
-EPI = {"0": "plain", "1": "res_f32", "2": "res_bf16", "3": "res2", "4": "convT"}
+EPI = {"0": "plain", "1": "res_f32", "2": "res_bf16", "3": "res2", "4": "convT", "5": "q8"}
 
 
 def label(name: str) -> str:
     n = re.sub(r"^void ", "", name.split("(")[0].strip())
     n = re.sub(r"\b[A-Za-z_]\w*::", "", n)
-    m = re.match(r"k_gemm_p<(\d+), (\w+), (\w+), (\d+)>", n)
+    # k_gemm_p<BM, CONV, RELU_A, EPI[, BN, F8]> -> the bench labels (gemm.hip plan_name / plan8_name)
+    m = re.match(r"k_gemm_p<(\d+), (\w+), (\w+), (\d+)(?:, (\d+), (\w+))?>", n)
     if m:
+        if m[6] == "true":
+            return f"k_gemm_f8<{m[5]}, {m[2]}, {m[3]}, {EPI.get(m[4], m[4])}>"
         return f"k_gemm_p<{m[1]}, {m[2]}, {m[3]}, {EPI.get(m[4], m[4])}>"
     if n.startswith("k_attention"):
         return "k_attention"
