@@ -207,16 +207,32 @@ def test_band_unproject_matches_whole_image(density, parts):
     in-process all-reduce as the exchange) each unproject a row band of one image; the
     concatenated bands are bit-identical to the whole-image unprojection, every rank gets
     the same p2/p98 / nanmedian stats, and the min/max of the band bboxes is the bbox."""
+    dep = _smooth_depth(48, 64, 51)
+    dep[3, 4] = np.nan                      # exercises the nanmedian pass as well
+    _band_check(dep, _rgb(301, 410, 52), parts, density)
+
+
+def test_c4_panorama_full_size_bands_and_oracle():
+    """C4 at its real size: an 8192 x 4096 panorama with 518 x 1036 model-resolution depth
+    (the DA processor's keep-aspect output for it), density high (33,554,432 points).  The
+    whole-image unprojection is bit-exact with the vectorised oracle, and the 8-band split
+    (8 'ranks') concatenates bit-identically to it."""
+    dep = _smooth_depth(518, 1036, 71)
+    img = _rgb(4096, 8192, 72)
+    whole = _band_check(dep, img, 8, "high", depth_scale=10.0)
+    ep, ec = ref.depth_to_point_cloud(img, dep, density="high", depth_scale=10.0, loop=False)
+    assert _same_bits(whole.xyz[0].cpu().numpy(), ep), _first_diff(whole.xyz[0].cpu().numpy(), ep)
+    assert _same_bits(whole.rgb[0].cpu().numpy().astype(np.float32), ec)
+
+
+def _band_check(dep, img, parts, density, depth_scale=12.0):
     import threading
     g = _geom()
     dev = torch.device("cuda")
-    h, w, H, W = 48, 64, 301, 410
-    dep = _smooth_depth(h, w, 51)
-    dep[3, 4] = np.nan                      # exercises the nanmedian pass as well
-    img = _rgb(H, W, 52)
+    H, W = img.shape[:2]
     tdep = torch.from_numpy(dep).to(dev)
     timg = torch.from_numpy(img).to(dev)
-    whole = g.unproject_batch(tdep[None], timg[None], density=density, depth_scale=12.0)
+    whole = g.unproject_batch(tdep[None], timg[None], density=density, depth_scale=depth_scale)
     torch.cuda.synchronize()
     step = g.DENSITY_STEP[density]
     bands = g.band_rows(H, parts, step)
@@ -245,7 +261,7 @@ def test_band_unproject_matches_whole_image(density, parts):
                 r0, r1 = bands[i]
                 ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
                 results[i] = g.unproject_band(tdep, timg[r0:r1], H, W, r0, r1, exchange_for(i), density=density,
-                                              depth_scale=12.0, workspace=ws)
+                                              depth_scale=depth_scale, workspace=ws)
                 torch.cuda.current_stream().synchronize()
         except Exception as e:   # pragma: no cover - reported below
             errs.append(e)
@@ -268,3 +284,4 @@ def test_band_unproject_matches_whole_image(density, parts):
     glob[0::2] = bb[:, 0::2].min(0)
     glob[1::2] = bb[:, 1::2].max(0)
     assert _same_bits(glob, whole.bbox[0].cpu().numpy())
+    return whole
