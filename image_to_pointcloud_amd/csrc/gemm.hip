@@ -1041,6 +1041,242 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     after_epi = true;
   }
 }
+// ---------------------------------------------------------------------------
+// Quarter-pipelined persistent 256 x 256 x 64 bf16 engine (k_gemm_q).  The LDS holds two
+// K-tiles (128 KB), each split into four 16-KB quarters: A-q0 / A-q1 (the 64-row halves
+// mp of both 128-row wave halves) and B-q0 / B-q1 (the 32-column halves np of every wave's
+// 64 columns).  A K-tile is computed in four phases, one (mp, np) quadrant of every wave's
+// 128 x 64 output each: (0,0) (0,1) (1,1) (1,0), with the A fragments of a quadrant reused by
+// the next one and the B-q0 fragments kept in registers from phase 1 to phase 4.  A quarter is
+// therefore last read in phase 1 (A-q0, B-q0), 2 (B-q1) or 3 (A-q1), and is refilled with the
+// K-tile two ahead right after that phase's barrier: every quarter has two K-tiles of
+// latency cover instead of one, and at most ~7/8 of the LDS is in flight at any time.
+// One barrier per phase: [ds_read this phase's quarter] [lgkmcnt(0)] [vmcnt(N): the quarter
+// the next phase reads has landed] [s_barrier] [refill the quarter this phase released]
+// [16 MFMAs].  The counts N are exact because every wave issues the same 2 glds per quarter;
+// an epilogue between two tiles adds its E_ALL operations to the first waits of the next tile.
+// acc[i][j] covers rows wm*128 + i*16 + (lane & 15), columns wn*64 + j*16 + (lane >> 4)*4 --
+// the k_gemm_p layout, so epilogue_p is shared (bias read from global memory).
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N < 63 ? N : 63) : "memory");
+}
+
+template <bool CONV, bool RELU_A, int EPI>
+__global__ __launch_bounds__(512) void k_gemm_q(Args p) {
+  constexpr int BM = 256, BN = 256, RM = 8, RN = 4, ROWB = 128, QB = 128 * ROWB;   // quarter bytes
+  constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
+  constexpr int E_ALL = RM * (NRL + NS);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // [2][A-q0, A-q1, B-q0, B-q1]
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, pchunk = lane & 7;
+
+  const int T = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, xl = blockIdx.x >> 3, xq = G >> 3, xr = G & 7;
+  int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + xl;
+  if (t >= T) return;
+
+  const rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, p.a_bytes, 0x00020000);
+  const rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W), 0, p.w_bytes, 0x00020000);
+  const int chunk16 = (pchunk ^ lrow) << 4;
+  // quarter row r (0..127) -> tile row / column; this wave fills quarter rows wid*16 + j*8 + lrow
+  auto a_row = [&](int mp, int j) { const int r = wid * 16 + j * 8 + lrow; return (r >> 6) * 128 + mp * 64 + (r & 63); };
+  auto b_row = [&](int np, int j) { const int r = wid * 16 + j * 8 + lrow; return (r >> 5) * 64 + np * 32 + (r & 31); };
+
+  uint32_t a_off[2][2], w_off[2][2];       // dense A / W byte offsets of this lane's rows [quarter][j]
+  int cpix[2][2], cyx[2][2];               // conv: pixel of this lane's A rows
+  int nm0 = 0, nn0 = 0;
+  auto setup = [&](int tile) {
+    int tm, tn;
+    grouped(p, tile, tm, tn);
+    nm0 = tm * BM;
+    nn0 = tn * BN;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = nm0 + a_row(q, j);
+        if constexpr (!CONV) {
+          a_off[q][j] = (uint32_t)m * (uint32_t)(p.lda * 2) + chunk16;
+        } else {
+          const int hw = p.coh * p.cow;
+          const int b = m / hw;
+          const int rem = m - b * hw;
+          const int oy = rem / p.cow;
+          const int ox = rem - oy * p.cow;
+          cpix[q][j] = b * p.ch * p.cw;
+          cyx[q][j] = m < p.M ? ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff) : (int)(0x4000u << 16);
+        }
+        w_off[q][j] = (uint32_t)(nn0 + b_row(q, j)) * (uint32_t)(p.ldw * 2) + chunk16;
+      }
+  };
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  // one quarter (0: A-q0, 1: A-q1, 2: B-q0, 3: B-q1) of K-tile k0 into buffer `buf`
+  auto fill = [&](int buf, int quarter, int k0) {
+    uint8_t* dst = smem + (buf * 4 + quarter) * QB + wid * 16 * ROWB;
+    if (quarter < 2) {
+      const int q = quarter;
+      if constexpr (!CONV) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(dst + j * 8 * ROWB), 16, a_off[q][j], k0 * 2, 0, 0);
+      } else {
+        const int kk = k0 / p.cc;
+        const int ky = kk / p.ck;
+        const int kx = kk - ky * p.ck;
+        const int ci0 = k0 - kk * p.cc;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int yi = (cyx[q][j] >> 16) + ky, xi = ((int)(short)(cyx[q][j] & 0xffff)) + kx;
+          const bool ok = (unsigned)yi < (unsigned)p.ch && (unsigned)xi < (unsigned)p.cw;
+          const int off = ok ? ((cpix[q][j] + yi * p.cw + xi) * p.cc + ci0) * 2 + chunk16 : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(dst + j * 8 * ROWB), 16, off, 0, 0, 0);
+        }
+      }
+    } else {
+      const int q = quarter - 2;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rs, (lds_ptr_t)(dst + j * 8 * ROWB), 16, w_off[q][j], k0 * 2, 0, 0);
+    }
+  };
+  auto read_frag = [&](int buf, int quarter, int row, int s) {
+    const uint8_t* base = smem + (buf * 4 + quarter) * QB + row * ROWB;
+    return *reinterpret_cast<const bf16x8*>(base + (((4 * s + fq) ^ (row & 7)) << 4));
+  };
+
+  const rsrc_t c_rs = make_rsrc(p.C);
+  const rsrc_t r_rs = make_rsrc(p.res);
+  const rsrc_t r2_rs = make_rsrc(p.res2);
+  const int nk = p.K / BK;
+
+  setup(t);
+  // prologue: K-tiles 0 and 1 in quarter order
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    if (kt < nk) {
+      fill(kt, 0, kt * BK); fill(kt, 2, kt * BK); fill(kt, 3, kt * BK); fill(kt, 1, kt * BK);
+    }
+  }
+  if (nk >= 2) I2PC_WAIT_VM(12); else I2PC_WAIT_VM(0);
+  I2PC_LDS_BARRIER();
+
+  int g = 0;                 // global K-tile counter (buffer parity)
+  bool after_epi = false;
+  int m0 = nm0, n0 = nn0;
+  for (;;) {
+    const int t_next = t + G;
+    const bool has_next = t_next < T;
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = g & 1;
+      // what K-tile two ahead is (this tile's, the next tile's, or none)
+      const bool ahead_here = kt + 2 < nk;
+      const bool ahead_next = !ahead_here && has_next;
+      const bool issue = ahead_here || ahead_next;
+      const int k_ahead = ahead_here ? (kt + 2) * BK : (kt + 2 - nk) * BK;
+      if (kt == nk - 2 && has_next) setup(t_next);        // (nk >= 2) offsets switch to the next tile
+      // the epilogue of the previous tile issued E_ALL operations after the loads that the
+      // first waits of K-tiles 0 and 1 target; with nothing issued ahead (the last tile's
+      // tail) the counted waits would undercount: wait for everything there
+      const bool epi_gap = after_epi && kt < 2;
+      const bool tail = !has_next && kt + 2 >= nk;
+      bf16x8 af[4][2], b0[2][2], b1[2][2];
+      // ---------------- phase 1: (mp 0, np 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) af[i][s] = read_frag(buf, 0, wm * 64 + i * 16 + frow, s);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b0[j][s] = read_frag(buf, 2, wn * 32 + j * 16 + frow, s);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (tail) I2PC_WAIT_VM(0);
+      else if (epi_gap) wait_vm<10 + E_ALL>();
+      else I2PC_WAIT_VM(10);
+      I2PC_LDS_BARRIER();
+      if (issue) { fill(buf, 0, k_ahead); fill(buf, 2, k_ahead); }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a, acc[i][j], 0, 0, 0);
+        }
+      // ---------------- phase 2: (mp 0, np 1)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b1[j][s] = read_frag(buf, 3, wn * 32 + j * 16 + frow, s);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (tail) I2PC_WAIT_VM(0);
+      else if (epi_gap) wait_vm<12 + E_ALL>();
+      else I2PC_WAIT_VM(12);
+      I2PC_LDS_BARRIER();
+      if (issue) fill(buf, 3, k_ahead);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a, acc[i][2 + j], 0, 0, 0);
+        }
+      // ---------------- phase 3: (mp 1, np 1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) af[i][s] = read_frag(buf, 1, wm * 64 + i * 16 + frow, s);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      I2PC_LDS_BARRIER();                                   // (phase 4 reads nothing new)
+      if (issue) fill(buf, 1, k_ahead);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a, acc[4 + i][2 + j], 0, 0, 0);
+        }
+      // ---------------- phase 4: (mp 1, np 0): the next K-tile's A-q0 / B-q0 must land
+      if (tail) I2PC_WAIT_VM(0);
+      else if (epi_gap && kt == 0) wait_vm<12 + E_ALL>();
+      else I2PC_WAIT_VM(12);
+      I2PC_LDS_BARRIER();
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a, acc[4 + i][j], 0, 0, 0);
+        }
+      ++g;
+    }
+    // ---- epilogue of tile (m0, n0): register-direct, counted; bias straight from memory
+    const float* bias = p.bias ? p.bias + n0 + wn * 64 : reinterpret_cast<const float*>(g_zero);
+    epilogue_p<RM, RN, EPI, false>(p, acc, m0 + wm * 128, n0 + wn * 64, bias, c_rs, r_rs, r2_rs, c_rs);
+    if (!has_next) break;
+    t = t_next;
+    m0 = nm0;
+    n0 = nn0;
+    after_epi = true;
+  }
+}
+
 #undef I2PC_WAIT_VM
 #undef I2PC_LDS_BARRIER
 
@@ -1090,6 +1326,31 @@ static void launch_p(const Args& p, hipStream_t s) {
   }
   const int tiles = q.tiles_m * q.tiles_n;
   const int grid = std::min(tiles, num_cus());
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
+}
+
+template <bool CONV, bool RELU_A, int EPI>
+static void launch_q(const Args& p, hipStream_t s) {
+  Args q = p;
+  if (!CONV) {
+    q.A = p.A + (int64_t)p.a_o * p.lda;
+    q.a_o = 0;
+    q.a_bytes = (uint32_t)((int64_t)p.M * p.lda * 2);
+  } else {
+    q.a_bytes = (uint32_t)((int64_t)p.cb * p.ch * p.cw * p.cc * 2);
+  }
+  q.w_bytes = (uint32_t)((int64_t)p.N * p.ldw * 2);
+  q.tiles_m = (p.M + 255) / 256;
+  q.tiles_n = p.N / 256;
+  q.group_m = group_m_for(q.tiles_m);
+  const int smem = 2 * 4 * 128 * 128;
+  auto kern = pers::k_gemm_q<CONV, RELU_A, EPI>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int grid = std::min(q.tiles_m * q.tiles_n, num_cus());
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
 }
 
@@ -1183,9 +1444,26 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   return pl;
 }
 
+// I2PC_GEMM_Q=1: the quarter-pipelined engine (k_gemm_q) replaces k_gemm_p wherever the
+// persistent engine was chosen (K >= 128)
+static const int g_quarter = [] { const char* e = getenv("I2PC_GEMM_Q"); return e ? atoi(e) : 0; }();
+
 template <bool CONV, bool RELU_A>
 static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
   using namespace pers;
+  if (g_quarter && p.K >= 128) {
+    if constexpr (!CONV && !RELU_A) {
+      if (pl.epi == EPI_PLAIN) { launch_q<false, false, EPI_PLAIN>(p, s); return check_launch("gemm_q"); }
+      if (pl.epi == EPI_RESF32) { launch_q<false, false, EPI_RESF32>(p, s); return check_launch("gemm_q"); }
+    } else if constexpr (CONV && !RELU_A) {
+      if (pl.epi == EPI_PLAIN) { launch_q<true, false, EPI_PLAIN>(p, s); return check_launch("gemm_q"); }
+      if (pl.epi == EPI_RESBF16) { launch_q<true, false, EPI_RESBF16>(p, s); return check_launch("gemm_q"); }
+      if (pl.epi == EPI_RES2) { launch_q<true, false, EPI_RES2>(p, s); return check_launch("gemm_q"); }
+    } else if constexpr (CONV && RELU_A) {
+      launch_q<true, true, EPI_PLAIN>(p, s);
+      return check_launch("gemm_q");
+    }
+  }
   if constexpr (!CONV && !RELU_A) {
     if (pl.epi == EPI_PLAIN) launch_p<256, false, false, EPI_PLAIN>(p, s);
     else if (pl.epi == EPI_RESF32) launch_p<256, false, false, EPI_RESF32>(p, s);
@@ -1223,7 +1501,8 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu) {
   const char* r = relu ? "true" : "false";
   if (pl.kind == 1) {
     static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT"};
-    snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
+    if (g_quarter && pl.epi != pers::EPI_CT) snprintf(buf, sizeof buf, "k_gemm_q<%s, %s, %s>", c, r, epis[pl.epi]);
+    else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
   } else if (pl.kind == 0) {
     const int wm = pl.bn == 32 ? 4 : 2, wn = pl.bn == 256 ? 4 : pl.bn == 32 ? 1 : 2;
     snprintf(buf, sizeof buf, "k_gemm<%d, %d, %d, %d, %d, %s, %s>", pl.bm, pl.bn, wm, wn, pl.epi, c, r);
