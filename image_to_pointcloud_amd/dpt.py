@@ -215,9 +215,12 @@ class DPTDepthModel:
         self.w_pe = bf(pe.reshape(D, 3 * P * P))
         self.b_pe = f32(sd["dpt.embeddings.patch_embeddings.projection.bias"])
         pos = sd["dpt.embeddings.position_embeddings"][0]
-        if pos.shape[0] != g * g + 1:
-            raise NotImplementedError("position-embedding interpolation to another grid is not implemented")
-        self.pos_tok = f32(pos[1:])
+        g0 = int(round(math.sqrt(pos.shape[0] - 1)))
+        if g0 * g0 != pos.shape[0] - 1:
+            raise ValueError(f"position table of {pos.shape[0]} rows is not a square grid + CLS")
+        self._pos_grid = f32(pos[1:]).view(g0, g0, D)
+        self._pos_tables = {}
+        self.pos_tok = self._pos_table(g, g)
         self.pos0 = f32(pos[0])
         self.cls = f32(sd["dpt.embeddings.cls_token"].reshape(D))
         self.layers = []
@@ -268,33 +271,53 @@ class DPTDepthModel:
         self.w_h4 = f32(sd["head.head.4.weight"].reshape(32))
         self.b_h4 = float(sd["head.head.4.bias"].reshape(()).item())
 
+    def _pos_table(self, gh: int, gw: int):
+        """Position rows for a gh x gw patch grid: DPTViTEmbeddings._resize_pos_embed
+        (modeling_dpt.py:202-214, bilinear, align_corners=False).  A one-time parameter
+        transform per grid size, done with torch on the device and cached."""
+        key = (gh, gw)
+        if key not in self._pos_tables:
+            import torch
+            g0 = self._pos_grid.shape[0]
+            if (gh, gw) == (g0, g0):
+                t = self._pos_grid.reshape(g0 * g0, -1).contiguous()
+            else:
+                grid = self._pos_grid.permute(2, 0, 1).unsqueeze(0)
+                t = torch.nn.functional.interpolate(grid, size=(gh, gw), mode="bilinear")
+                t = t[0].permute(1, 2, 0).reshape(gh * gw, -1).contiguous()
+            self._pos_tables[key] = t
+        return self._pos_tables[key]
+
     # ------------------------------------------------------------------ buffers
-    def buffers(self, B: int) -> dict:
+    def buffers(self, B: int, gh: int = None, gw: int = None) -> dict:
         import torch
-        if B in self._bufs:
-            return self._bufs[B]
         s, dev = self.spec, self.device
-        D, g = s.hidden, s.grid
-        T = g * g + 1
+        gh, gw = gh or s.grid, gw or s.grid
+        if (B, gh, gw) in self._bufs:
+            return self._bufs[(B, gh, gw)]
+        D = s.hidden
+        T = gh * gw + 1
         M = B * T
         e = lambda shape, dt=torch.bfloat16: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
         b = dict(x=e((M, D), torch.float32), ln=e((M, D)), qkv=e((M, 3 * D)), att=e((M, D)), mlp=e((M, s.mlp)),
-                 hs=[e((M, D)) for _ in s.out_indices], rb=e((B, D), torch.float32), tok=e((B * g * g, D)))
-        self._bufs[B] = b
+                 hs=[e((M, D)) for _ in s.out_indices], rb=e((B, D), torch.float32), tok=e((B * gh * gw, D)))
+        self._bufs[(B, gh, gw)] = b
         return b
 
     # ------------------------------------------------------------------ forward
     def forward(self, patches, B: int, gh: int = None, gw: int = None):
-        """patches: bf16 [B * grid^2, 3*patch^2] (preprocess layout 'patches') -> depth fp32 [B, H', W']."""
-        if (gh or self.spec.grid, gw or self.spec.grid) != (self.spec.grid, self.spec.grid):
-            raise NotImplementedError("DPT runs on its square checkpoint grid (the Intel processors resize to 384x384)")
+        """patches: bf16 [B * gh * gw, 3*patch^2] (preprocess layout 'patches') -> depth fp32 [B, H', W'].
+        Any patch grid (the position table is interpolated as DPTViTEmbeddings does); the Intel
+        processors resize to the square checkpoint grid."""
         s = self.spec
-        D, g = s.hidden, s.grid
-        np_, T = g * g, g * g + 1
-        buf = self.buffers(B)
+        gh, gw = gh or s.grid, gw or s.grid
+        D = s.hidden
+        np_, T = gh * gw, gh * gw + 1
+        self._grid = (gh, gw)
+        buf = self.buffers(B, gh, gw)
         x = buf["x"]
         # embeddings: patch GEMM + bias + position table written into token rows 1..T-1; CLS row
-        ops.linear(patches, self.w_pe, bias=self.b_pe, table=self.pos_tok, table_rows=np_, out=x,
+        ops.linear(patches, self.w_pe, bias=self.b_pe, table=self._pos_table(gh, gw), table_rows=np_, out=x,
                    out_map=(np_, T, 1), rows=B * np_)
         ops.cls_pos(self.cls, self.pos0, x, B, T, D)
         scale = 1.0 / math.sqrt(D // s.heads)
@@ -325,13 +348,14 @@ class DPTDepthModel:
 
     def _reassemble(self, j, hs, B, buf):
         s, st = self.spec, self.stages[j]
-        D, g = s.hidden, s.grid
-        np_, T = g * g, g * g + 1
+        D = s.hidden
+        gh, gw = getattr(self, "_grid", (s.grid, s.grid))
+        np_, T = gh * gw, gh * gw + 1
         rb = ops.linear(hs, st["w_cls"], bias=st["b_ro"], rows=B, a_map=(1, T, 0), out=buf["rb"])
         tok = ops.linear(hs, st["w_tok"], rows=B * np_, a_map=(np_, T, 1), row_bias=rb, row_bias_group=np_,
                          act="gelu", out=buf["tok"])
         c = st["c"]
-        proj = ops.linear(tok, st["w_proj"], bias=st["b_proj"]).view(B, g, g, c)
+        proj = ops.linear(tok, st["w_proj"], bias=st["b_proj"]).view(B, gh, gw, c)
         fac = st["fac"]
         if fac > 1:
             r = ops.conv_transpose(proj, st["w_rs"], st["b_rs"], int(fac))
@@ -345,8 +369,8 @@ class DPTDepthModel:
         if hidden is None:
             h = feat
         else:
-            if tuple(hidden.shape) != tuple(feat.shape):
-                raise NotImplementedError("fusion residual resize (shape mismatch) is not implemented")
+            if tuple(hidden.shape) != tuple(feat.shape):   # odd grids: modeling_dpt.py:696-699
+                feat = ops.resize_bilinear(feat, hidden.shape[1], hidden.shape[2], align_corners=False)
             t = ops.conv2d(feat, fl["residual_layer1.convolution1.w"], bias=fl["residual_layer1.convolution1.b"],
                            relu_in=True, act="relu")
             h = ops.conv2d(t, fl["residual_layer1.convolution2.w"], bias=fl["residual_layer1.convolution2.b"],

@@ -182,3 +182,30 @@ def test_c3_dpt_large_512_batch():
         ep, ec = oref.depth_to_point_cloud(imgs[i], depth[i], density="high", loop=False)
         assert pb.xyz[i].cpu().numpy().tobytes() == ep.tobytes(), i
         assert pb.rgb[i].cpu().numpy().astype(np.float32).tobytes() == ec.tobytes(), i
+
+
+def test_dpt_any_grid_pos_interpolation_and_fusion_resize():
+    """DPT on an odd patch grid (112 x 112 network input -> 7 x 7 patches against the checkpoint's
+    8 x 8): the position table is interpolated (DPTViTEmbeddings._resize_pos_embed) and the
+    fusion stage resizes the residual feature to the fused map (4 -> 8 vs 7,
+    modeling_dpt.py:696-699).  (transformers' ViT-DPT reshapes tokens to a square grid, so a
+    non-square grid, which this module also runs, has no reference to compare with.)"""
+    from image_to_pointcloud_amd.dpt import DPT_TINY, DPTDepthModel, synthetic_state_dict
+    from image_to_pointcloud_amd.preprocess import Preprocessor, ProcessorSpec
+    spec, B = DPT_TINY, 2
+    dev = torch.device("cuda")
+    sd = synthetic_state_dict(spec, seed=0)
+    ours = DPTDepthModel(spec, sd, dev)
+    ref = _hf_model(spec, sd, dev)
+    imgs = _images(B, 100, 150, 9)
+    prep = Preprocessor(100, 150, ProcessorSpec(size=(112, 112)), patch=16)
+    timgs = torch.from_numpy(imgs).to(dev)
+    pix = prep(timgs, layout="nchw")
+    depth = ours(prep(timgs, layout="patches"), B, 7, 7)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        exp = ref(pixel_values=pix).predicted_depth.float()
+    assert depth.shape == exp.shape, (depth.shape, exp.shape)
+    rel = ((depth - exp).norm() / exp.norm()).item()
+    _report("dpt-tiny 7x7 grid", rel_l2=rel)
+    assert rel <= 1e-2, rel
