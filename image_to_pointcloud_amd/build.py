@@ -35,6 +35,7 @@ SOURCES = [
     "area.hip",
     "fp8.hip",
     "bit.hip",
+    "comm.cpp",
     "writers.cpp",
 ]
 HEADERS = ["common.h", "mx.h", "../../include/i2pc.h"]
@@ -78,7 +79,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if (force or not os.path.exists(LIB)
             or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs)):
-        cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lrccl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

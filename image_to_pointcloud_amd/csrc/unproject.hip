@@ -285,8 +285,8 @@ __device__ __forceinline__ float sample_rows(const Geo& g, const float* rows, in
 template <int LEVEL, int PASS>
 __global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32_t* hist, int B, Sweep sw) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
-  uint32_t* sh = smem_u;                                        // [kSlots * kBins]
-  float* rows = reinterpret_cast<float*>(smem_u + kSlots * kBins);
+  uint32_t* sh = smem_u;                                        // [slots * kBins]
+  float* rows = reinterpret_cast<float*>(smem_u + (LEVEL == 0 ? 1 : kSlots) * kBins);
   __shared__ uint32_t red[4][4];
   int b, rb;
   map_rows(blockIdx.x, B, sw.nrb, b, rb);
@@ -1132,10 +1132,12 @@ static int exchange(const Exchange* x, uint32_t* hist, SelState* st, int B, hipS
 template <int PASS>
 static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, const Sweep& sw, hipStream_t s,
                          const Exchange* x = nullptr) {
+  // level 0 histograms one slot (8 KB of LDS); levels 1-2 up to kSlots target prefixes
+  const size_t lds0 = sizeof(uint32_t) * kBins + sweep_lds(sw, g.dw);
   const size_t lds = sizeof(uint32_t) * kSlots * kBins + sweep_lds(sw, g.dw);
   const dim3 grid(B * sw.nrb), block(kBlock);
   int rc;
-  hipLaunchKernelGGL((k_sel_hist<0, PASS>), grid, block, lds, s, g, st, hist, B, sw);
+  hipLaunchKernelGGL((k_sel_hist<0, PASS>), grid, block, lds0, s, g, st, hist, B, sw);
   if ((rc = exchange<0>(x, hist, st, B, s))) return rc;
   hipLaunchKernelGGL((k_sel_resolve<0, PASS>), dim3(B), block, 0, s, st, hist, B);
   hipLaunchKernelGGL((k_sel_hist<1, PASS>), grid, block, lds, s, g, st, hist, B, sw);
@@ -1224,8 +1226,10 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
-  // selection sweeps: ~8 output rows per workgroup for 1024-wide images
-  const int sel_rows = std::max(1, std::min(16, (8 * 1024 + img_w - 1) / img_w));
+  // selection sweeps: I2PC_SEL_PTS points per workgroup (default 8 rows of a 1024-wide image)
+  // (measured r02, B = 32 x 1024^2: 4096 pts 476 us, 8192 462 us, 16384 505 us, 32768 598 us per call)
+  static const int sel_pts = [] { const char* e = getenv("I2PC_SEL_PTS"); return e ? atoi(e) : 8192; }();
+  const int sel_rows = std::max(1, std::min(64, (sel_pts + img_w - 1) / img_w));
   const Sweep ssel = plan_sweep(img_h, 1, dep_h, dep_w, img_h, g.same != 0, sel_rows, row0, row1);
   Exchange xb = xch ? *xch : Exchange{nullptr, nullptr, nullptr};
   xb.ex = reinterpret_cast<int64_t*>(ws + L.ex);

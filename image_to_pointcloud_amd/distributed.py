@@ -131,3 +131,48 @@ def reduce_bbox(bbox, group=None):
     out[0::2] = mins
     out[1::2] = maxs
     return out
+
+
+class RcclComm:
+    """An RCCL communicator owned by libi2pc.so (i2pc_comm_create) for the device-side band
+    exchange of the tile-parallel panorama mode (geometry.unproject_band(comm=...)).
+
+    Rank 0 draws the 128-byte unique id and torch.distributed ships it to the others (any
+    backend: it is a host object), or pass `unique_id` yourself (world 1 needs no process group).
+    The current HIP device must be this rank's GPU."""
+
+    def __init__(self, group=None, nranks=None, rank=None, unique_id: bytes = None):
+        import ctypes
+        from . import _lib
+        lib = _lib.load()
+        self._lib = lib
+        if nranks is None:
+            import torch.distributed as dist
+            nranks, rank = dist.get_world_size(group), dist.get_rank(group)
+            if unique_id is None:
+                obj = [self.unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0, group=group)
+                unique_id = obj[0]
+        elif unique_id is None:
+            if nranks != 1:
+                raise ValueError("nranks > 1 needs the unique id rank 0 drew (or a process group)")
+            unique_id = self.unique_id()
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
+        _lib.call("i2pc_comm_create", buf, int(nranks), int(rank or 0), ctypes.byref(h))
+        self.handle, self.nranks, self.rank = h, nranks, rank or 0
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        from . import _lib
+        buf = ctypes.create_string_buffer(128)
+        _lib.call("i2pc_comm_unique_id", buf, 128)
+        return buf.raw
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self._lib.i2pc_comm_destroy(self.handle)
+            self.handle = None
+
+    __del__ = close

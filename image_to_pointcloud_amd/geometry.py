@@ -218,6 +218,14 @@ def remove_statistical_outlier(xyz, rgb=None, nb_neighbors: int = 20, std_ratio:
 # ----------------------------------------------------------------- tile-parallel (C4)
 EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                ctypes.c_int, ctypes.c_void_p)
+_lib.register("i2pc_comm_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int])
+_lib.register("i2pc_comm_create", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_void_p)])
+_lib.register("i2pc_comm_destroy", None, [ctypes.c_void_p])
+_lib.register("i2pc_unproject_band_rccl", ctypes.c_int,
+              [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+               ctypes.c_int, ctypes.c_int, ctypes.POINTER(_lib.UnprojectParams), ctypes.c_void_p, ctypes.c_void_p,
+               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p])
 _lib.register("i2pc_unproject_band", ctypes.c_int,
               [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                ctypes.c_int, ctypes.c_int, ctypes.POINTER(_lib.UnprojectParams), ctypes.c_void_p, ctypes.c_void_p,
@@ -249,10 +257,15 @@ def band_rows(img_h: int, parts: int, step: int = 1) -> list:
     return out
 
 
-def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: int, exchange,
+def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: int, exchange=None,
                    density: str = "high", invert: bool = True, depth_scale: float = 10.0,
-                   fov: Optional[float] = None, workspace=None):
+                   fov: Optional[float] = None, workspace=None, comm=None, out=None):
     """This rank's band [row0, row1) of one image's unprojection (i2pc_unproject_band).
+
+    comm       : a distributed.RcclComm: the exchange runs on the device (RCCL all-reduces on
+                 the current stream, i2pc_unproject_band_rccl) -- no host callback, graph-capturable;
+                 otherwise `exchange` (host callable, below) is used
+    out        : optional (xyz, rgb, bbox, stats) device tensors to write (graph capture)
 
     depth      : torch.float32 [h, w] model-resolution depth of the WHOLE image (device)
     image_band : torch.uint8 [row1 - row0, img_w, C] the band's image rows (device)
@@ -278,12 +291,24 @@ def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: i
     wn = (img_w + step - 1) // step
     nb = ((row1 + step - 1) // step - row0 // step) * wn
     dev = depth.device
-    xyz = torch.empty((nb, 3), dtype=torch.float32, device=dev)
-    rgb = torch.empty((nb, 3), dtype=torch.uint8, device=dev)
-    bbox = torch.empty(6, dtype=torch.float64, device=dev)
-    stats = torch.empty(4, dtype=torch.float64, device=dev)
+    if out is not None:
+        xyz, rgb, bbox, stats = out
+    else:
+        xyz = torch.empty((nb, 3), dtype=torch.float32, device=dev)
+        rgb = torch.empty((nb, 3), dtype=torch.uint8, device=dev)
+        bbox = torch.empty(6, dtype=torch.float64, device=dev)
+        stats = torch.empty(4, dtype=torch.float64, device=dev)
     lib = _lib.load()
     ws = workspace if workspace is not None else _workspace(lib.i2pc_unproject_workspace_bytes(1, img_h, img_w, 0), dev)
+    if comm is not None:
+        p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
+                                 fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5)
+        _lib.call("i2pc_unproject_band_rccl", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
+                  img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),
+                  _ptr(ws), ws.numel(), comm.handle, _stream_handle())
+        return xyz, rgb, bbox, stats
+    if exchange is None:
+        raise ValueError("unproject_band needs an exchange callable or an RcclComm")
     errors = []
 
     def _cb(user, hist, words, counters, batch, stream):

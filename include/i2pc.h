@@ -108,6 +108,21 @@ int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, const uint8_t*
                         void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange, void* user,
                         void* stream);
 
+/* The same band call with the exchange done on the device by RCCL (three all-reduces on
+ * `stream` per selection sweep: histogram SUM, counters SUM / MIN / MAX), so the call is
+ * stream-ordered end to end and can be captured into a HIP graph.  `comm` comes from
+ * i2pc_comm_create on every rank with the id rank 0 got from i2pc_comm_unique_id
+ * (ncclGetUniqueId / ncclCommInitRank; 128 bytes, shipped by the caller); the current HIP
+ * device must be the rank's GPU. */
+typedef struct i2pc_comm i2pc_comm;
+int i2pc_comm_unique_id(void* out, int nbytes);
+int i2pc_comm_create(const void* unique_id, int nranks, int rank, i2pc_comm** comm);
+void i2pc_comm_destroy(i2pc_comm* comm);
+int i2pc_unproject_band_rccl(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
+                             int img_h, int img_w, int row0, int row1, const i2pc_unproject_params* params,
+                             float* xyz_band, uint8_t* rgb_band, double* bbox, double* stats, void* workspace,
+                             size_t workspace_bytes, i2pc_comm* comm, void* stream);
+
 /* Depth preview image (create_depth_preview, backend/app.py:124-172) for a batch of
  * model-resolution depth maps, before any resize: nanmedian fill, exact p2/p98 of
  * the map itself, clip/normalise/invert exactly as i2pc_unproject, then

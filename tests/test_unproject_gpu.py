@@ -285,3 +285,39 @@ def _band_check(dep, img, parts, density, depth_scale=12.0):
     glob[1::2] = bb[:, 1::2].max(0)
     assert _same_bits(glob, whole.bbox[0].cpu().numpy())
     return whole
+
+
+def test_band_rccl_exchange_single_rank_and_graph_capture():
+    """C4 with the device-side exchange: a one-rank RCCL communicator (i2pc_comm_create) drives
+    i2pc_unproject_band_rccl over the whole image -- bit-identical to i2pc_unproject -- and the
+    same call captured into a HIP graph replays to the same bytes (no host callback inside)."""
+    from image_to_pointcloud_amd.distributed import RcclComm
+    g = _geom()
+    dev = torch.device("cuda")
+    dep = _smooth_depth(96, 128, 81)
+    img = _rgb(600, 800, 82)
+    tdep, timg = torch.from_numpy(dep).to(dev), torch.from_numpy(img).to(dev)
+    whole = g.unproject_batch(tdep[None], timg[None], density="high")
+    comm = RcclComm(nranks=1, rank=0)
+    ws = torch.empty(g.workspace_bytes(1, 600, 800), dtype=torch.uint8, device=dev)
+    xyz, rgb, bbox, stats = g.unproject_band(tdep, timg, 600, 800, 0, 600, comm=comm, workspace=ws)
+    torch.cuda.synchronize()
+    assert _same_bits(xyz.cpu().numpy(), whole.xyz[0].cpu().numpy())
+    assert _same_bits(stats.cpu().numpy(), whole.stats[0].cpu().numpy())
+    out = (torch.zeros_like(xyz), torch.zeros_like(rgb), torch.zeros_like(bbox), torch.zeros_like(stats))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g.unproject_band(tdep, timg, 600, 800, 0, 600, comm=comm, workspace=ws, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        g.unproject_band(tdep, timg, 600, 800, 0, 600, comm=comm, workspace=ws, out=out)
+    for t in out:
+        t.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert _same_bits(out[0].cpu().numpy(), whole.xyz[0].cpu().numpy())
+    assert _same_bits(out[1].cpu().numpy(), whole.rgb[0].cpu().numpy())
+    comm.close()
