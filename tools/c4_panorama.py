@@ -5,9 +5,11 @@
 
 Each rank holds the model-resolution depth (518 x 1036, the Depth-Anything processor's
 keep-aspect size for 2:1; synthetic smooth field + a NaN) and ONLY its band of
-the image rows; i2pc_unproject_band runs the exact global p2/p98 through three histogram
-all-reduces per selection pass (RCCL when every rank has its own GPU, gloo when ranks share
-one), then unprojects its band.  Rank 0 prints one JSON line (points/s over the job, max
+the image rows; the band call runs the exact global p2/p98 through three histogram
+all-reduces per selection pass, then unprojects its band.  With one GPU per rank the
+exchange is device-side (i2pc_unproject_band_rccl on an RCCL communicator of libi2pc.so,
+and --graph captures each rank's whole band call into a HIP graph); when ranks share a GPU
+it falls back to the host-callback exchange over gloo (correctness runs only).  Rank 0 prints one JSON line (points/s over the job, max
 over ranks), and --check compares every band bit-for-bit with the whole-image unprojection.
 """
 import argparse
@@ -33,6 +35,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--density", default="high")
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay each rank's band call as a HIP graph (RCCL mode)")
     a = ap.parse_args()
     rank, local, world = D.world()
     ngpu = torch.cuda.device_count()
@@ -57,16 +60,27 @@ def main():
     for y in range(r0, r1):
         band[y - r0] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
     timg = torch.from_numpy(band).to(dev)
-    ex = D.band_exchange() if world > 1 else (lambda hist, cnt: None)
+    comm = D.RcclComm() if world > 1 and backend == "nccl" else (D.RcclComm(nranks=1, rank=0) if world == 1 else None)
+    ex = D.band_exchange() if comm is None else None
+    ws = torch.empty(G.workspace_bytes(1, H, W), dtype=torch.uint8, device=dev)
     res = None
-    for _ in range(a.warmup):
-        res = G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density)
+
+    def run():
+        return G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density, comm=comm, workspace=ws, out=res)
+    for _ in range(max(1, a.warmup)):
+        res = run()
     torch.cuda.synchronize()
+    step_fn = run
+    if a.graph and comm is not None:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            run()
+        step_fn = graph.replay
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        res = G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density)
+        step_fn()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -91,9 +105,13 @@ def main():
     if rank == 0:
         print(json.dumps({"metric": "Mpoints/sec tile-parallel unprojection of one panorama (C4)",
                           "value": round(n * a.steps / el / 1e6, 1), "unit": "Mpoints/s", "n_ranks": world,
-                          "backend": backend if world > 1 else None, "ms_per_image": round(el / a.steps * 1e3, 3),
+                          "backend": backend if world > 1 else None,
+                          "exchange": "RCCL on device (i2pc_unproject_band_rccl)" if comm is not None else "host callback",
+                          "hip_graph": bool(a.graph and comm is not None), "ms_per_image": round(el / a.steps * 1e3, 3),
                           "image": [H, W], "depth": [h, w], "density": a.density, "points": n,
                           "bit_exact_vs_whole_image": ok, "stats": res[3].tolist(), "bbox": bbox.tolist()}))
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 
