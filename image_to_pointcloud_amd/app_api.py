@@ -65,12 +65,14 @@ class ProcessingStatus(BaseModel):        # app.py:58-63
     results: Optional[Dict[str, Any]] = None
 
 
-# model id -> (spec factory, hub name the reference would fetch)
+# model id -> (spec factory, hub name the reference would fetch, network dtype)
 def _registry():
     from .depth_anything import DA_V2_SMALL
     from .dpt import DPT_LARGE
-    return {"depth-anything-v2": (DA_V2_SMALL, "depth-anything/Depth-Anything-V2-Small-hf"),
-            "dpt-large": (DPT_LARGE, "Intel/dpt-large")}
+    from .dpt_hybrid import DPT_HYBRID
+    return {"depth-anything-v2": (DA_V2_SMALL, "depth-anything/Depth-Anything-V2-Small-hf", "bf16"),
+            "dpt-large": (DPT_LARGE, "Intel/dpt-large", "bf16"),
+            "dpt-hybrid": (DPT_HYBRID, "Intel/dpt-hybrid-midas", "fp8")}
 
 
 def _load_weights(model_name: str, spec):
@@ -95,9 +97,10 @@ def load_model(model_name: str):
         reg = _registry()
         if model_name in reg:
             from .pipeline import default_processor, model_for
-            spec, _hub = reg[model_name]
+            spec, _hub, dtype = reg[model_name]
             dev = geometry.require_device()
-            model = {"processor": default_processor(spec), "model": model_for(spec, _load_weights(model_name, spec), dev),
+            model = {"processor": default_processor(spec),
+                     "model": model_for(spec, _load_weights(model_name, spec), dev, dtype=dtype),
                      "type": "depth", "spec": spec, "preprocessors": {}}
         elif model_name in ("triposr", "instantmesh"):
             model = {"type": model_name, "loaded": True}             # the reference's demo stubs (app.py:72-86)
@@ -121,12 +124,13 @@ def _depth_device(image_t, model_info):
     pre = cache.get((H, W))
     if pre is None:
         p = model_info["processor"]
-        if getattr(spec, "family", "dpt") == "dpt":
+        if getattr(spec, "family", "dpt") in ("dpt", "dpt-hybrid"):
             p = ProcessorSpec(size=(spec.image, spec.image), mean=p.mean, std=p.std)
         pre = cache[(H, W)] = Preprocessor(H, W, p, patch=spec.patch)
-    patches = pre(image_t[None], layout="patches")
+    net = model_info["model"]
+    patches = pre(image_t[None], layout=getattr(net, "input_layout", "patches"))
     gh, gw = pre.out_h // spec.patch, pre.out_w // spec.patch
-    return model_info["model"](patches, 1, gh, gw)[0]
+    return net(patches, 1, gh, gw)[0]
 
 
 def process_with_depth_anything(image: np.ndarray, model_info: dict) -> np.ndarray:

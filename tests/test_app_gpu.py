@@ -67,3 +67,27 @@ def test_load_model_and_depth_shapes():
         assert d.dtype == np.float32 and d.shape == exp and np.isfinite(d).all()
     with pytest.raises(Exception):
         app_api.load_model("no-such-model")
+
+
+def test_rest_job_with_dpt_hybrid_fp8(monkeypatch, tmp_path):
+    """The REST job on the C5 network: model=dpt-hybrid loads the MX fp8 DPT-Hybrid (BiT-R50 +
+    ViT-B/16) and the job completes with a coloured PLY of every point."""
+    from fastapi.testclient import TestClient
+    from PIL import Image
+    from image_to_pointcloud_amd import app_api, server
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setattr(app_api, "REFINE_POINT_CLOUD", False)
+    rng = np.random.Generator(np.random.PCG64(4))
+    img = rng.integers(0, 256, (240, 320, 3), dtype=np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray(img).save(buf, format="PNG")
+    c = TestClient(server.app)
+    r = c.post("/process", files={"file": ("img.png", buf.getvalue(), "image/png")},
+               params={"model": "dpt-hybrid", "point_density": "medium", "output_format": "ply"})
+    job = r.json()["job_id"]
+    st = c.get(f"/status/{job}").json()
+    assert st["status"] == "completed", st["message"]
+    assert app_api.models_cache["dpt-hybrid"]["model"].dtype == "fp8"
+    assert st["results"]["pointCloud"]["points"] == 120 * 160
+    ply = c.get(f"/download/{job}").content
+    assert b"element vertex 19200" in ply[:400] and b"property uchar red" in ply[:400]
