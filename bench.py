@@ -265,7 +265,11 @@ def main():
         pmc, pmc_src = _pmc_traffic(f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}"))
         dom = max(per.items(), key=lambda kv: kv[1]["t"])
         name, d = dom
-        if d["flops"] > 0:
+        # the bound of a kernel: whichever of its algorithmic FLOPs (at the dtype's dense MFMA peak)
+        # and algorithmic HBM bytes (at 8 TB/s) takes longer
+        t_mfma = d["flops"] / (_peak(name) * 1e12) if d["flops"] else 0.0
+        t_hbm = d["bytes"] / (HBM_PEAK_GBS * 1e9)
+        if d["flops"] > 0 and t_mfma >= t_hbm:
             ach = d["flops"] / d["n"] / (d["t"] / d["n"]) / 1e12
             pk = _peak(name)
             roofline = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": pk,
@@ -277,7 +281,11 @@ def main():
         else:
             ach = d["bytes"] / (d["t"]) / 1e9
             roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "launches": d["n"], "avg_us": round(d["t"] / d["n"] * 1e6, 2),
+                        "bytes_per_launch": d["bytes"] / d["n"], "share_of_step": round(d["t"] / (ms * 1e-3), 3)}
+            if d["flops"]:
+                roofline["tflops"] = round(d["flops"] / d["t"] / 1e12, 1)
             roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name)
         geo_bytes = B * (4.0 * pipe.pre.out_h * pipe.pre.out_w + 18.0 * pipe.points_per_image)
         roof_geo = {"kernel": "i2pc_unproject (select + unproject + bbox launches)", "bound": "hbm",
@@ -308,9 +316,14 @@ def main():
                                    "frac": round(t_peak / net_t, 4), "traffic": None,
                                    "ms": round(net_t * 1e3, 3),
                                    "fp8_flop_share": round(sum(v["flops"] for k, v in per.items()
-                                                               if k.startswith("k_gemm_f8")) / max(net_f, 1.0), 4)}
+                                                               if k.startswith("k_gemm_f8")) / max(net_f, 1.0), 4),
+                                   # attainment against each kernel's own bound (MFMA or HBM, whichever is slower)
+                                   "roofline_frac": round(sum(max(v["flops"] / (_peak(k) * 1e12),
+                                                                  v["bytes"] / (HBM_PEAK_GBS * 1e9))
+                                                              for k, v in per.items()) / net_t, 4)}
         kernels = {k: {"launches": v["n"], "ms": round(v["t"] * 1e3, 3),
-                       "tflops": round(v["flops"] / v["t"] / 1e12, 1) if v["flops"] else None}
+                       "tflops": round(v["flops"] / v["t"] / 1e12, 1) if v["flops"] else None,
+                       "gbs": round(v["bytes"] / v["t"] / 1e9, 1) if v["bytes"] else None}
                    for k, v in sorted(per.items(), key=lambda kv: -kv[1]["t"])}
 
     cpu = None

@@ -121,11 +121,26 @@ def set_gemm_engine(mode: int) -> None:
     _lib.call("i2pc_gemm_set_engine", int(mode))
 
 
+def gemm_bytes(d: GemmDesc, esz: float = 2.0, c_esz: float = None) -> float:
+    """Algorithmic HBM bytes of one GEMM / implicit-GEMM conv: A read once (a conv reads its
+    input map once), W once, C written once, residuals read once (scales of fp8 operands add
+    1/32 per element)."""
+    M, N, K = d.m, d.n, d.k
+    a = (d.conv_batch * d.conv_h * d.conv_w * d.conv_c) if d.conv else M * K
+    c_esz = (4.0 if d.c_f32 else 2.0) if c_esz is None else c_esz
+    b = a * esz + N * K * esz + M * N * c_esz
+    if d.res:
+        b += M * N * (4.0 if d.res_f32 else 2.0)
+    if d.res2:
+        b += M * N * 2.0
+    return b
+
+
 def gemm(desc: GemmDesc) -> None:
     if profile is None:
         _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
         return
-    with _Timed(gemm_kernel_label(desc), 2.0 * desc.m * desc.n * desc.k):
+    with _Timed(gemm_kernel_label(desc), 2.0 * desc.m * desc.n * desc.k, gemm_bytes(desc)):
         _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
 
 
@@ -233,7 +248,7 @@ def attention(qkv, batch, tokens, heads, scale, out=None):
     D = heads * 64
     if out is None:
         out = torch.empty((batch * tokens, D), dtype=torch.bfloat16, device=qkv.device)
-    with _Timed("k_attention", 4.0 * batch * heads * tokens * tokens * 64):
+    with _Timed("k_attention", 4.0 * batch * heads * tokens * tokens * 64, 2.0 * 4 * batch * tokens * D):
         _lib.call("i2pc_attention", _p(qkv), batch, tokens, heads, float(scale), _p(out), _stream())
     return out
 
@@ -426,7 +441,8 @@ def gemm_fp8(d: GemmFp8Desc) -> None:
         _lib.call("i2pc_gemm_fp8", ctypes.byref(d), _stream())
         return
     label = _lib.load().i2pc_gemm_fp8_kernel_name(ctypes.byref(d)).decode()
-    with _Timed(label, 2.0 * d.g.m * d.g.n * d.g.k):
+    nbytes = gemm_bytes(d.g, esz=1.0 + 1.0 / 32, c_esz=(1.0 + 1.0 / 32) if d.c_fp8 else None)
+    with _Timed(label, 2.0 * d.g.m * d.g.n * d.g.k, nbytes):
         _lib.call("i2pc_gemm_fp8", ctypes.byref(d), _stream())
 
 
