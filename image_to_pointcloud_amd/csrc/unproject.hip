@@ -4,14 +4,17 @@
 // generate_gis_metadata (app.py:393-400) for a whole batch of images.
 //
 // Pipeline per call (all stream-ordered, graph-capturable, fixed launch list):
-//   k_init            per-image selection state + cv2 INTER_LINEAR tap tables
-//   k_sel_hist/resolve x3 levels (pass 0)   exact order statistics of the
-//                     full-resolution depth (recomputed on the fly from the
-//                     model-resolution map, which stays L2-resident): the
-//                     p2/p98 ranks of np.percentile (app.py:197) -- or, if the
-//                     map holds NaN/Inf, the ranks of np.nanmedian (app.py:195)
-//   k_sel_hist/resolve x3 levels (pass 1)   only when a nanmedian fill was
-//                     needed: p2/p98 of the sanitised map (no-op launches otherwise)
+//   k_prepare         per-image selection state, cv2 INTER_LINEAR tap tables,
+//                     zeroed histograms, model-map key range partials
+//   k_model_hist / k_window   the model map's level-0 histogram -> windows around
+//                     its p2 / p98 whose full-resolution keys the first sweep compacts
+//   k_sweep/k_resolve x3 levels   exact order statistics of the full-resolution
+//                     depth (recomputed on the fly from the model-resolution map,
+//                     which stays L2-resident): the p2/p98 ranks of np.percentile
+//                     (app.py:197) by interval narrowing -- usually a histogram
+//                     sweep, a compaction sweep and a no-op third level
+//   k_sel_slow        maps holding NaN/Inf only (np.nanmedian fill, app.py:194-196):
+//                     the whole selection of such an image in one workgroup
 //   [k_norm_field, k_blur<rows>, k_blur<cols>]  only when smooth=True (app.py:209-214), any odd k
 //   k_unproject       normalise (fp64 / fp32 / constant branch exactly as
 //                     numpy evaluates app.py:198-206), pinhole back-projection in
@@ -19,9 +22,8 @@
 //                     (app.py:239-244), per-image bbox via wave reductions
 //   k_finalize        bbox / stats to float64
 //
-// Selection: 3-level radix select on order-preserving 32-bit float keys
-// (11 + 11 + 10 bits) with LDS histograms and wave-aggregated LDS atomics
-// (a smooth depth field puts most lanes of a wave in the same bin).
+// Selection: see the "selection" section (linear key bins over the model map's range,
+// run-length aggregated LDS histograms, candidate compaction).
 // Arithmetic is bit-faithful: no FMA contraction in this file.
 #include "common.h"
 
@@ -38,8 +40,19 @@ constexpr int kSlots = 4;
 constexpr int kBins = 2048;
 constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
+constexpr int kSlowBlock = 1024;
+constexpr int kRangeChunks = 32;
+constexpr int kLdsCand = 12288;  // candidate keys a resolve keeps in LDS
+constexpr int kWinKeys = 6144;   // expected full-resolution keys per level-0 window
+constexpr int kTileW = 1024;     // selection sweep column tile (4 columns per thread)
+constexpr int kSlotWords = kBins / 2;   // sweep LDS per slot: 2048 packed 16-bit counts or 1024 staged keys
+constexpr int kHrowBudget = 40 * 1024;   // LDS bytes of staged + horizontally interpolated model rows
 
-enum Phase : uint32_t { PH_INIT = 0, PH_PCT = 1, PH_MED = 2, PH_PCT2_INIT = 3, PH_PCT2 = 4, PH_DONE = 5 };
+// PH_INIT: level-0 sweep pending; PH_SEL: targets being narrowed; PH_SLOW: handed to
+// k_sel_slow (non-finite map); PH_DONE: p2 / p98 / mode final.
+enum Phase : uint32_t { PH_INIT = 0, PH_SEL = 1, PH_SLOW = 2, PH_DONE = 5 };
+enum SlotMode : uint32_t { SM_HIST = 0, SM_COMPACT = 1 };
+constexpr uint32_t kNoSlot = 0xffffffffu;
 
 struct Tap {
   int i0, i1;     // i1 < 0: single tap (cv2 HResizeLinear right border copies S[sx])
@@ -48,27 +61,32 @@ struct Tap {
 
 struct alignas(16) SelState {
   uint32_t phase;
-  uint32_t n;            // pixels per image
-  uint32_t nan_count;
+  uint32_t n;              // pixels per image
+  uint32_t nan_count;      // NaN / non-finite pixel counts (band exchange rows 0-1)
   uint32_t nonfinite_count;
-  uint32_t kmin, kmax;   // ordered keys of the non-NaN values of the current pass
-  uint32_t ntgt, nslot;
-  uint32_t rank[4];      // remaining rank of each target inside its prefix range
-  uint32_t prefix[4];
-  uint32_t slot[4];
-  uint32_t slot_prefix[4];
-  uint32_t med_ranks;    // 1 = odd count (one rank), 2 = even
+  uint32_t kmin, kmax;     // ordered keys: min / max over the image (level-0 sweep)
+  uint32_t rlo, rhi;       // finite key range of the model-resolution map (k_prepare / k_model_hist)
+  uint32_t ntgt, nslot, nwin, pad0;
+  uint32_t wbin[4];        // level-0 window w = level-0 bins [wbin[2w], wbin[2w+1]] (k_window)
+  uint32_t rank[4];        // remaining rank of target t inside its key interval
+  uint32_t tlo[4], thi[4]; // key interval holding target t (tlo == thi: resolved)
+  uint32_t tslot[4];       // slot target t is swept in next (kNoSlot: resolved)
+  uint32_t slo[4], shi[4]; // key interval of slot q
+  uint32_t smult[4];       // bin multiplier of slot q (0: one key per bin)
+  uint32_t smode[4];       // SM_HIST / SM_COMPACT
+  uint32_t ccount[4];      // candidate keys appended to slot q by a compaction sweep
+  uint32_t med_ranks;      // 1 = odd count (one rank), 2 = even
   uint32_t has_med;
   float med;
-  int32_t mode;          // 0: float64 branch, 1: float32 min/max branch, 2: constant
+  int32_t mode;            // 0: float64 branch, 1: float32 min/max branch, 2: constant
   uint32_t err;
-  uint32_t pad0;
+  uint32_t pad1;
   double p2, p98, den64;
-  float lo32, hi32, den32, pad1;
+  float lo32, hi32, den32, pad2;
   uint32_t bbox_key[6];
-  uint32_t pad2[2];
-  double rden64;         // RN(1 / den64): quotient seed for div_rn
-  double pad3;
+  uint32_t pad3[2];
+  double rden64;           // RN(1 / den64): quotient seed for div_rn
+  double pad4;
 };
 
 // Correctly rounded a / b from r = RN(1 / b) (Markstein's correction: q0 = RN(a r),
@@ -94,14 +112,24 @@ struct Geo {
 inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
-  size_t state, hist, xtab, ytab, ex, field, tmp, total;
+  size_t state, hist, cand, rpart, xtab, ytab, ex, field, tmp, total;
+  uint32_t cap;   // candidate keys per slot and image (compaction sweeps)
 };
+
+// Candidate capacity per target interval: a level-0 bin holds ~n / 2048 keys on average, so
+// n / 64 leaves a 32x margin for dense bins before the slower histogram level is taken.
+static uint32_t cand_cap(int64_t n) {
+  return (uint32_t)std::min<int64_t>(1 << 18, std::max<int64_t>(4096, n / 64)) / 256 * 256;   // DMA-able slots
+}
 
 static Layout layout(int B, int H, int W, int smooth) {
   Layout L{};
   size_t off = 0;
+  L.cap = cand_cap((int64_t)H * W);
   L.state = off; off = align_up(off + sizeof(SelState) * (size_t)B, 256);
   L.hist = off;  off = align_up(off + sizeof(uint32_t) * kSlots * kBins * (size_t)B, 256);
+  L.cand = off;  off = align_up(off + sizeof(uint32_t) * kSlots * (size_t)L.cap * B, 256);
+  L.rpart = off; off = align_up(off + sizeof(uint32_t) * 2 * kRangeChunks * (size_t)B, 256);
   L.xtab = off;  off = align_up(off + sizeof(Tap) * (size_t)W, 256);
   L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
   L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)B, 256);
@@ -160,21 +188,6 @@ __device__ __forceinline__ float sample(const Geo& g, int b, int v, int u) {
   return h0 * ty.w0 + h1 * ty.w1;
 }
 
-// Wave-aggregated LDS histogram add: lanes with equal bins are merged (up to 4
-// distinct bins per wave-instruction), the rest fall back to per-lane atomics.
-__device__ __forceinline__ void agg_add(uint32_t* h, int bin, bool active) {
-  const int lane = threadIdx.x & 63;
-  uint64_t pending = __ballot(active);
-  for (int it = 0; it < 4 && pending; ++it) {
-    const int leader = __ffsll((unsigned long long)pending) - 1;
-    const int lbin = __builtin_amdgcn_readlane(bin, leader);   // SALU broadcast, no LDS round trip
-    const uint64_t same = __ballot(active && bin == lbin) & pending;
-    if (lane == leader) atomicAdd(&h[lbin], (uint32_t)__popcll(same));
-    pending &= ~same;
-  }
-  if ((pending >> lane) & 1ull) atomicAdd(&h[bin], 1u);
-}
-
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
   for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
   return x;
@@ -204,49 +217,222 @@ __device__ Tap make_tap(int dx, int in, double scale) {
   return t;
 }
 
-// ---------------------------------------------------------------- kernels
+// ---------------------------------------------------------------- selection
+//
+// Exact p2 / p98 ranks of the full-resolution map (np.percentile, app.py:197) by narrowing
+// key intervals.  A key is the order-preserving 32-bit image of a float (f2key), so every
+// order statistic is a key, and a monotone map key -> bin turns counting into selection:
+//   level 0  bins every key linearly over the finite key range of the MODEL-resolution map
+//            (k_prepare; the bilinear resize stays within it up to rounding, keys outside
+//            clamp to the end bins) -> the bin of each target rank + its rank inside it;
+//   level 1  keys inside a target's bin interval are binned again (2048 finer bins), or --
+//            when the bin holds at most `cap` keys, the usual case -- appended to a
+//            candidate list, from which the resolve selects the exact key;
+//   level 2  the same again (a level-1 bin spans at most 1024 keys: one key per bin).
+// So a typical call sweeps the image twice (histogram, compaction).  The histogram adds are
+// run-length aggregated per thread: a thread walks down its columns, consecutive keys of a
+// smooth map fall in the same bin, and one LDS atomic carries the run.
+// Non-finite maps (the nanmedian fill of app.py:194-196) go to k_sel_slow, which redoes the
+// whole selection of such an image in one workgroup.
 
-__global__ void k_init(SelState* st, int B, int n, Tap* xt, Tap* yt, int dh, int dw, int H, int W, double sx,
-                       double sy) {
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid < B) {
+// Linear bins over a key interval starting at lo: bin = floor(d * kBins / span) for
+// d = key - lo, as umulhi(d, mult) with mult = floor(kBins * 2^32 / span) (mult = 0 when
+// span <= kBins: one key per bin).  Keys below lo go to bin 0, above the span to the last.
+__host__ __device__ inline uint32_t bin_mult(uint32_t lo, uint32_t hi) {
+  const uint64_t span = (uint64_t)hi - lo + 1;
+  return span <= (uint64_t)kBins ? 0u : (uint32_t)(((uint64_t)kBins << 32) / span);
+}
+__device__ __forceinline__ uint32_t bin_of(uint32_t key, uint32_t lo, uint32_t mult) {
+  const uint32_t d = key > lo ? key - lo : 0u;
+  const uint32_t bn = mult ? __umulhi(d, mult) : d;
+  return min(bn, (uint32_t)kBins - 1);
+}
+// key interval of bin bn (smallest offset of a bin: ceil(bn * 2^32 / mult)), clipped to [clo, chi]
+__device__ inline void bin_interval(uint32_t bn, uint32_t lo, uint32_t mult, uint32_t clo, uint32_t chi,
+                                    uint32_t& a, uint32_t& z) {
+  auto first = [&](uint64_t k) -> uint64_t { return mult ? ((k << 32) + mult - 1) / mult : k; };
+  uint64_t A = bn == 0 ? 0ull : (uint64_t)lo + first(bn);
+  uint64_t Z = bn == (uint32_t)kBins - 1 ? 0xffffffffull : (uint64_t)lo + first((uint64_t)bn + 1) - 1;
+  A = A < clo ? (uint64_t)clo : A;
+  Z = Z > chi ? (uint64_t)chi : Z;
+  a = (uint32_t)A;
+  z = (uint32_t)(Z < A ? A : Z);
+}
+// level-0 binning origin / multiplier from the model-map key range
+__device__ __forceinline__ void level0_bins(uint32_t rlo, uint32_t rhi, uint32_t& lo, uint32_t& mult) {
+  if (rlo <= rhi) { lo = rlo; mult = bin_mult(rlo, rhi); }
+  else { lo = 0; mult = bin_mult(0u, 0xffffffffu); }   // no finite model value: any monotone binning
+}
+
+__device__ __forceinline__ bool key_nonfinite(uint32_t k) { return k >= 0xff800000u || k <= 0x007fffffu; }
+
+// First launch of a call (kRangeChunks workgroups per image): per-image selection state,
+// cv2 tap tables, zeroed histograms, and the finite key range of each model-resolution map
+// as per-chunk partials (k_model_hist reduces them).
+__global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, int m, int n, SelState* st,
+                                                    uint32_t* hist, uint32_t* rpart, Tap* xt, Tap* yt, int dh, int dw,
+                                                    int H, int W, double sx, double sy) {
+  __shared__ uint32_t red[2][kBlock / 64];
+  const int gtid = blockIdx.x * kBlock + threadIdx.x;
+  const int nthr = gridDim.x * kBlock;
+  if (gtid < B) {
     SelState s{};
     s.phase = PH_INIT;
     s.n = (uint32_t)n;
     s.kmin = 0xffffffffu;
     s.kmax = 0u;
+    s.rlo = 0xffffffffu;
+    s.rhi = 0u;
     for (int i = 0; i < 6; i += 2) { s.bbox_key[i] = 0xffffffffu; s.bbox_key[i + 1] = 0u; }
     s.med = __uint_as_float(0x7fc00000u);
-    st[tid] = s;
+    st[gtid] = s;
   }
-  if (tid < W) {
-    Tap t = make_tap(tid, dw, sx);
+  for (int i = gtid; i < W; i += nthr) {
+    Tap t = make_tap(i, dw, sx);
     if (dw == 1) { t.i0 = 0; t.i1 = -1; t.w0 = 1.f; t.w1 = 0.f; }
-    xt[tid] = t;
+    xt[i] = t;
   }
-  if (tid < H) {
-    Tap t = make_tap(tid, dh, sy);
+  for (int i = gtid; i < H; i += nthr) {
+    Tap t = make_tap(i, dh, sy);
     // vertical pass always uses two rows: the second clamps to the last row
     if (t.i1 < 0) t.i1 = t.i0;
-    yt[tid] = t;
+    yt[i] = t;
+  }
+  for (size_t i = gtid; i < (size_t)B * kSlots * kBins; i += nthr) hist[i] = 0;
+  if (!depth) return;                     // (state only)
+  const int b = blockIdx.x % B, c = blockIdx.x / B;
+  const float* D = depth + (size_t)b * m;
+  uint32_t lo = 0xffffffffu, hi = 0u;
+  auto take = [&](float v) {
+    if (isfinite(v)) {
+      const uint32_t k = f2key(v);
+      lo = min(lo, k);
+      hi = max(hi, k);
+    }
+  };
+  if ((m & 3) == 0) {
+    const int m4 = m >> 2;
+    const int per = (m4 + kRangeChunks - 1) / kRangeChunks;
+    const int i1 = min(m4, (c + 1) * per);
+    const float4* D4 = reinterpret_cast<const float4*>(D);
+    for (int i = c * per + threadIdx.x; i < i1; i += kBlock) {
+      const float4 v = D4[i];
+      take(v.x); take(v.y); take(v.z); take(v.w);
+    }
+  } else {
+    const int per = (m + kRangeChunks - 1) / kRangeChunks;
+    const int i1 = min(m, (c + 1) * per);
+    for (int i = c * per + threadIdx.x; i < i1; i += kBlock) take(D[i]);
+  }
+  lo = wave_min_u32(lo);
+  hi = wave_max_u32(hi);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = lo; red[1][threadIdx.x >> 6] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) { lo = min(lo, red[0][w]); hi = max(hi, red[1][w]); }
+    rpart[((size_t)b * kRangeChunks + c) * 2] = lo;
+    rpart[((size_t)b * kRangeChunks + c) * 2 + 1] = hi;
   }
 }
 
-template <int PASS>
-__device__ __forceinline__ bool hist_gate(uint32_t phase, int level) {
-  if (PASS == 0) return level == 0 ? phase == PH_INIT : (phase == PH_PCT || phase == PH_MED);
-  return level == 0 ? phase == PH_PCT2_INIT : phase == PH_PCT2;
+// Level-0 histogram of each model-resolution map (finite values, the level-0 binning), into
+// histogram slot 3 (unused at level 0): the estimate k_window predicts the target bins from.
+__global__ __launch_bounds__(kBlock) void k_model_hist(const float* depth, int B, int m, SelState* st, uint32_t* hist,
+                                                       const uint32_t* rpart) {
+  __shared__ uint32_t lh[kBins];
+  __shared__ uint32_t rr[2];
+  const int b = blockIdx.x % B, c = blockIdx.x / B;
+  SelState* S = st + b;
+  for (int i = threadIdx.x; i < kBins; i += kBlock) lh[i] = 0;
+  if (threadIdx.x < 64) {     // the image's key range from k_prepare's partials
+    uint32_t lo = 0xffffffffu, hi = 0u;
+    if (threadIdx.x < kRangeChunks) {
+      lo = rpart[((size_t)b * kRangeChunks + threadIdx.x) * 2];
+      hi = rpart[((size_t)b * kRangeChunks + threadIdx.x) * 2 + 1];
+    }
+    lo = wave_min_u32(lo);
+    hi = wave_max_u32(hi);
+    if (threadIdx.x == 0) {
+      rr[0] = lo;
+      rr[1] = hi;
+      if (c == 0) { S->rlo = lo; S->rhi = hi; }
+    }
+  }
+  __syncthreads();
+  uint32_t lo, mult;
+  level0_bins(rr[0], rr[1], lo, mult);
+  // each thread bins a contiguous run of the chunk (neighbouring values share bins: one LDS
+  // atomic per run of equal bins), loads issued 8 at a time
+  const float* D = depth + (size_t)b * m;
+  const int per = (m + kRangeChunks - 1) / kRangeChunks;
+  const int i0 = c * per, i1 = min(m, i0 + per);
+  const int tper = (per + kBlock - 1) / kBlock;
+  const int t0 = i0 + threadIdx.x * tper, t1 = min(i1, t0 + tper);
+  int run = -1;
+  uint32_t cnt = 0;
+  for (int i = t0; i < t1; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = D[min(i + k, t1 - 1)];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int bn = (i + k < t1 && isfinite(v[k])) ? (int)bin_of(f2key(v[k]), lo, mult) : -1;
+      if (bn != run && run >= 0) atomicAdd(&lh[run], cnt);
+      cnt = (bn == run ? cnt : 0u) + 1u;
+      run = bn;
+    }
+  }
+  if (run >= 0) atomicAdd(&lh[run], cnt);
+  __syncthreads();
+  uint32_t* gh = hist + ((size_t)b * kSlots + 3) * kBins;
+  for (int i = threadIdx.x; i < kBins; i += kBlock)
+    if (lh[i]) atomicAdd(&gh[i], lh[i]);
+}
+
+// Block histogram in LDS as packed 16-bit counts (bin pairs share a word; a sweep workgroup
+// covers at most 32 * kTileW < 65536 pixels, so a half never carries into its neighbour).
+__device__ __forceinline__ void hist_add(uint32_t* sh, int bin, uint32_t cnt) {
+  atomicAdd(&sh[bin >> 1], cnt << ((bin & 1) << 4));
+}
+
+// Copy n floats global -> LDS (256 threads) with each thread's loads all in flight before its
+// first store; 16-byte accesses when the source is 16-byte aligned and n % 4 == 0.
+__device__ __forceinline__ void stage_floats(float* dst, const float* src, int n) {
+  if (((uintptr_t)src & 15) == 0 && (n & 3) == 0) {
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const int n4 = n >> 2;
+    for (int base = 0; base < n4; base += 4 * 256) {
+      float4 r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = s4[min(base + k * 256 + (int)threadIdx.x, n4 - 1)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (base + k * 256 + (int)threadIdx.x < n4) d4[base + k * 256 + threadIdx.x] = r[k];
+    }
+  } else {
+    for (int base = 0; base < n; base += 8 * 256) {
+      float r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = src[min(base + k * 256 + (int)threadIdx.x, n - 1)];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (base + k * 256 + (int)threadIdx.x < n) dst[base + k * 256 + threadIdx.x] = r[k];
+    }
+  }
 }
 
 // Row-blocked sweep geometry: a workgroup owns image b and output rows [v0, v1);
 // the model-resolution rows feeding them are staged once into LDS, every thread
-// owns 4 consecutive columns (+1024 per chunk), the row taps are wave-uniform.
+// owns 4 columns (+1024 per chunk), the row taps are wave-uniform.
 struct Sweep {
   int R;         // output rows per workgroup
   int nrb;       // row blocks per image
   int lds_rows;  // capacity of the LDS row window (0: sample from global)
   int row0;      // first output row swept (a band of the image in tile-parallel mode)
   int row_end;   // one past the last output row swept
+  int ntiles;    // selection sweeps: column tiles of kTileW per row block (others: 1)
+  int raw;       // selection sweeps: raw model rows staged in LDS before interpolation
 };
 
 __device__ __forceinline__ void map_rows(int bid, int B, int nrb, int& b, int& rb) { map_block(bid, B, nrb, b, rb); }
@@ -262,184 +448,262 @@ __device__ __forceinline__ int stage_rows(const Geo& g, int b, int v0, int v1, f
   return lo;
 }
 
-__device__ __forceinline__ float sample_rows(const Geo& g, const float* rows, int lo, bool use_lds, int b,
-                                             const Tap& ty, int v, int u) {
-  if (g.same) return g.depth[((size_t)b * g.dh + v) * g.dw + u];
-  if (!use_lds) return sample(g, b, v, u);
-  const Tap tx = g.xt[u];
-  const float* r0 = rows + (ty.i0 - lo) * g.dw;
-  const float* r1 = rows + (ty.i1 - lo) * g.dw;
-  float h0, h1;
-  if (tx.i1 < 0) {
-    h0 = r0[tx.i0];
-    h1 = r1[tx.i0];
-  } else {
-    h0 = r0[tx.i0] * tx.w0 + r0[tx.i1] * tx.w1;
-    h1 = r1[tx.i0] * tx.w0 + r1[tx.i1] * tx.w1;
-  }
-  return h0 * ty.w0 + h1 * ty.w1;
-}
-
-// (Materialising the keys in the first sweep and streaming them in the later ones
-// was measured slower: the sweeps are bound by the histogram, not the resize.)
-template <int LEVEL, int PASS>
-__global__ __launch_bounds__(kBlock) void k_sel_hist(Geo g, SelState* st, uint32_t* hist, int B, Sweep sw) {
+// One selection sweep over the full-resolution depth.  Workgroup = image b x output rows
+// [v0, v1) x a column tile of kTileW; the model rows feeding it are interpolated horizontally
+// once (cv2's first pass) into LDS, so a pixel costs two LDS reads and the vertical blend.
+// (For finite values the generic a0*w0 + a1*w1 equals cv2's single-tap copy at the right
+// border, whose weights are (1, 0); a non-finite tap only has to be detected here.)
+// Level 0 bins every key over the model map's key range; levels 1-2 match each key against
+// the slots' key intervals and either bin it (SM_HIST) or append it to the slot's candidate
+// list (SM_COMPACT, staged in the slot's LDS region).  Histogram adds are run-length
+// aggregated per thread down its columns.
+template <int LEVEL, bool SAME>
+__global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t* hist, uint32_t* cand, uint32_t cap,
+                                                  int B, Sweep sw) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
-  uint32_t* sh = smem_u;                                        // [slots * kBins]
-  float* rows = reinterpret_cast<float*>(smem_u + (LEVEL == 0 ? 1 : kSlots) * kBins);
-  __shared__ uint32_t red[4][4];
-  int b, rb;
-  map_rows(blockIdx.x, B, sw.nrb, b, rb);
+  uint32_t* sh = smem_u;                                        // [slots * kSlotWords]
+  // LDS: level 0 = [histogram | window 0 keys | window 1 keys], levels 1-2 = one region per slot
+  float* hrow = reinterpret_cast<float*>(smem_u + (LEVEL == 0 ? 3 : kSlots) * kSlotWords);   // [rows][kTileW]
+  __shared__ uint32_t red[3][kBlock / 64];
+  __shared__ uint32_t lcnt[kSlots], gbase[kSlots];
+  int b, chunk;
+  map_block(blockIdx.x, B, sw.nrb * sw.ntiles, b, chunk);
+  const int rb = chunk / sw.ntiles, c0 = (chunk - rb * sw.ntiles) * kTileW;
+  const int cw = min(kTileW, g.W - c0);
   SelState* S = st + b;
-  const uint32_t phase = S->phase;
-  if (!hist_gate<PASS>(phase, LEVEL)) return;
+  if (S->phase != (LEVEL == 0 ? PH_INIT : PH_SEL)) return;
 
-  const int nslot = LEVEL == 0 ? 1 : (int)S->nslot;
-  uint32_t sp[kSlots];
+  int nslot = 1;
+  uint32_t slo[kSlots], shi[kSlots], smult[kSlots];
+  bool scomp[kSlots];
+  // level 0: windows of level-0 bins whose keys are compacted (k_window); empty = [1, 0]
+  int wlo0 = 1, whi0 = 0, wlo1 = 1, whi1 = 0, nwin = 0;
+  if (LEVEL == 0) {
+    level0_bins(S->rlo, S->rhi, slo[0], smult[0]);
+    nwin = (int)S->nwin;
+    if (nwin > 0) { wlo0 = (int)S->wbin[0]; whi0 = (int)S->wbin[1]; }
+    if (nwin > 1) { wlo1 = (int)S->wbin[2]; whi1 = (int)S->wbin[3]; }
+  } else {
+    nslot = (int)S->nslot;
 #pragma unroll
-  for (int q = 0; q < kSlots; ++q) sp[q] = S->slot_prefix[q];
-  const bool sanitize = PASS == 1;
-  const float med = S->med;
-  constexpr int match_shift = LEVEL == 1 ? 21 : 10;
-  constexpr int bin_shift = LEVEL == 0 ? 21 : (LEVEL == 1 ? 10 : 0);
-  constexpr uint32_t bin_mask = LEVEL == 2 ? 1023u : 2047u;
-
+    for (int q = 0; q < kSlots; ++q) {
+      slo[q] = S->slo[q];
+      shi[q] = S->shi[q];
+      smult[q] = S->smult[q];
+      scomp[q] = S->smode[q] == SM_COMPACT;
+    }
+  }
   const int v0 = sw.row0 + rb * sw.R;
   const int v1 = min(sw.row_end, v0 + sw.R);
-  for (int i = threadIdx.x; i < nslot * kBins; i += kBlock) sh[i] = 0;
-  const int lo = stage_rows(g, b, v0, v1, rows, sw.lds_rows);
-  const bool use_lds = sw.lds_rows > 0;
-  __syncthreads();
-
-  uint32_t nan_c = 0, nonfin_c = 0, kmin = 0xffffffffu, kmax = 0u;
-  // thread columns u = cb + j*256 + tid: neighbouring lanes read neighbouring LDS words
-  for (int cb = 0; cb < g.W; cb += 4 * kBlock) {
+  for (int i = threadIdx.x; i < (LEVEL == 0 ? 1 : nslot) * kSlotWords; i += kBlock) sh[i] = 0;
+  if (threadIdx.x < kSlots) lcnt[threadIdx.x] = 0;
+  int lo = 0;
+  if (!SAME) {
+    // cv2's horizontal pass over the model rows of this block, into LDS: from raw rows staged
+    // in LDS when they fit (else straight from the L2-resident map)
+    lo = g.yt[v0].i0;
+    const int nr = g.yt[v1 - 1].i1 - lo + 1;
+    const float* D = g.depth + ((size_t)b * g.dh + lo) * g.dw;
+    float* raw = hrow + (size_t)sw.lds_rows * kTileW;
     Tap tx[4];
-    bool colok[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int u = cb + j * kBlock + threadIdx.x;
-      colok[j] = u < g.W;
-      tx[j] = g.xt[min(u, g.W - 1)];      // unconditional (clamped) load: no divergent waits
+    for (int j = 0; j < 4; ++j) tx[j] = g.xt[c0 + min(j * kBlock + (int)threadIdx.x, cw - 1)];
+    if (sw.raw) {
+      stage_floats(raw, D, nr * g.dw);
+      __syncthreads();
     }
-    for (int v = v0; v < v1; ++v) {
-      const Tap ty = g.same ? Tap{0, 0, 1.f, 0.f} : g.yt[v];
-      const float* r0 = use_lds ? rows + (ty.i0 - lo) * g.dw : g.depth + ((size_t)b * g.dh + ty.i0) * g.dw;
-      const float* r1 = use_lds ? rows + (ty.i1 - lo) * g.dw : g.depth + ((size_t)b * g.dh + ty.i1) * g.dw;
+    const float* src = sw.raw ? raw : D;
+    for (int k = 0; k < nr; ++k) {
+      const float* r = src + (size_t)k * g.dw;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int u = min(cb + j * kBlock + threadIdx.x, g.W - 1);
-        bool active = colok[j];
-        float val;
-        if (g.same) {
-          val = g.depth[((size_t)b * g.dh + v) * g.dw + u];
-        } else {
-          // single-tap columns (i1 < 0) use weights (1, 0) on a duplicated index: identical
-          // value except for Inf/NaN neighbours, so keep the exact expression via select
-          const int i1 = tx[j].i1 < 0 ? tx[j].i0 : tx[j].i1;
-          const float a0 = r0[tx[j].i0], a1 = r0[i1], c0 = r1[tx[j].i0], c1 = r1[i1];
-          const float h0 = tx[j].i1 < 0 ? a0 : a0 * tx[j].w0 + a1 * tx[j].w1;
-          const float h1 = tx[j].i1 < 0 ? c0 : c0 * tx[j].w0 + c1 * tx[j].w1;
-          val = h0 * ty.w0 + h1 * ty.w1;
-        }
-        if (sanitize && !isfinite(val)) val = med;
-        if (LEVEL == 0 && active && !isfinite(val)) ++nonfin_c;   // NaN and +-Inf
-        if (active && isnan(val)) { ++nan_c; active = false; }
-        const uint32_t key = f2key(val);
-        int bin = 0;
-        if (LEVEL == 0) {
-          if (active) { kmin = min(kmin, key); kmax = max(kmax, key); }
-          bin = (int)((key >> bin_shift) & bin_mask);
-        } else {
-          bool hit = false;
-#pragma unroll
-          for (int q = 0; q < kSlots; ++q) {
-            if (q < nslot && (key >> match_shift) == sp[q]) { hit = true; bin = q * kBins + (int)((key >> bin_shift) & bin_mask); }
-          }
-          active = active && hit;
-        }
-        agg_add(sh, bin, active);
+        const int u = j * kBlock + (int)threadIdx.x;
+        if (u < cw) hrow[k * kTileW + u] = r[tx[j].i0] * tx[j].w0 + r[tx[j].i1 < 0 ? tx[j].i0 : tx[j].i1] * tx[j].w1;
       }
     }
   }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const float* Dimg = g.depth + (size_t)b * g.dh * g.dw;
+  uint32_t nf = 0, kmin = 0xffffffffu, kmax = 0u;
+  int run_bin[4] = {-1, -1, -1, -1};
+  uint32_t run_cnt[4] = {0, 0, 0, 0};
+  Tap ty_next = SAME ? Tap{0, 0, 1.f, 0.f} : g.yt[v0];
+  for (int v = v0; v < v1; ++v) {
+    // every load unconditional (columns clamped into the tile), all issued before any use;
+    // the next row's taps are loaded a row ahead
+    float ha[4], hc[4];
+    const Tap ty = ty_next;
+    if (!SAME) ty_next = g.yt[min(v + 1, v1 - 1)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int uc = min(j * kBlock + (int)threadIdx.x, cw - 1);
+      if (SAME) {
+        ha[j] = Dimg[(size_t)v * g.dw + c0 + uc];
+      } else {
+        ha[j] = hrow[(ty.i0 - lo) * kTileW + uc];
+        hc[j] = hrow[(ty.i1 - lo) * kTileW + uc];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool active = j * kBlock + (int)threadIdx.x < cw;
+      const float val = SAME ? ha[j] : ha[j] * ty.w0 + hc[j] * ty.w1;
+      const uint32_t key = f2key(val);
+      int hb = -1;
+      int cq = -1;
+      if (LEVEL == 0) {
+        nf += (active && key_nonfinite(key)) ? 1u : 0u;
+        kmin = min(kmin, active ? key : 0xffffffffu);
+        kmax = max(kmax, active ? key : 0u);
+        hb = active ? (int)bin_of(key, slo[0], smult[0]) : -1;
+        cq = (hb >= wlo0 && hb <= whi0) ? 0 : ((hb >= wlo1 && hb <= whi1) ? 1 : -1);
+      } else {
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) {
+          const bool in = active && q < nslot && key >= slo[q] && key <= shi[q];
+          cq = (in && scomp[q]) ? q : cq;
+          hb = (in && !scomp[q]) ? q * kBins + (int)bin_of(key, slo[q], smult[q]) : hb;
+        }
+      }
+      if (hb != run_bin[j] && run_bin[j] >= 0) hist_add(sh, run_bin[j], run_cnt[j]);
+      run_cnt[j] = (hb == run_bin[j] ? run_cnt[j] : 0u) + 1u;
+      run_bin[j] = hb;
+      if ((LEVEL > 0 || nwin > 0) && __ballot(cq >= 0)) {
+        // a compaction slot's LDS region (unused by a histogram) stages its keys; one
+        // LDS atomic per slot and wave, global appends only past kSlotWords keys per block
+#pragma unroll
+        for (int q = 0; q < (LEVEL == 0 ? 2 : kSlots); ++q) {
+          const uint64_t m = __ballot(cq == q);
+          if (!m) continue;
+          const int leader = __ffsll((unsigned long long)m) - 1;
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(&lcnt[q], (uint32_t)__popcll(m));
+          base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+          if (cq == q) {
+            const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (pos < (uint32_t)kSlotWords) {
+              sh[(LEVEL == 0 ? q + 1 : q) * kSlotWords + pos] = key;
+            } else {
+              const uint32_t gpos = atomicAdd(&S->ccount[q], 1u);
+              if (gpos < cap) cand[((size_t)b * kSlots + q) * cap + gpos] = key;
+            }
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (run_bin[j] >= 0) hist_add(sh, run_bin[j], run_cnt[j]);
   if (LEVEL == 0) {
     const int wid = threadIdx.x >> 6;
-    nan_c = wave_sum_u32(nan_c);
-    nonfin_c = wave_sum_u32(nonfin_c);
+    nf = wave_sum_u32(nf);
     kmin = wave_min_u32(kmin);
     kmax = wave_max_u32(kmax);
-    if ((threadIdx.x & 63) == 0) { red[0][wid] = nan_c; red[1][wid] = nonfin_c; red[2][wid] = kmin; red[3][wid] = kmax; }
+    if (lane == 0) { red[0][wid] = nf; red[1][wid] = kmin; red[2][wid] = kmax; }
   }
   __syncthreads();
   if (LEVEL == 0 && threadIdx.x == 0) {
-    uint32_t a = 0, c = 0, mn = 0xffffffffu, mx = 0;
-    for (int w = 0; w < kBlock / 64; ++w) { a += red[0][w]; c += red[1][w]; mn = min(mn, red[2][w]); mx = max(mx, red[3][w]); }
-    if (a) atomicAdd(&S->nan_count, a);
+    uint32_t c = 0, mn = 0xffffffffu, mx = 0;
+    for (int w = 0; w < kBlock / 64; ++w) { c += red[0][w]; mn = min(mn, red[1][w]); mx = max(mx, red[2][w]); }
     if (c) atomicAdd(&S->nonfinite_count, c);
     if (mn != 0xffffffffu) atomicMin(&S->kmin, mn);
     if (mx) atomicMax(&S->kmax, mx);
   }
   uint32_t* gh = hist + (size_t)b * kSlots * kBins;
-  for (int i = threadIdx.x; i < nslot * kBins; i += kBlock) {
-    const uint32_t c = sh[i];
-    if (c) atomicAdd(&gh[i], c);
+  // compaction slots: q -> LDS region (level 0: the windows, regions 1-2), cand slot q
+  const int ncq = LEVEL == 0 ? nwin : nslot;
+  for (int q = 0; q < ncq; ++q) {
+    if (LEVEL > 0 && !scomp[q]) continue;
+    if (threadIdx.x == 0) {
+      const uint32_t nq = min(lcnt[q], (uint32_t)kSlotWords);
+      gbase[q] = nq ? atomicAdd(&S->ccount[q], nq) : 0u;
+    }
+  }
+  // histogram slots (packed 16-bit LDS counts -> global)
+  for (int q = 0; q < (LEVEL == 0 ? 1 : nslot); ++q) {
+    if (LEVEL > 0 && scomp[q]) continue;
+    for (int i = threadIdx.x; i < kSlotWords; i += kBlock) {
+      const uint32_t w = sh[q * kSlotWords + i];
+      if (w & 0xffffu) atomicAdd(&gh[q * kBins + 2 * i], w & 0xffffu);
+      if (w >> 16) atomicAdd(&gh[q * kBins + 2 * i + 1], w >> 16);
+    }
+  }
+  if (ncq > 0) {
+    __syncthreads();
+    for (int q = 0; q < ncq; ++q) {
+      if (LEVEL > 0 && !scomp[q]) continue;
+      const uint32_t nq = min(lcnt[q], (uint32_t)kSlotWords);
+      const uint32_t* src = sh + (LEVEL == 0 ? q + 1 : q) * kSlotWords;
+      uint32_t* dst = cand + ((size_t)b * kSlots + q) * cap;
+      for (uint32_t i = threadIdx.x; i < nq; i += kBlock)
+        if (gbase[q] + i < cap) dst[gbase[q] + i] = src[i];
+    }
   }
 }
 
-// Find, for one histogram of `nb` bins, the bin holding 0-based `rank`
-// (all threads call; result left in *out_bin / *out_rem by the owning thread).
-__device__ void find_bin(const uint32_t* h, int nb, uint32_t rank, uint32_t* sc, uint32_t* out_bin, uint32_t* out_rem) {
-  const int per = nb / kBlock;   // 8 or 4
-  const int t = threadIdx.x;
+// For one histogram of `nb` bins, the bins holding the 0-based ranks[0..nt) and the ranks
+// inside them (all NT threads call; results in out_bin / out_rem after the closing barrier).
+// Each thread owns nb / NT consecutive bins; the segment sums are scanned per wave with
+// lane shuffles and offset by the preceding waves' totals.
+template <int NT = kBlock>
+__device__ void find_bins(const uint32_t* h, int nb, const uint32_t* ranks, int nt, uint32_t* wsum,
+                          uint32_t* out_bin, uint32_t* out_rem) {
+  const int per = nb / NT;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t local = 0;
   for (int i = 0; i < per; ++i) local += h[t * per + i];
-  sc[t] = local;
-  __syncthreads();
-  // Hillis-Steele inclusive scan over 256 entries
-  for (int o = 1; o < kBlock; o <<= 1) {
-    uint32_t x = t >= o ? sc[t - o] : 0u;
-    __syncthreads();
-    sc[t] += x;
-    __syncthreads();
+  uint32_t x = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (lane >= o) x += y;
   }
-  const uint32_t incl = sc[t];
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int i = 0; i < w; ++i) off += wsum[i];
+  const uint32_t incl = x + off;
   const uint32_t excl = incl - local;
-  if (rank >= excl && rank < incl) {
-    uint32_t c = excl;
-    for (int i = 0; i < per; ++i) {
-      const uint32_t hv = h[t * per + i];
-      if (rank < c + hv) { *out_bin = (uint32_t)(t * per + i); *out_rem = rank - c; break; }
-      c += hv;
+  for (int k = 0; k < nt; ++k) {
+    const uint32_t rank = ranks[k];
+    if (rank >= excl && rank < incl) {
+      uint32_t c = excl;
+      for (int i = 0; i < per; ++i) {
+        const uint32_t hv = h[t * per + i];
+        if (rank < c + hv) { out_bin[k] = (uint32_t)(t * per + i); out_rem[k] = rank - c; break; }
+        c += hv;
+      }
     }
   }
   __syncthreads();
 }
 
-__device__ void pct_targets(SelState& s) {
-  const uint32_t n = s.n;
-  int k = 0;
+__device__ void pct_ranks(uint32_t n, uint32_t* rank) {
   const double qs[2] = {2.0 / 100.0, 98.0 / 100.0};   // q = [2,98] / float32(100) -> float64
   for (int j = 0; j < 2; ++j) {
     const double v = (double)(n - 1) * qs[j];
     uint32_t i0, i1;
     if (v >= (double)(n - 1)) { i0 = i1 = n - 1; }
     else { i0 = (uint32_t)floor(v); i1 = i0 + 1; }
-    s.rank[k++] = i0;
-    s.rank[k++] = i1;
+    rank[2 * j] = i0;
+    rank[2 * j + 1] = i1;
   }
-  s.ntgt = 4;
-  for (int i = 0; i < 4; ++i) s.prefix[i] = 0;
 }
 
-__device__ void finalize_pct(SelState& s) {
+// np.percentile's linear interpolation between the keys of ranks i0 / i1 (keys[4]), then
+// app.py:198-206's branch choice.
+__device__ void finalize_pct(SelState& s, const uint32_t* keys) {
   const uint32_t n = s.n;
   const double qs[2] = {2.0 / 100.0, 98.0 / 100.0};
   double r[2];
   for (int j = 0; j < 2; ++j) {
     const double v = (double)(n - 1) * qs[j];
     const double t = v - floor(v);
-    const float a = key2f(s.prefix[2 * j]);
-    const float bb = key2f(s.prefix[2 * j + 1]);
+    const float a = key2f(keys[2 * j]);
+    const float bb = key2f(keys[2 * j + 1]);
     const float diff = bb - a;
     r[j] = t >= 0.5 ? (double)bb - (double)diff * (1.0 - t) : (double)a + (double)diff * t;
   }
@@ -465,92 +729,453 @@ __device__ void finalize_pct(SelState& s) {
   s.phase = PH_DONE;
 }
 
-template <int LEVEL, int PASS>
-__global__ __launch_bounds__(kBlock) void k_sel_resolve(SelState* st, uint32_t* hist, int B) {
-  __shared__ uint32_t sc[kBlock];
-  __shared__ uint32_t res_bin[4], res_rem[4];
+// n 32-bit words global -> LDS by global_load_lds (16 B per lane, 1 KiB per wave-instruction,
+// every piece in flight at once; 256 threads).  src 16-byte aligned and readable up to the next
+// multiple of 256 words past n (the tail lanes copy that slack); dst holds that many words.
+// Ends with the wait and the barrier.
+__device__ __forceinline__ void dma_words(uint32_t* dst, const uint32_t* src, uint32_t n) {
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t base = w * 256; base < n; base += 4 * 256)
+    __builtin_amdgcn_global_load_lds(src + base + lane * 4, (__attribute__((address_space(3))) void*)(dst + base), 16,
+                                     0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// Candidate keys global -> LDS, 4 loads per thread in flight.
+__device__ __forceinline__ void load_keys(uint32_t* dst, const uint32_t* src, uint32_t c) {
+  for (uint32_t i0 = 0; i0 < c; i0 += 4 * kBlock) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) kk[k] = src[min(i0 + k * kBlock + threadIdx.x, c - 1)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k * kBlock + threadIdx.x < c) dst[i0 + k * kBlock + threadIdx.x] = kk[k];
+  }
+}
+
+// One narrowing round over candidate keys: a linear 2048-bin histogram of [lo, hi] and the
+// bins of ranks[0..nt) (block-wide; results in rbin / rrem).
+__device__ void cand_round(const uint32_t* keys, uint32_t c, uint32_t lo, uint32_t hi, const uint32_t* ranks, int nt,
+                           uint32_t* lh, uint32_t* wsum, uint32_t* rbin, uint32_t* rrem) {
+  const uint32_t mult = bin_mult(lo, hi);
+  for (int i = threadIdx.x; i < kBins; i += kBlock) lh[i] = 0;
+  if (threadIdx.x < nt) { rbin[threadIdx.x] = 0; rrem[threadIdx.x] = 0; }
+  __syncthreads();
+  for (uint32_t i0 = 0; i0 < c; i0 += 4 * kBlock) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) kk[k] = keys[min(i0 + k * kBlock + threadIdx.x, c - 1)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k * kBlock + threadIdx.x < c && kk[k] >= lo && kk[k] <= hi) atomicAdd(&lh[bin_of(kk[k], lo, mult)], 1u);
+  }
+  __syncthreads();
+  find_bins(lh, kBins, ranks, nt, wsum, rbin, rrem);
+}
+
+// Exact keys of ranks[0..nt) among one slot's candidate keys, all inside [lo, hi]: one round
+// for every target of the slot, then per target on its bin (at most 1024 keys wide after
+// level 0, so one key per bin) until its interval is one key wide.  Block-wide; out, tl, tz,
+// tr are shared arrays of nt entries.
+__device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint32_t hi, const uint32_t* ranks, int nt,
+                            uint32_t* out, uint32_t* lh, uint32_t* wsum, uint32_t* rbin, uint32_t* rrem,
+                            uint32_t* tl, uint32_t* tz, uint32_t* tr) {
+  cand_round(keys, c, lo, hi, ranks, nt, lh, wsum, rbin, rrem);
+  if (threadIdx.x == 0) {
+    const uint32_t mult = bin_mult(lo, hi);
+    for (int j = 0; j < nt; ++j) {
+      bin_interval(rbin[j], lo, mult, lo, hi, tl[j], tz[j]);
+      tr[j] = rrem[j];
+    }
+  }
+  __syncthreads();
+  for (int j = 0; j < nt; ++j) {
+    for (int it = 0; it < 4 && tl[j] < tz[j]; ++it) {
+      cand_round(keys, c, tl[j], tz[j], &tr[j], 1, lh, wsum, rbin, rrem);
+      if (threadIdx.x == 0) {
+        const uint32_t l = tl[j], z = tz[j];
+        bin_interval(rbin[0], l, bin_mult(l, z), l, z, tl[j], tz[j]);
+        tr[j] = rrem[0];
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[j] = tl[j];
+  }
+  __syncthreads();
+}
+
+// Speculative level-0 windows.  The full-resolution map is a bilinear resize of the model
+// map, so its p2 / p98 fall near the model map's: around the model map's bin of each quantile,
+// a run of level-0 bins expected to hold about kWinKeys full-resolution keys becomes a window
+// whose keys the level-0 sweep compacts.  When a target's bin lies inside a window (and the
+// window did not overflow), the level-0 resolve selects the exact key from those candidates
+// and the later levels are no-ops; otherwise they run as usual.  Consumes histogram slot 3.
+__global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist, uint32_t cap, int B, int enable) {
+  __shared__ uint32_t mh[kBins];
+  __shared__ uint32_t wsum[kBlock / 64], wb[4], tot;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  SelState* S = st + b;
+  uint32_t* gh = hist + ((size_t)b * kSlots + 3) * kBins;
+  uint32_t local = 0;
+  for (int i = threadIdx.x; i < kBins; i += kBlock) {
+    mh[i] = gh[i];
+    local += gh[i];
+    gh[i] = 0;
+  }
+  if (threadIdx.x == 0) tot = 0;
+  __syncthreads();
+  local = wave_sum_u32(local);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&tot, local);
+  __syncthreads();
+  const uint32_t mtot = tot;
+  if (!enable || mtot == 0) {
+    if (threadIdx.x == 0) S->nwin = 0;
+    return;
+  }
+  // window k = the bins whose cumulative model counts overlap [r_k - h, r_k + h]: model rank
+  // r_k of the quantile, h = half the candidate budget in model counts
+  const double scale = (double)S->n / (double)mtot;
+  const double h = 0.5 * (double)kWinKeys / scale;
+  const int per = kBins / kBlock;
+  uint32_t seg = 0;
+  for (int i = 0; i < per; ++i) seg += mh[threadIdx.x * per + i];
+  uint32_t x = seg;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  if (threadIdx.x < 4) wb[threadIdx.x] = (threadIdx.x & 1) ? 0u : (uint32_t)kBins;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int i = 0; i < wv; ++i) off += wsum[i];
+  double cum = (double)(x + off - seg);   // exclusive prefix of this thread's first bin
+  for (int k = 0; k < 2; ++k) {
+    const double r = floor((double)(mtot - 1) * (k ? 0.98 : 0.02));
+    double c = cum;
+    for (int i = 0; i < per; ++i) {
+      const int bn = threadIdx.x * per + i;
+      const double c1 = c + mh[bn];
+      if (c1 > r - h && c <= r + h) { atomicMin(&wb[2 * k], (uint32_t)bn); atomicMax(&wb[2 * k + 1], (uint32_t)bn); }
+      c = c1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t w[4] = {wb[0], wb[1], wb[2], wb[3]};
+    uint32_t nwin = 2;
+    if (w[2] <= w[1] + 1) {      // overlapping / touching windows: one window
+      w[0] = min(w[0], w[2]);
+      w[1] = max(w[1], w[3]);
+      nwin = 1;
+    }
+    for (int i = 0; i < 4; ++i) S->wbin[i] = w[i];
+    S->nwin = w[0] <= w[1] ? nwin : 0;
+  }
+}
+
+// One resolve per level (a workgroup per image): histogram slots -> the bin of each target
+// (its key interval narrows ~2048x), compaction slots -> the exact key; then the next
+// level's slots (compaction when the interval holds <= cap keys and `compact` is set).
+template <int LEVEL>
+__global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist, const uint32_t* cand, uint32_t cap,
+                                                    int B, int compact) {
+  __shared__ uint32_t lh[kBins];
+  __shared__ uint32_t ck[kLdsCand];
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t rbin[4], rrem[4], tcnt[4], qr[4], qk[4], tl[4], tz[4], tr[4], tbin[4];
   __shared__ SelState s;
   const int b = blockIdx.x;
   if (b >= B) return;
   if (threadIdx.x == 0) s = st[b];
   __syncthreads();
-  bool run;
-  if (PASS == 0) run = LEVEL == 0 ? s.phase == PH_INIT : (s.phase == PH_PCT || s.phase == PH_MED);
-  else run = LEVEL == 0 ? s.phase == PH_PCT2_INIT : s.phase == PH_PCT2;
-  if (!run) return;
+  if (s.phase != (LEVEL == 0 ? PH_INIT : PH_SEL)) return;
+  uint32_t* gh = hist + (size_t)b * kSlots * kBins;
+  uint32_t clo[kSlots], chi[kSlots];
+  if (LEVEL == 0) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (s.nonfinite_count != 0) {
+        s.phase = PH_SLOW;
+      } else {
+        pct_ranks(s.n, s.rank);
+        s.ntgt = 4;
+        s.nslot = 1;
+        level0_bins(s.rlo, s.rhi, s.slo[0], s.smult[0]);
+        s.smode[0] = SM_HIST;
+        for (int t = 0; t < 4; ++t) s.tslot[t] = 0;
+      }
+    }
+    __syncthreads();
+    if (s.phase == PH_SLOW) {
+      for (int i = threadIdx.x; i < kBins; i += kBlock) gh[i] = 0;
+      if (threadIdx.x == 0) st[b] = s;
+      return;
+    }
+    clo[0] = s.kmin;
+    chi[0] = s.kmax;
+  } else {
+    for (int q = 0; q < kSlots; ++q) { clo[q] = s.slo[q]; chi[q] = s.shi[q]; }
+    bool overflow = false;
+    for (int q = 0; q < (int)s.nslot; ++q) overflow |= s.smode[q] == SM_COMPACT && s.ccount[q] > cap;
+    if (overflow) {      // (cannot happen: the counts come from the previous histogram)
+      __syncthreads();
+      if (threadIdx.x == 0) { s.phase = PH_SLOW; st[b] = s; }
+      return;
+    }
+  }
+  for (int q = 0; q < (int)s.nslot; ++q) {
+    // the targets swept in slot q (every thread builds the same list)
+    int nq = 0, tq[4];
+    for (int t = 0; t < (int)s.ntgt; ++t)
+      if (s.tslot[t] == (uint32_t)q) tq[nq++] = t;
+    if (nq == 0) continue;
+    if (threadIdx.x < nq) qr[threadIdx.x] = s.rank[tq[threadIdx.x]];
+    if (threadIdx.x < 4) { rbin[threadIdx.x] = 0; rrem[threadIdx.x] = 0; }
+    __syncthreads();
+    if (s.smode[q] == SM_HIST) {
+      dma_words(lh, gh + q * kBins, kBins);     // the slot's histogram into LDS
+      find_bins(lh, kBins, qr, nq, wsum, rbin, rrem);
+      if (threadIdx.x == 0) {
+        for (int k = 0; k < nq; ++k) {
+          const int t = tq[k];
+          tcnt[t] = lh[rbin[k]];
+          tbin[t] = rbin[k];
+          bin_interval(rbin[k], s.slo[q], s.smult[q], clo[q], chi[q], s.tlo[t], s.thi[t]);
+          s.rank[t] = rrem[k];
+        }
+      }
+    } else {
+      const uint32_t c = s.ccount[q];
+      const uint32_t* keys = cand + ((size_t)b * kSlots + q) * cap;
+      if (c <= (uint32_t)kLdsCand) {
+        dma_words(ck, keys, c);
+        keys = ck;
+        __syncthreads();
+      }
+      cand_select(keys, c, s.slo[q], s.shi[q], qr, nq, qk, lh, wsum, rbin, rrem, tl, tz, tr);
+      if (threadIdx.x == 0) {
+        for (int k = 0; k < nq; ++k) {
+          const int t = tq[k];
+          s.tlo[t] = s.thi[t] = qk[k];
+          s.rank[t] = 0;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (LEVEL == 0 && s.nwin > 0) {
+    // targets whose level-0 bin lies in a k_window window: exact key from its candidates
+    for (int t = 0; t < 4; ++t) {
+      if (s.tlo[t] == s.thi[t]) continue;
+      int w = -1;
+      for (int k = 0; k < (int)s.nwin; ++k)
+        if (tbin[t] >= s.wbin[2 * k] && tbin[t] <= s.wbin[2 * k + 1]) w = k;
+      if (w < 0 || s.ccount[w] > cap) continue;
+      // the unresolved targets of the same bin go together
+      int ng = 0, tg[4];
+      for (int u = t; u < 4; ++u)
+        if (s.tlo[u] != s.thi[u] && tbin[u] == tbin[t]) tg[ng++] = u;
+      if (threadIdx.x < ng) qr[threadIdx.x] = s.rank[tg[threadIdx.x]];
+      const uint32_t c = s.ccount[w];
+      const uint32_t* keys = cand + ((size_t)b * kSlots + w) * cap;
+      if (c <= (uint32_t)kLdsCand) {
+        dma_words(ck, keys, c);
+        keys = ck;
+      }
+      __syncthreads();
+      cand_select(keys, c, s.tlo[t], s.thi[t], qr, ng, qk, lh, wsum, rbin, rrem, tl, tz, tr);
+      if (threadIdx.x == 0) {
+        for (int k = 0; k < ng; ++k) {
+          s.tlo[tg[k]] = s.thi[tg[k]] = qk[k];
+          s.rank[tg[k]] = 0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // consumed histograms -> zero for the next level
+  for (int i = threadIdx.x; i < (int)s.nslot * kBins; i += kBlock) gh[i] = 0;
+  if (threadIdx.x == 0) {
+    // unresolved targets -> next level's slots (targets with equal intervals share one)
+    int nslot = 0;
+    bool all = true;
+    for (int t = 0; t < (int)s.ntgt; ++t) {
+      if (s.tlo[t] == s.thi[t]) { s.tslot[t] = kNoSlot; continue; }
+      all = false;
+      int found = -1;
+      for (int q = 0; q < nslot; ++q)
+        if (s.slo[q] == s.tlo[t] && s.shi[q] == s.thi[t]) found = q;
+      if (found < 0) {
+        found = nslot++;
+        s.slo[found] = s.tlo[t];
+        s.shi[found] = s.thi[t];
+        s.smult[found] = bin_mult(s.tlo[t], s.thi[t]);
+        s.smode[found] = (compact && tcnt[t] <= cap) ? SM_COMPACT : SM_HIST;
+        s.ccount[found] = 0;
+      }
+      s.tslot[t] = (uint32_t)found;
+    }
+    s.nslot = (uint32_t)nslot;
+    if (all) {
+      finalize_pct(s, s.tlo);
+    } else {
+      s.phase = LEVEL == 2 ? PH_SLOW : PH_SEL;   // (a level-2 interval is one key wide: not reached)
+    }
+    st[b] = s;
+  }
+}
+
+// Non-finite maps (app.py:194-196: NaN / +-Inf filled with np.nanmedian, then the
+// percentiles of the filled map) and any image the fast levels did not finish: the whole
+// selection of one image in one workgroup, 3-level radix select on the key bits (11 + 11 +
+// 10) over every output row of the image (the model map is whole on every band, so this
+// needs no exchange in tile-parallel mode).  Rare path: one launch that returns at once
+// for every other image.
+__device__ void slow_radix(const Geo& g, int b, bool fill, float med, const uint32_t* rank_in, int ntgt,
+                           uint32_t* keys_out, uint32_t* sh, uint32_t* sc, uint32_t* rbin, uint32_t* rrem,
+                           uint32_t (*red)[kSlowBlock / 64], uint32_t* kmm) {
+  uint32_t prefix[4] = {0, 0, 0, 0}, rank[4] = {0, 0, 0, 0}, slot[4] = {0, 0, 0, 0}, sp[4] = {0, 0, 0, 0};
+  for (int t = 0; t < ntgt; ++t) rank[t] = rank_in[t];
+  const int n = g.H * g.W;
+  for (int level = 0; level < 3; ++level) {
+    int nslot = 1;
+    if (level > 0) {
+      nslot = 0;
+      for (int t = 0; t < ntgt; ++t) {
+        int found = -1;
+        for (int q = 0; q < nslot; ++q) if (sp[q] == prefix[t]) found = q;
+        if (found < 0) { found = nslot; sp[nslot++] = prefix[t]; }
+        slot[t] = (uint32_t)found;
+      }
+    }
+    const int match_shift = level == 1 ? 21 : 10;
+    const int bin_shift = level == 0 ? 21 : (level == 1 ? 10 : 0);
+    const uint32_t bin_mask = level == 2 ? 1023u : 2047u;
+    for (int i = threadIdx.x; i < nslot * kBins; i += kSlowBlock) sh[i] = 0;
+    __syncthreads();
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+    for (int p = threadIdx.x; p < n; p += kSlowBlock) {
+      const int v = p / g.W, u = p - v * g.W;
+      float val = sample(g, b, v, u);
+      if (fill && !isfinite(val)) val = med;
+      if (isnan(val)) continue;
+      const uint32_t key = f2key(val);
+      if (level == 0) {
+        kmin = min(kmin, key);
+        kmax = max(kmax, key);
+        atomicAdd(&sh[(key >> bin_shift) & bin_mask], 1u);
+      } else {
+        for (int q = 0; q < nslot; ++q)
+          if ((key >> match_shift) == sp[q]) atomicAdd(&sh[q * kBins + ((key >> bin_shift) & bin_mask)], 1u);
+      }
+    }
+    if (level == 0) {
+      kmin = wave_min_u32(kmin);
+      kmax = wave_max_u32(kmax);
+      if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = kmin; red[1][threadIdx.x >> 6] = kmax; }
+    }
+    __syncthreads();
+    if (level == 0 && threadIdx.x == 0) {
+      uint32_t mn = 0xffffffffu, mx = 0u;
+      for (int w = 0; w < kSlowBlock / 64; ++w) { mn = min(mn, red[0][w]); mx = max(mx, red[1][w]); }
+      kmm[0] = mn;
+      kmm[1] = mx;
+    }
+    const int nb = level == 2 ? 1024 : kBins;
+    const int bits = level == 2 ? 10 : 11;
+    for (int t = 0; t < ntgt; ++t) {
+      if (threadIdx.x == 0) { *rbin = 0; *rrem = 0; }
+      __syncthreads();
+      find_bins<kSlowBlock>(sh + slot[t] * kBins, nb, &rank[t], 1, sc, rbin, rrem);
+      prefix[t] = (prefix[t] << bits) | *rbin;
+      rank[t] = *rrem;
+      __syncthreads();
+    }
+  }
+  for (int t = 0; t < ntgt; ++t) keys_out[t] = prefix[t];
+}
+
+__global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, int B) {
+  __shared__ uint32_t sh[kSlots * kBins];
+  __shared__ uint32_t sc[kSlowBlock];
+  __shared__ uint32_t red[2][kSlowBlock / 64];
+  __shared__ uint32_t rbin, rrem, kmm[2], keys[4];
+  __shared__ SelState s;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  if (threadIdx.x == 0) s = st[b];
   __syncthreads();
-  if (threadIdx.x == 0 && LEVEL == 0) {
-    if (PASS == 0 && s.nonfinite_count != 0) {
-      const uint32_t m = s.n - s.nan_count;
-      if (m == 0) {                      // all-NaN: nanmedian is NaN, every value stays NaN
+  if (s.phase != PH_SLOW) return;
+  const int n = g.H * g.W;
+  uint32_t nan_c = 0, nf_c = 0;
+  for (int p = threadIdx.x; p < n; p += kSlowBlock) {
+    const int v = p / g.W, u = p - v * g.W;
+    const float val = sample(g, b, v, u);
+    nan_c += isnan(val) ? 1u : 0u;
+    nf_c += isfinite(val) ? 0u : 1u;
+  }
+  nan_c = wave_sum_u32(nan_c);
+  nf_c = wave_sum_u32(nf_c);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = nan_c; red[1][threadIdx.x >> 6] = nf_c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0, c = 0;
+    for (int w = 0; w < kSlowBlock / 64; ++w) { a += red[0][w]; c += red[1][w]; }
+    s.nan_count = a;
+    s.nonfinite_count = c;
+  }
+  __syncthreads();
+  bool fill = false;
+  float med = __uint_as_float(0x7fc00000u);
+  if (s.nonfinite_count != 0) {
+    const uint32_t m = s.n - s.nan_count;
+    if (m == 0) {                        // all-NaN: nanmedian is NaN, every value stays NaN
+      if (threadIdx.x == 0) {
         s.has_med = 1;
         s.mode = 2;
         s.p2 = s.p98 = (double)__uint_as_float(0x7fc00000u);
         s.phase = PH_DONE;
-      } else {
-        const uint32_t h = m / 2;
-        if (m & 1u) { s.rank[0] = s.rank[1] = h; s.med_ranks = 1; }
-        else { s.rank[0] = h - 1; s.rank[1] = h; s.med_ranks = 2; }
-        s.ntgt = 2;
-        s.prefix[0] = s.prefix[1] = 0;
-        s.phase = PH_MED;
+        st[b] = s;
       }
-    } else {
-      pct_targets(s);
-      s.phase = PASS == 0 ? PH_PCT : PH_PCT2;
+      return;
     }
-    for (int i = 0; i < 4; ++i) s.slot[i] = 0;
-    s.nslot = 1;
+    uint32_t r[2];
+    const uint32_t h = m / 2;
+    int nr;
+    if (m & 1u) { r[0] = r[1] = h; nr = 1; }
+    else { r[0] = h - 1; r[1] = h; nr = 2; }
+    slow_radix(g, b, false, 0.f, r, 2, keys, sh, sc, &rbin, &rrem, red, kmm);
+    const float a = key2f(keys[0]);
+    const float c = key2f(keys[1]);
+    med = nr == 1 ? a : (a + c) / 2.0f;   // np.mean of the middle pair in float32
+    fill = true;
+    if (threadIdx.x == 0) {
+      s.med = med;
+      s.has_med = 1;
+      s.med_ranks = (uint32_t)nr;
+    }
+    if (isnan(med)) {   // e.g. median of {-inf, +inf}: the filled map has NaNs -> np.percentile is NaN
+      if (threadIdx.x == 0) {
+        s.mode = 2;
+        s.p2 = s.p98 = (double)med;
+        s.phase = PH_DONE;
+        st[b] = s;
+      }
+      return;
+    }
   }
-  __syncthreads();
-  if (s.phase == PH_DONE) {
-    if (threadIdx.x == 0) st[b] = s;
-    return;
-  }
-  uint32_t* gh = hist + (size_t)b * kSlots * kBins;
-  const int nb = LEVEL == 2 ? 1024 : kBins;
-  for (int t = 0; t < (int)s.ntgt; ++t) {
-    if (threadIdx.x == 0) { res_bin[t] = 0; res_rem[t] = 0; }
-    __syncthreads();
-    find_bin(gh + s.slot[t] * kBins, nb, s.rank[t], sc, &res_bin[t], &res_rem[t]);
-  }
-  __syncthreads();
-  // consumed histograms -> zero for the next level
-  for (int i = threadIdx.x; i < (int)s.nslot * kBins; i += kBlock) gh[i] = 0;
+  uint32_t r[4];
+  pct_ranks(s.n, r);
+  slow_radix(g, b, fill, med, r, 4, keys, sh, sc, &rbin, &rrem, red, kmm);
   if (threadIdx.x == 0) {
-    const int bits = LEVEL == 2 ? 10 : 11;
-    for (int t = 0; t < (int)s.ntgt; ++t) {
-      s.prefix[t] = (s.prefix[t] << bits) | res_bin[t];
-      s.rank[t] = res_rem[t];
-    }
-    // distinct prefixes -> histogram slots for the next level
-    s.nslot = 0;
-    for (int t = 0; t < (int)s.ntgt; ++t) {
-      int found = -1;
-      for (int q = 0; q < (int)s.nslot; ++q) if (s.slot_prefix[q] == s.prefix[t]) found = q;
-      if (found < 0) { found = (int)s.nslot; s.slot_prefix[s.nslot++] = s.prefix[t]; }
-      s.slot[t] = (uint32_t)found;
-    }
-    if (LEVEL == 2) {
-      if (s.phase == PH_MED) {
-        const float a = key2f(s.prefix[0]);
-        const float c = key2f(s.prefix[1]);
-        s.med = s.med_ranks == 1 ? a : (a + c) / 2.0f;  // np.mean of the middle pair in float32
-        s.has_med = 1;
-        s.phase = PH_PCT2_INIT;
-        if (isnan(s.med)) {  // e.g. median of {-inf, +inf}: the filled map has NaNs -> np.percentile is NaN
-          s.mode = 2;
-          s.p2 = s.p98 = (double)s.med;
-          s.phase = PH_DONE;
-        }
-        s.kmin = 0xffffffffu;
-        s.kmax = 0u;
-        s.nslot = 1;
-        s.slot_prefix[0] = 0;
-      } else {
-        finalize_pct(s);
-      }
-    }
+    s.kmin = kmm[0];
+    s.kmax = kmm[1];
+    finalize_pct(s, keys);
     st[b] = s;
   }
 }
@@ -774,6 +1399,19 @@ __device__ __forceinline__ Tap ytap(const Geo& g, int v) {
 // the compiler never parks a wave on a divergent vmcnt(0); the RGB of both point
 // groups a thread owns is in flight before any arithmetic; cv2 taps are recomputed
 // in registers (no table loads).
+// bbox / stats of one image to float64 (the k_finalize work for image b)
+__device__ __forceinline__ void write_final(const SelState& s, const uint32_t* bbox_key, int b, double* bbox,
+                                            double* stats) {
+  if (bbox)
+    for (int k = 0; k < 6; ++k) bbox[b * 6 + k] = (double)key2f(bbox_key[k]);
+  if (stats) {
+    stats[b * 4 + 0] = s.p2;
+    stats[b * 4 + 1] = s.p98;
+    stats[b * 4 + 2] = (double)s.mode;
+    stats[b * 4 + 3] = s.has_med ? (double)s.med : (double)__uint_as_float(0x7fc00000u);
+  }
+}
+
 template <int STEP>
 __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState* st, const uint8_t* img, int B,
                                                            Sweep sw, int invert, Cam cam, float* xyz, uint8_t* rgb,
@@ -798,9 +1436,7 @@ __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState
   if (use_lds) {
     lo = ytap(g, r0 * STEP).i0;
     const int hi = ytap(g, (r1 - 1) * STEP).i1;
-    const int n = (hi - lo + 1) * g.dw;
-    const float* src = g.depth + ((size_t)b * g.dh + lo) * g.dw;
-    for (int i = threadIdx.x; i < n; i += kBlock) rows[i] = src[i];
+    stage_floats(rows, g.depth + ((size_t)b * g.dh + lo) * g.dw, (hi - lo + 1) * g.dw);
   }
   __syncthreads();
   const int Wn4 = cam.Wn >> 2;
@@ -1016,15 +1652,7 @@ static BlurTaps gaussian_taps(int k) {
 __global__ void k_finalize(const SelState* st, int B, double* bbox, double* stats) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const SelState& s = st[b];
-  if (bbox)
-    for (int k = 0; k < 6; ++k) bbox[b * 6 + k] = (double)key2f(s.bbox_key[k]);
-  if (stats) {
-    stats[b * 4 + 0] = s.p2;
-    stats[b * 4 + 1] = s.p98;
-    stats[b * 4 + 2] = (double)s.mode;
-    stats[b * 4 + 3] = s.has_med ? (double)s.med : (double)__uint_as_float(0x7fc00000u);
-  }
+  write_final(st[b], st[b].bbox_key, b, bbox, stats);
 }
 
 // Depth preview colouring (create_depth_preview, app.py:124-172): the model-res depth
@@ -1082,6 +1710,7 @@ static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same
   sw.row0 = row0;
   sw.row_end = row1;
   sw.nrb = std::max(1, (row1 - row0 + sw.R - 1) / sw.R);
+  sw.ntiles = 1;
   // allocate only the window R output rows can span (not the whole budget): occupancy
   if (cap_rows) cap_rows = std::min(cap_rows, (int)std::floor((double)(sw.R - 1) * step * dh / H) + 3);
   sw.lds_rows = cap_rows;
@@ -1129,23 +1758,57 @@ static int exchange(const Exchange* x, uint32_t* hist, SelState* st, int B, hipS
   return I2PC_OK;
 }
 
-template <int PASS>
-static int launch_select(const Geo& g, SelState* st, uint32_t* hist, int B, const Sweep& sw, hipStream_t s,
-                         const Exchange* x = nullptr) {
-  // level 0 histograms one slot (8 KB of LDS); levels 1-2 up to kSlots target prefixes
-  const size_t lds0 = sizeof(uint32_t) * kBins + sweep_lds(sw, g.dw);
-  const size_t lds = sizeof(uint32_t) * kSlots * kBins + sweep_lds(sw, g.dw);
-  const dim3 grid(B * sw.nrb), block(kBlock);
+// Selection sweep geometry: kTileW-column tiles, rows per workgroup from I2PC_SEL_PTS
+// points (default 8192) and the LDS the interpolated model rows of R output rows take.
+static Sweep plan_select(int H, int W, int dh, int dw, bool same, int row0, int row1) {
+  static const int sel_pts = [] { const char* e = getenv("I2PC_SEL_PTS"); return e ? atoi(e) : 8192; }();
+  Sweep sw{};
+  const int tw = std::min(W, kTileW);
+  int R = std::max(1, std::min(32, (sel_pts + tw - 1) / tw));   // <= 32 rows: 16-bit LDS counts
+  auto rows_for = [&](int r) { return std::min(dh, (int)std::floor((double)(r - 1) * dh / H) + 3); };
+  auto bytes = [&](int r, bool raw) { return (size_t)rows_for(r) * (kTileW + (raw ? dw : 0)) * sizeof(float); };
+  sw.raw = 1;
+  if (!same) {
+    while (R > 1 && bytes(R, true) > (size_t)kHrowBudget) R /= 2;
+    if (bytes(R, true) > (size_t)kHrowBudget) sw.raw = 0;   // very wide model rows: interpolate from global
+  }
+  sw.R = R;
+  sw.row0 = row0;
+  sw.row_end = row1;
+  sw.nrb = std::max(1, (row1 - row0 + R - 1) / R);
+  sw.ntiles = (W + kTileW - 1) / kTileW;
+  sw.lds_rows = same ? 0 : rows_for(R);
+  return sw;
+}
+
+template <int LEVEL>
+static int select_level(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, uint32_t cap, int B,
+                        const Sweep& sw, hipStream_t s, const Exchange* x) {
+  // level 0 histograms one slot (8 KB of LDS); levels 1-2 up to kSlots target intervals
+  const size_t lds = sizeof(uint32_t) * (LEVEL == 0 ? 3 : kSlots) * kSlotWords +
+                     (size_t)sw.lds_rows * (kTileW + (sw.raw ? g.dw : 0)) * sizeof(float);
+  const dim3 grid(B * sw.nrb * sw.ntiles), block(kBlock);
+  if (g.same)
+    hipLaunchKernelGGL((k_sweep<LEVEL, true>), grid, block, lds, s, g, st, hist, cand, cap, B, sw);
+  else
+    hipLaunchKernelGGL((k_sweep<LEVEL, false>), grid, block, lds, s, g, st, hist, cand, cap, B, sw);
+  int rc = exchange<LEVEL>(x, hist, st, B, s);
+  if (rc) return rc;
+  // tile-parallel runs only histogram: the histograms are what the bands exchange
+  hipLaunchKernelGGL((k_resolve<LEVEL>), dim3(B), dim3(kBlock), 0, s, st, hist, cand, cap, B, x ? 0 : 1);
+  return I2PC_OK;
+}
+
+static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, const uint32_t* rpart,
+                         uint32_t cap, int B, const Sweep& sw, hipStream_t s, const Exchange* x = nullptr) {
+  hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g.depth, B, g.dh * g.dw, st, hist,
+                     rpart);
+  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, hist, cap, B, x ? 0 : 1);
   int rc;
-  hipLaunchKernelGGL((k_sel_hist<0, PASS>), grid, block, lds0, s, g, st, hist, B, sw);
-  if ((rc = exchange<0>(x, hist, st, B, s))) return rc;
-  hipLaunchKernelGGL((k_sel_resolve<0, PASS>), dim3(B), block, 0, s, st, hist, B);
-  hipLaunchKernelGGL((k_sel_hist<1, PASS>), grid, block, lds, s, g, st, hist, B, sw);
-  if ((rc = exchange<1>(x, hist, st, B, s))) return rc;
-  hipLaunchKernelGGL((k_sel_resolve<1, PASS>), dim3(B), block, 0, s, st, hist, B);
-  hipLaunchKernelGGL((k_sel_hist<2, PASS>), grid, block, lds, s, g, st, hist, B, sw);
-  if ((rc = exchange<2>(x, hist, st, B, s))) return rc;
-  hipLaunchKernelGGL((k_sel_resolve<2, PASS>), dim3(B), block, 0, s, st, hist, B);
+  if ((rc = select_level<0>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
+  if ((rc = select_level<1>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
+  if ((rc = select_level<2>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
+  hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
   return check_launch("select");
 }
 
@@ -1217,25 +1880,21 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   Tap* xt = reinterpret_cast<Tap*>(ws + L.xtab);
   Tap* yt = reinterpret_cast<Tap*>(ws + L.ytab);
 
-  if (hipMemsetAsync(hist, 0, sizeof(uint32_t) * kSlots * kBins * (size_t)batch, s) != hipSuccess)
-    return set_error(I2PC_ELAUNCH, "memset failed");
   const int n = img_h * img_w;
-  const int init_threads = std::max(std::max(batch, img_h), img_w);
-  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, dep_h, dep_w, img_h, img_w,
-                     cv_scale(dep_w, img_w), cv_scale(dep_h, img_h));
+  uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
+  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n, st, hist,
+                     rpart, xt, yt, dep_h, dep_w, img_h, img_w, cv_scale(dep_w, img_w), cv_scale(dep_h, img_h));
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
-  // selection sweeps: I2PC_SEL_PTS points per workgroup (default 8 rows of a 1024-wide image)
-  // (measured r02, B = 32 x 1024^2: 4096 pts 476 us, 8192 462 us, 16384 505 us, 32768 598 us per call)
-  static const int sel_pts = [] { const char* e = getenv("I2PC_SEL_PTS"); return e ? atoi(e) : 8192; }();
-  const int sel_rows = std::max(1, std::min(64, (sel_pts + img_w - 1) / img_w));
-  const Sweep ssel = plan_sweep(img_h, 1, dep_h, dep_w, img_h, g.same != 0, sel_rows, row0, row1);
+  // selection sweeps: I2PC_SEL_PTS points per workgroup (default 8192: 8 rows of a 1024-wide
+  // tile; measured r02, B = 32 x 1024^2 whole call: 4096 pts 334 us, 8192 299 us, 16384 = 8192
+  // (the LDS budget caps the rows at 8))
+  const Sweep ssel = plan_select(img_h, img_w, dep_h, dep_w, g.same != 0, row0, row1);
   Exchange xb = xch ? *xch : Exchange{nullptr, nullptr, nullptr};
   xb.ex = reinterpret_cast<int64_t*>(ws + L.ex);
-  int rc = launch_select<0>(g, st, hist, batch, ssel, s, xch ? &xb : nullptr);
-  if (rc) return rc;
-  rc = launch_select<1>(g, st, hist, batch, ssel, s, xch ? &xb : nullptr);
+  uint32_t* cand = reinterpret_cast<uint32_t*>(ws + L.cand);
+  int rc = launch_select(g, st, hist, cand, rpart, L.cap, batch, ssel, s, xch ? &xb : nullptr);
   if (rc) return rc;
 
   Cam cam;
@@ -1258,6 +1917,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   const Sweep sunp = plan_sweep(Hn, step, dep_h, dep_w, img_h, g.same != 0, unp_rows, prow0, prow1);
   const size_t unp_lds = sweep_lds(sunp, dep_w);
   const double* field = nullptr;
+  const bool fast = !params->smooth && channels == 3 && cam.N % 4 == 0 && cam.Wn % 4 == 0;
   if (params->smooth) {
     double* f0 = reinterpret_cast<double*>(ws + L.field);
     double* f1 = reinterpret_cast<double*>(ws + L.tmp);
@@ -1269,7 +1929,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
     field = f0;
     hipLaunchKernelGGL((k_unproject<true>), dim3(batch * sunp.nrb), dim3(kBlock), 0, s, g, st, field, image,
                        channels, batch, sunp, params->invert, cam, xyz, rgb, st);
-  } else if (channels == 3 && cam.N % 4 == 0 && cam.Wn % 4 == 0) {
+  } else if (fast) {
     // 8 rows of 1024 points (or the equivalent) per workgroup
     static const int pts_per_wg = [] { const char* e = getenv("I2PC_UNP_PTS"); return e ? atoi(e) : 8192; }();
     const int fast_rows = std::max(1, std::min(16, (pts_per_wg + cam.Wn - 1) / cam.Wn));
@@ -1352,17 +2012,13 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
   uint32_t* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
   Tap* xt = reinterpret_cast<Tap*>(ws + L.xtab);
   Tap* yt = reinterpret_cast<Tap*>(ws + L.ytab);
-  if (hipMemsetAsync(hist, 0, sizeof(uint32_t) * kSlots * kBins * (size_t)batch, s) != hipSuccess)
-    return set_error(I2PC_ELAUNCH, "memset failed");
   const int n = h * w;
-  const int init_threads = std::max(std::max(batch, h), w);
-  hipLaunchKernelGGL(k_init, dim3((init_threads + 255) / 256), dim3(256), 0, s, st, batch, n, xt, yt, h, w, h, w, 1.0, 1.0);
+  uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
+  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, n, n, st, hist, rpart, xt,
+                     yt, h, w, h, w, 1.0, 1.0);
   Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
-  const int sel_rows = std::max(1, std::min(16, (8 * 1024 + w - 1) / w));
-  const Sweep ssel = plan_sweep(h, 1, h, w, h, true, sel_rows);
-  int rc = launch_select<0>(g, st, hist, batch, ssel, s);
-  if (rc) return rc;
-  rc = launch_select<1>(g, st, hist, batch, ssel, s);
+  const Sweep ssel = plan_select(h, w, h, w, true, 0, h);
+  int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart, L.cap, batch, ssel, s);
   if (rc) return rc;
   const int64_t total = (int64_t)batch * n;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
