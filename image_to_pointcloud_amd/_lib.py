@@ -32,6 +32,8 @@ class UnprojectParams(ctypes.Structure):
         ("fov_deg", c_double),
         ("smooth", c_int32),
         ("smooth_ksize", c_int32),
+        ("projection", c_int32),     # 0 pinhole, 1 equirectangular
+        ("reserved", c_int32),
     ]
 
 

@@ -37,12 +37,13 @@ namespace i2pc {
 namespace unproj {
 
 constexpr int kSlots = 4;
+constexpr int kMaxTgt = 10;  // p2 / p98 ranks (4); with NaN / Inf also their shifted twins (4) + the median (2)
 constexpr int kBins = 2048;
 constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
 constexpr int kSlowBlock = 1024;
 constexpr int kRangeChunks = 32;
-constexpr int kLdsCand = 12288;  // candidate keys a resolve keeps in LDS
+constexpr int kLdsCand = 10240;  // candidate keys a resolve keeps in LDS
 constexpr int kWinKeys = 6144;   // expected full-resolution keys per level-0 window
 constexpr int kTileW = 1024;     // selection sweep column tile (4 columns per thread)
 constexpr int kSlotWords = kBins / 2;   // sweep LDS per slot: 2048 packed 16-bit counts or 1024 staged keys
@@ -66,11 +67,12 @@ struct alignas(16) SelState {
   uint32_t nonfinite_count;
   uint32_t kmin, kmax;     // ordered keys: min / max over the image (level-0 sweep)
   uint32_t rlo, rhi;       // finite key range of the model-resolution map (k_prepare / k_model_hist)
-  uint32_t ntgt, nslot, nwin, pad0;
-  uint32_t wbin[4];        // level-0 window w = level-0 bins [wbin[2w], wbin[2w+1]] (k_window)
-  uint32_t rank[4];        // remaining rank of target t inside its key interval
-  uint32_t tlo[4], thi[4]; // key interval holding target t (tlo == thi: resolved)
-  uint32_t tslot[4];       // slot target t is swept in next (kNoSlot: resolved)
+  uint32_t ntgt, nslot, nwin, fill;   // fill: NaN / Inf present (nanmedian fill targets)
+  uint32_t wbin[6];        // level-0 window w = level-0 bins [wbin[2w], wbin[2w+1]] (k_window)
+  uint32_t ninf_neg, ninf_pos;   // -inf / +inf pixel counts (level-0 sweep)
+  uint32_t rank[kMaxTgt];  // remaining rank of target t inside its key interval
+  uint32_t tlo[kMaxTgt], thi[kMaxTgt];   // key interval holding target t (tlo == thi: resolved)
+  uint32_t tslot[kMaxTgt]; // slot target t is swept in next (kNoSlot: resolved)
   uint32_t slo[4], shi[4]; // key interval of slot q
   uint32_t smult[4];       // bin multiplier of slot q (0: one key per bin)
   uint32_t smode[4];       // SM_HIST / SM_COMPACT
@@ -112,7 +114,7 @@ struct Geo {
 inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
-  size_t state, hist, cand, rpart, xtab, ytab, ex, field, tmp, total;
+  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, field, tmp, total;
   uint32_t cap;   // candidate keys per slot and image (compaction sweeps)
 };
 
@@ -132,6 +134,7 @@ static Layout layout(int B, int H, int W, int smooth) {
   L.rpart = off; off = align_up(off + sizeof(uint32_t) * 2 * kRangeChunks * (size_t)B, 256);
   L.xtab = off;  off = align_up(off + sizeof(Tap) * (size_t)W, 256);
   L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
+  L.trig = off;  off = align_up(off + sizeof(double) * 2 * ((size_t)W + H), 256);
   L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)B, 256);
   L.field = off;
   if (smooth) {
@@ -264,14 +267,16 @@ __device__ __forceinline__ void level0_bins(uint32_t rlo, uint32_t rhi, uint32_t
   else { lo = 0; mult = bin_mult(0u, 0xffffffffu); }   // no finite model value: any monotone binning
 }
 
-__device__ __forceinline__ bool key_nonfinite(uint32_t k) { return k >= 0xff800000u || k <= 0x007fffffu; }
+constexpr uint32_t kKeyPosInf = 0xff800000u;   // f2key(+inf); larger keys are +NaN payloads
+constexpr uint32_t kKeyNegInf = 0x007fffffu;   // f2key(-inf); smaller keys are -NaN payloads
+__device__ __forceinline__ bool key_nonfinite(uint32_t k) { return k >= kKeyPosInf || k <= kKeyNegInf; }
 
 // First launch of a call (kRangeChunks workgroups per image): per-image selection state,
 // cv2 tap tables, zeroed histograms, and the finite key range of each model-resolution map
 // as per-chunk partials (k_model_hist reduces them).
 __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, int m, int n, SelState* st,
                                                     uint32_t* hist, uint32_t* rpart, Tap* xt, Tap* yt, int dh, int dw,
-                                                    int H, int W, double sx, double sy) {
+                                                    int H, int W, double sx, double sy, double* trig) {
   __shared__ uint32_t red[2][kBlock / 64];
   const int gtid = blockIdx.x * kBlock + threadIdx.x;
   const int nthr = gridDim.x * kBlock;
@@ -299,7 +304,15 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
     yt[i] = t;
   }
   for (size_t i = gtid; i < (size_t)B * kSlots * kBins; i += nthr) hist[i] = 0;
-  if (!depth) return;                     // (state only)
+  if (trig) {       // equirectangular ray tables (the oracle evaluates the same expressions)
+    const double pi = 3.141592653589793;
+    for (int i = gtid; i < W + H; i += nthr) {
+      const double a = i < W ? ((double)i + 0.5) * (2.0 * pi / (double)W) - pi
+                             : pi / 2.0 - ((double)(i - W) + 0.5) * (pi / (double)H);
+      trig[2 * i] = sin(a);
+      trig[2 * i + 1] = cos(a);
+    }
+  }
   const int b = blockIdx.x % B, c = blockIdx.x / B;
   const float* D = depth + (size_t)b * m;
   uint32_t lo = 0xffffffffu, hi = 0u;
@@ -462,8 +475,8 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
                                                   int B, Sweep sw) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
   uint32_t* sh = smem_u;                                        // [slots * kSlotWords]
-  // LDS: level 0 = [histogram | window 0 keys | window 1 keys], levels 1-2 = one region per slot
-  float* hrow = reinterpret_cast<float*>(smem_u + (LEVEL == 0 ? 3 : kSlots) * kSlotWords);   // [rows][kTileW]
+  // LDS: level 0 = [histogram | window 0-2 keys], levels 1-2 = one region per slot
+  float* hrow = reinterpret_cast<float*>(smem_u + kSlots * kSlotWords);   // [rows][kTileW]
   __shared__ uint32_t red[3][kBlock / 64];
   __shared__ uint32_t lcnt[kSlots], gbase[kSlots];
   int b, chunk;
@@ -477,12 +490,13 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
   uint32_t slo[kSlots], shi[kSlots], smult[kSlots];
   bool scomp[kSlots];
   // level 0: windows of level-0 bins whose keys are compacted (k_window); empty = [1, 0]
-  int wlo0 = 1, whi0 = 0, wlo1 = 1, whi1 = 0, nwin = 0;
+  int wlo[3] = {1, 1, 1}, whi[3] = {0, 0, 0}, nwin = 0;
   if (LEVEL == 0) {
     level0_bins(S->rlo, S->rhi, slo[0], smult[0]);
     nwin = (int)S->nwin;
-    if (nwin > 0) { wlo0 = (int)S->wbin[0]; whi0 = (int)S->wbin[1]; }
-    if (nwin > 1) { wlo1 = (int)S->wbin[2]; whi1 = (int)S->wbin[3]; }
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+      if (w < nwin) { wlo[w] = (int)S->wbin[2 * w]; whi[w] = (int)S->wbin[2 * w + 1]; }
   } else {
     nslot = (int)S->nslot;
 #pragma unroll
@@ -526,7 +540,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
 
   const int lane = threadIdx.x & 63;
   const float* Dimg = g.depth + (size_t)b * g.dh * g.dw;
-  uint32_t nf = 0, kmin = 0xffffffffu, kmax = 0u;
+  uint32_t nf = 0, nnan = 0, nneg = 0, npos = 0, kmin = 0xffffffffu, kmax = 0u;
   int run_bin[4] = {-1, -1, -1, -1};
   uint32_t run_cnt[4] = {0, 0, 0, 0};
   Tap ty_next = SAME ? Tap{0, 0, 1.f, 0.f} : g.yt[v0];
@@ -554,11 +568,18 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
       int hb = -1;
       int cq = -1;
       if (LEVEL == 0) {
-        nf += (active && key_nonfinite(key)) ? 1u : 0u;
-        kmin = min(kmin, active ? key : 0xffffffffu);
-        kmax = max(kmax, active ? key : 0u);
-        hb = active ? (int)bin_of(key, slo[0], smult[0]) : -1;
-        cq = (hb >= wlo0 && hb <= whi0) ? 0 : ((hb >= wlo1 && hb <= whi1) ? 1 : -1);
+        // finite keys only are binned (NaN / +-Inf are counted: the nanmedian fill)
+        const bool fin = active && !key_nonfinite(key);
+        if (active && !fin) {
+          ++nf;
+          nnan += (key != kKeyPosInf && key != kKeyNegInf) ? 1u : 0u;
+          nneg += key == kKeyNegInf ? 1u : 0u;
+          npos += key == kKeyPosInf ? 1u : 0u;
+        }
+        kmin = min(kmin, fin ? key : 0xffffffffu);
+        kmax = max(kmax, fin ? key : 0u);
+        hb = fin ? (int)bin_of(key, slo[0], smult[0]) : -1;
+        cq = (hb >= wlo[0] && hb <= whi[0]) ? 0 : (hb >= wlo[1] && hb <= whi[1]) ? 1 : (hb >= wlo[2] && hb <= whi[2]) ? 2 : -1;
       } else {
 #pragma unroll
         for (int q = 0; q < kSlots; ++q) {
@@ -574,7 +595,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
         // a compaction slot's LDS region (unused by a histogram) stages its keys; one
         // LDS atomic per slot and wave, global appends only past kSlotWords keys per block
 #pragma unroll
-        for (int q = 0; q < (LEVEL == 0 ? 2 : kSlots); ++q) {
+        for (int q = 0; q < (LEVEL == 0 ? 3 : kSlots); ++q) {
           const uint64_t m = __ballot(cq == q);
           if (!m) continue;
           const int leader = __ffsll((unsigned long long)m) - 1;
@@ -603,6 +624,16 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
     kmin = wave_min_u32(kmin);
     kmax = wave_max_u32(kmax);
     if (lane == 0) { red[0][wid] = nf; red[1][wid] = kmin; red[2][wid] = kmax; }
+    if (__builtin_amdgcn_readfirstlane(nf)) {       // rare: split the non-finite count
+      nnan = wave_sum_u32(nnan);
+      nneg = wave_sum_u32(nneg);
+      npos = wave_sum_u32(npos);
+      if (lane == 0) {
+        if (nnan) atomicAdd(&S->nan_count, nnan);
+        if (nneg) atomicAdd(&S->ninf_neg, nneg);
+        if (npos) atomicAdd(&S->ninf_pos, npos);
+      }
+    }
   }
   __syncthreads();
   if (LEVEL == 0 && threadIdx.x == 0) {
@@ -613,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
     if (mx) atomicMax(&S->kmax, mx);
   }
   uint32_t* gh = hist + (size_t)b * kSlots * kBins;
-  // compaction slots: q -> LDS region (level 0: the windows, regions 1-2), cand slot q
+  // compaction slots: q -> LDS region (level 0: the windows, regions 1-3), cand slot q
   const int ncq = LEVEL == 0 ? nwin : nslot;
   for (int q = 0; q < ncq; ++q) {
     if (LEVEL > 0 && !scomp[q]) continue;
@@ -811,9 +842,10 @@ __device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint3
 // whose keys the level-0 sweep compacts.  When a target's bin lies inside a window (and the
 // window did not overflow), the level-0 resolve selects the exact key from those candidates
 // and the later levels are no-ops; otherwise they run as usual.  Consumes histogram slot 3.
-__global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist, uint32_t cap, int B, int enable) {
+__global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist, uint32_t cap, int B, int enable,
+                                                   int m) {
   __shared__ uint32_t mh[kBins];
-  __shared__ uint32_t wsum[kBlock / 64], wb[4], tot;
+  __shared__ uint32_t wsum[kBlock / 64], wb[6], tot;
   const int b = blockIdx.x;
   if (b >= B) return;
   SelState* S = st + b;
@@ -849,13 +881,16 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist,
     if (lane >= o) x += y;
   }
   if (lane == 63) wsum[wv] = x;
-  if (threadIdx.x < 4) wb[threadIdx.x] = (threadIdx.x & 1) ? 0u : (uint32_t)kBins;
+  // a model map holding NaN / Inf adds a window at its median (the nanmedian fill)
+  const int nq = (uint32_t)m > mtot ? 3 : 2;
+  if (threadIdx.x < 6) wb[threadIdx.x] = (threadIdx.x & 1) ? 0u : (uint32_t)kBins;
   __syncthreads();
   uint32_t off = 0;
   for (int i = 0; i < wv; ++i) off += wsum[i];
   double cum = (double)(x + off - seg);   // exclusive prefix of this thread's first bin
-  for (int k = 0; k < 2; ++k) {
-    const double r = floor((double)(mtot - 1) * (k ? 0.98 : 0.02));
+  for (int k = 0; k < nq; ++k) {
+    const double q = k == 0 ? 0.02 : (k == nq - 1 ? 0.98 : 0.5);
+    const double r = floor((double)(mtot - 1) * q);
     double c = cum;
     for (int i = 0; i < per; ++i) {
       const int bn = threadIdx.x * per + i;
@@ -866,16 +901,83 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist,
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t w[4] = {wb[0], wb[1], wb[2], wb[3]};
-    uint32_t nwin = 2;
-    if (w[2] <= w[1] + 1) {      // overlapping / touching windows: one window
-      w[0] = min(w[0], w[2]);
-      w[1] = max(w[1], w[3]);
-      nwin = 1;
+    // ascending windows; overlapping / touching neighbours merge
+    uint32_t w[6];
+    int nw = 0;
+    for (int k = 0; k < nq; ++k) {
+      const uint32_t lo = wb[2 * k], hi = wb[2 * k + 1];
+      if (lo > hi) continue;
+      if (nw > 0 && lo <= w[2 * nw - 1] + 1) {
+        w[2 * nw - 1] = max(w[2 * nw - 1], hi);
+      } else {
+        w[2 * nw] = lo;
+        w[2 * nw + 1] = hi;
+        ++nw;
+      }
     }
-    for (int i = 0; i < 4; ++i) S->wbin[i] = w[i];
-    S->nwin = w[0] <= w[1] ? nwin : 0;
+    for (int i = 0; i < 2 * nw; ++i) S->wbin[i] = w[i];
+    S->nwin = (uint32_t)nw;
   }
+}
+
+// Targets of a map holding NaN / +-Inf (app.py:194-197: np.nanmedian of the non-NaN values,
+// then np.percentile of the map with every non-finite value replaced by it), all as order
+// statistics of the FINITE keys F, known right after level 0 (k = non-finite count):
+//   non-NaN sorted    = [-inf x nneg] + F + [+inf x npos]           -> median targets 8, 9
+//   filled map sorted = [F < med] + [med x (#F == med + k)] + [F > med]
+// so the filled map's rank-r value is F_(r) if F_(r) < med, else F_(r-k) if F_(r-k) > med,
+// else med: targets t = F_(r_t) and 4 + t = F_(r_t - k) for the four percentile ranks.
+// Ranks outside F are resolved at once to the +-inf keys (they never win those tests).
+__device__ void fill_targets(SelState& s) {
+  const uint32_t n = s.n, k = s.nonfinite_count, nfin = n - k, nneg = s.ninf_neg;
+  uint32_t r[4];
+  pct_ranks(n, r);
+  auto set = [&](int t, int64_t j) {      // F rank j, or a resolved +-inf sentinel
+    if (j < 0) { s.tlo[t] = s.thi[t] = kKeyNegInf; s.tslot[t] = kNoSlot; return; }
+    if (j >= (int64_t)nfin) { s.tlo[t] = s.thi[t] = kKeyPosInf; s.tslot[t] = kNoSlot; return; }
+    s.rank[t] = (uint32_t)j;
+    s.tlo[t] = 0;
+    s.thi[t] = 0xffffffffu;
+    s.tslot[t] = 0;
+  };
+  for (int t = 0; t < 4; ++t) {
+    set(t, (int64_t)r[t]);
+    set(4 + t, (int64_t)r[t] - (int64_t)k);
+  }
+  const uint32_t m = n - s.nan_count, hm = m / 2;
+  s.med_ranks = (m & 1u) ? 1u : 2u;
+  const uint32_t g[2] = {s.med_ranks == 1 ? hm : hm - 1, hm};
+  for (int i = 0; i < 2; ++i) {
+    if (g[i] < nneg) set(8 + i, -1);
+    else if (g[i] >= nneg + nfin) set(8 + i, (int64_t)nfin);
+    else set(8 + i, (int64_t)(g[i] - nneg));
+  }
+  s.ntgt = kMaxTgt;
+  s.fill = 1;
+}
+
+// All targets resolved: p2 / p98 (and their branch) from the target keys.
+__device__ void finish_targets(SelState& s) {
+  if (!s.fill) {
+    finalize_pct(s, s.tlo);
+    return;
+  }
+  const float a = key2f(s.tlo[8]), c = key2f(s.tlo[9]);
+  const float med = s.med_ranks == 1 ? a : (a + c) / 2.0f;   // np.mean of the middle pair in float32
+  s.med = med;
+  s.has_med = 1;
+  if (isnan(med)) {   // e.g. median of {-inf, +inf}: the filled map has NaNs -> np.percentile is NaN
+    s.mode = 2;
+    s.p2 = s.p98 = (double)med;
+    s.phase = PH_DONE;
+    return;
+  }
+  const uint32_t mk = f2key(med);
+  uint32_t pk[4];
+  for (int t = 0; t < 4; ++t) pk[t] = s.tlo[t] < mk ? s.tlo[t] : (s.tlo[4 + t] > mk ? s.tlo[4 + t] : mk);
+  s.kmin = min(s.kmin, mk);            // min / max of the filled map (app.py:198-199 branch)
+  s.kmax = max(s.kmax, mk);
+  finalize_pct(s, pk);
 }
 
 // One resolve per level (a workgroup per image): histogram slots -> the bin of each target
@@ -887,7 +989,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
   __shared__ uint32_t lh[kBins];
   __shared__ uint32_t ck[kLdsCand];
   __shared__ uint32_t wsum[kBlock / 64];
-  __shared__ uint32_t rbin[4], rrem[4], tcnt[4], qr[4], qk[4], tl[4], tz[4], tr[4], tbin[4];
+  __shared__ uint32_t rbin[kMaxTgt], rrem[kMaxTgt], tcnt[kMaxTgt], qr[kMaxTgt], qk[kMaxTgt], tl[kMaxTgt],
+      tz[kMaxTgt], tr[kMaxTgt], tbin[kMaxTgt];
   __shared__ SelState s;
   const int b = blockIdx.x;
   if (b >= B) return;
@@ -899,19 +1002,24 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
   if (LEVEL == 0) {
     __syncthreads();
     if (threadIdx.x == 0) {
-      if (s.nonfinite_count != 0) {
-        s.phase = PH_SLOW;
-      } else {
+      s.nslot = 1;
+      level0_bins(s.rlo, s.rhi, s.slo[0], s.smult[0]);
+      s.smode[0] = SM_HIST;
+      if (s.nonfinite_count == 0) {
         pct_ranks(s.n, s.rank);
         s.ntgt = 4;
-        s.nslot = 1;
-        level0_bins(s.rlo, s.rhi, s.slo[0], s.smult[0]);
-        s.smode[0] = SM_HIST;
         for (int t = 0; t < 4; ++t) s.tslot[t] = 0;
+      } else if (s.nan_count == s.n) {   // all-NaN: nanmedian is NaN, every value stays NaN
+        s.has_med = 1;
+        s.mode = 2;
+        s.p2 = s.p98 = (double)__uint_as_float(0x7fc00000u);
+        s.phase = PH_DONE;
+      } else {
+        fill_targets(s);
       }
     }
     __syncthreads();
-    if (s.phase == PH_SLOW) {
+    if (s.phase != PH_INIT) {
       for (int i = threadIdx.x; i < kBins; i += kBlock) gh[i] = 0;
       if (threadIdx.x == 0) st[b] = s;
       return;
@@ -930,12 +1038,12 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
   }
   for (int q = 0; q < (int)s.nslot; ++q) {
     // the targets swept in slot q (every thread builds the same list)
-    int nq = 0, tq[4];
+    int nq = 0, tq[kMaxTgt];
     for (int t = 0; t < (int)s.ntgt; ++t)
       if (s.tslot[t] == (uint32_t)q) tq[nq++] = t;
     if (nq == 0) continue;
     if (threadIdx.x < nq) qr[threadIdx.x] = s.rank[tq[threadIdx.x]];
-    if (threadIdx.x < 4) { rbin[threadIdx.x] = 0; rrem[threadIdx.x] = 0; }
+    if (threadIdx.x < kMaxTgt) { rbin[threadIdx.x] = 0; rrem[threadIdx.x] = 0; }
     __syncthreads();
     if (s.smode[q] == SM_HIST) {
       dma_words(lh, gh + q * kBins, kBins);     // the slot's histogram into LDS
@@ -947,6 +1055,37 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
           tbin[t] = rbin[k];
           bin_interval(rbin[k], s.slo[q], s.smult[q], clo[q], chi[q], s.tlo[t], s.thi[t]);
           s.rank[t] = rrem[k];
+        }
+        if (LEVEL == 1 && nq > 1) {
+          // unresolved targets of this slot whose bins lie within kBins keys of each other share
+          // the level-2 slot (one key per bin there, so it resolves them all): the group's
+          // interval spans their bins, ranks re-based by the counts of the bins before them
+          int ord[kMaxTgt], no = 0;
+          for (int k = 0; k < nq; ++k)
+            if (s.tlo[tq[k]] != s.thi[tq[k]]) ord[no++] = k;
+          for (int i = 1; i < no; ++i)
+            for (int j = i; j > 0 && rbin[ord[j]] < rbin[ord[j - 1]]; --j) { const int x = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = x; }
+          for (int i = 0; i < no;) {
+            const int t0 = tq[ord[i]];
+            const uint32_t glo = s.tlo[t0];
+            int e = i + 1;
+            while (e < no && (uint64_t)s.thi[tq[ord[e]]] - glo + 1 <= (uint64_t)kBins) ++e;
+            if (e - i > 1) {
+              const uint32_t b0 = rbin[ord[i]], ghi = s.thi[tq[ord[e - 1]]];
+              uint32_t below = 0, bcur = b0;
+              for (int j = i; j < e; ++j) {
+                const int t = tq[ord[j]];
+                for (; bcur < rbin[ord[j]]; ++bcur) below += lh[bcur];
+                s.rank[t] = below + rrem[ord[j]];
+                s.tlo[t] = glo;
+                s.thi[t] = ghi;
+              }
+              uint32_t cnt = below;
+              for (; bcur <= rbin[ord[e - 1]]; ++bcur) cnt += lh[bcur];
+              for (int j = i; j < e; ++j) tcnt[tq[ord[j]]] = cnt;
+            }
+            i = e;
+          }
         }
       }
     } else {
@@ -970,15 +1109,15 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
   }
   if (LEVEL == 0 && s.nwin > 0) {
     // targets whose level-0 bin lies in a k_window window: exact key from its candidates
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < (int)s.ntgt; ++t) {
       if (s.tlo[t] == s.thi[t]) continue;
       int w = -1;
       for (int k = 0; k < (int)s.nwin; ++k)
         if (tbin[t] >= s.wbin[2 * k] && tbin[t] <= s.wbin[2 * k + 1]) w = k;
       if (w < 0 || s.ccount[w] > cap) continue;
       // the unresolved targets of the same bin go together
-      int ng = 0, tg[4];
-      for (int u = t; u < 4; ++u)
+      int ng = 0, tg[kMaxTgt];
+      for (int u = t; u < (int)s.ntgt; ++u)
         if (s.tlo[u] != s.thi[u] && tbin[u] == tbin[t]) tg[ng++] = u;
       if (threadIdx.x < ng) qr[threadIdx.x] = s.rank[tg[threadIdx.x]];
       const uint32_t c = s.ccount[w];
@@ -1011,6 +1150,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
       for (int q = 0; q < nslot; ++q)
         if (s.slo[q] == s.tlo[t] && s.shi[q] == s.thi[t]) found = q;
       if (found < 0) {
+        if (nslot == kSlots) { s.phase = PH_SLOW; break; }   // more distinct intervals than slots
         found = nslot++;
         s.slo[found] = s.tlo[t];
         s.shi[found] = s.thi[t];
@@ -1021,10 +1161,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
       s.tslot[t] = (uint32_t)found;
     }
     s.nslot = (uint32_t)nslot;
-    if (all) {
-      finalize_pct(s, s.tlo);
-    } else {
-      s.phase = LEVEL == 2 ? PH_SLOW : PH_SEL;   // (a level-2 interval is one key wide: not reached)
+    if (s.phase != PH_SLOW) {
+      if (all) finish_targets(s);
+      else s.phase = LEVEL == 2 ? PH_SLOW : PH_SEL;   // (a level-2 interval is one key wide: not reached)
     }
     st[b] = s;
   }
@@ -1223,10 +1362,25 @@ __device__ __forceinline__ double normalize(float val, const Norm& nm) {
 struct Cam {
   double cx, cy, f, rf, scale;   // rf = RN(1 / f)
   int step, Wn, N;
+  int proj;                      // 0 pinhole (app.py:216-238), 1 equirectangular (panoramas)
+  const double* trig;            // equirectangular: [W] (sin, cos) of longitude, then [H] (sin, cos) of latitude
+  int W;
 };
 
 __device__ __forceinline__ void project(double d, int v, int u, const Cam& c, float& x, float& y, float& z) {
   const double zd = d * c.scale;                       // app.py:233
+  if (c.proj == 1) {
+    // equirectangular panorama (not in the reference): the depth is the range along the ray
+    // of longitude lon(u) = (u + 0.5) 2pi / W - pi, latitude lat(v) = pi / 2 - (v + 0.5) pi / H;
+    // x right, y down, z forward (the pinhole axes at the panorama centre)
+    const double slon = c.trig[2 * u], clon = c.trig[2 * u + 1];
+    const double slat = c.trig[2 * c.W + 2 * v], clat = c.trig[2 * c.W + 2 * v + 1];
+    const double rh = zd * clat;
+    x = (float)(rh * slon);
+    y = (float)(-(zd * slat));
+    z = (float)(rh * clon);
+    return;
+  }
   const double zz = zd != 0.0 ? zd : 1e-6;             // app.py:234-235
   x = (float)div_rn(((double)u - c.cx) * zz, c.f, c.rf);
   y = (float)div_rn(((double)v - c.cy) * zz, c.f, c.rf);
@@ -1724,7 +1878,7 @@ static size_t sweep_lds(const Sweep& sw, int dw) { return sw.lds_rows ? (size_t)
 // (sum, sum, min, max across the bands).
 __global__ void k_band_export(const SelState* st, int B, int64_t* ex) {
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    ex[b] = st[b].nan_count;
+    ex[b] = (int64_t)st[b].nan_count | ((int64_t)st[b].ninf_neg << 32);   // two sums in one row
     ex[B + b] = st[b].nonfinite_count;
     ex[2 * B + b] = st[b].kmin;
     ex[3 * B + b] = st[b].kmax;
@@ -1732,7 +1886,8 @@ __global__ void k_band_export(const SelState* st, int B, int64_t* ex) {
 }
 __global__ void k_band_import(SelState* st, int B, const int64_t* ex) {
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    st[b].nan_count = (uint32_t)ex[b];
+    st[b].nan_count = (uint32_t)(ex[b] & 0xffffffffll);
+    st[b].ninf_neg = (uint32_t)(ex[b] >> 32);
     st[b].nonfinite_count = (uint32_t)ex[B + b];
     st[b].kmin = (uint32_t)ex[2 * B + b];
     st[b].kmax = (uint32_t)ex[3 * B + b];
@@ -1785,7 +1940,7 @@ template <int LEVEL>
 static int select_level(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, uint32_t cap, int B,
                         const Sweep& sw, hipStream_t s, const Exchange* x) {
   // level 0 histograms one slot (8 KB of LDS); levels 1-2 up to kSlots target intervals
-  const size_t lds = sizeof(uint32_t) * (LEVEL == 0 ? 3 : kSlots) * kSlotWords +
+  const size_t lds = sizeof(uint32_t) * kSlots * kSlotWords +
                      (size_t)sw.lds_rows * (kTileW + (sw.raw ? g.dw : 0)) * sizeof(float);
   const dim3 grid(B * sw.nrb * sw.ntiles), block(kBlock);
   if (g.same)
@@ -1803,7 +1958,7 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
                          uint32_t cap, int B, const Sweep& sw, hipStream_t s, const Exchange* x = nullptr) {
   hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g.depth, B, g.dh * g.dw, st, hist,
                      rpart);
-  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, hist, cap, B, x ? 0 : 1);
+  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, hist, cap, B, x ? 0 : 1, g.dh * g.dw);
   int rc;
   if ((rc = select_level<0>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   if ((rc = select_level<1>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
@@ -1867,6 +2022,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   I2PC_REQUIRE(channels >= 1 && channels <= 4, "channels must be 1..4");
   const int step = params->step;
   I2PC_REQUIRE(step == 1 || step == 2 || step == 4, "step must be 1, 2 or 4 (low/medium/high)");
+  I2PC_REQUIRE(params->projection == 0 || params->projection == 1, "projection must be 0 (pinhole) or 1 (equirectangular)");
   I2PC_REQUIRE((int64_t)img_h * img_w < (1ll << 31), "image too large");
   const int blur_k = params->smooth_ksize < 3 ? 3 : params->smooth_ksize / 2 * 2 + 1;   // app.py:211
   if (params->smooth)
@@ -1882,8 +2038,9 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
 
   const int n = img_h * img_w;
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
+  double* trig = params->projection == 1 ? reinterpret_cast<double*>(ws + L.trig) : nullptr;
   hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n, st, hist,
-                     rpart, xt, yt, dep_h, dep_w, img_h, img_w, cv_scale(dep_w, img_w), cv_scale(dep_h, img_h));
+                     rpart, xt, yt, dep_h, dep_w, img_h, img_w, cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig);
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
@@ -1909,6 +2066,9 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   cam.rf = 1.0 / cam.f;
   cam.scale = params->depth_scale;
   cam.step = step;
+  cam.proj = params->projection;
+  cam.trig = trig;
+  cam.W = img_w;
   cam.Wn = (img_w + step - 1) / step;
   const int Hn = (img_h + step - 1) / step;
   cam.N = cam.Wn * Hn;
@@ -2015,7 +2175,7 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
   const int n = h * w;
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
   hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, n, n, st, hist, rpart, xt,
-                     yt, h, w, h, w, 1.0, 1.0);
+                     yt, h, w, h, w, 1.0, 1.0, nullptr);
   Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
   const Sweep ssel = plan_select(h, w, h, w, true, 0, h);
   int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart, L.cap, batch, ssel, s);

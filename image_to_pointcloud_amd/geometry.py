@@ -22,6 +22,9 @@ from . import _lib
 logger = logging.getLogger(__name__)
 
 DENSITY_STEP = {"low": 4, "medium": 2, "high": 1}   # app.py:226
+# camera model of the back-projection: the reference's pinhole (app.py:216-238), or an
+# equirectangular panorama (C4's 360-degree images; not in the reference, see i2pc.h)
+PROJECTION = {"pinhole": 0, "equirect": 1}
 
 
 def _torch():
@@ -80,13 +83,14 @@ def point_count(h: int, w: int, step: int) -> int:
 def unproject_batch(depth, images, density: str = "medium", invert: bool = True,
                     depth_scale: float = 10.0, smooth: bool = False, smooth_ksize: int = 5,
                     fov: Optional[float] = None, out: Optional[PointBatch] = None,
-                    workspace=None) -> PointBatch:
+                    workspace=None, projection: str = "pinhole") -> PointBatch:
     """Batched GPU depth_to_point_cloud.
 
     depth    : torch.float32 [B, h, w] (model resolution) on the device
     images   : torch.uint8 [B, H, W, C] BGR on the device
     workspace: optional caller-owned device uint8 buffer of >= workspace_bytes(B, H, W, smooth)
                bytes (required for graph capture: the shared per-device one may be reallocated)
+    projection: "pinhole" (the reference's camera) or "equirect" (360-degree panoramas)
     """
     torch = _torch()
     if density not in DENSITY_STEP:
@@ -126,7 +130,7 @@ def unproject_batch(depth, images, density: str = "medium", invert: bool = True,
         ws = _workspace(ws_bytes, dev)
     p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
                              fov_deg=float(fov) if fov else 0.0, smooth=int(bool(smooth)),
-                             smooth_ksize=int(smooth_ksize))
+                             smooth_ksize=int(smooth_ksize), projection=PROJECTION[projection])
     _lib.call("i2pc_unproject", _ptr(depth), depth.shape[1], depth.shape[2], _ptr(images), C, B, H, W,
               ctypes.byref(p), _ptr(out.xyz), _ptr(out.rgb), _ptr(out.bbox), _ptr(out.stats),
               _ptr(ws), ws.numel(), _stream_handle())
@@ -259,7 +263,8 @@ def band_rows(img_h: int, parts: int, step: int = 1) -> list:
 
 def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: int, exchange=None,
                    density: str = "high", invert: bool = True, depth_scale: float = 10.0,
-                   fov: Optional[float] = None, workspace=None, comm=None, out=None):
+                   fov: Optional[float] = None, workspace=None, comm=None, out=None,
+                   projection: str = "pinhole"):
     """This rank's band [row0, row1) of one image's unprojection (i2pc_unproject_band).
 
     comm       : a distributed.RcclComm: the exchange runs on the device (RCCL all-reduces on
@@ -302,7 +307,8 @@ def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: i
     ws = workspace if workspace is not None else _workspace(lib.i2pc_unproject_workspace_bytes(1, img_h, img_w, 0), dev)
     if comm is not None:
         p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
-                                 fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5)
+                                 fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5,
+                                 projection=PROJECTION[projection])
         _lib.call("i2pc_unproject_band_rccl", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
                   img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),
                   _ptr(ws), ws.numel(), comm.handle, _stream_handle())
@@ -323,7 +329,8 @@ def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: i
 
     cb = EXCHANGE_FN(_cb)
     p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
-                             fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5)
+                             fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5,
+                                 projection=PROJECTION[projection])
     try:
         _lib.call("i2pc_unproject_band", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
                   img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),

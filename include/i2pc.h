@@ -53,7 +53,11 @@ typedef struct i2pc_unproject_params {
   double depth_scale;  /* depth_scale (app.py:233) */
   double fov_deg;      /* fov; <= 0 or NaN selects f = 1.2*max(W,H) (app.py:219-223) */
   int32_t smooth;      /* smooth_depth (app.py:209-214) */
-  int32_t smooth_ksize;/* kernel size; only the default 5 is supported */
+  int32_t smooth_ksize;/* GaussianBlur kernel: ksize//2*2+1, at least 3, at most 63 taps (app.py:211) */
+  int32_t projection;  /* 0 pinhole (app.py:216-238); 1 equirectangular panorama (not in the
+                          reference): depth = range along the ray of longitude (u+0.5)2pi/W - pi,
+                          latitude pi/2 - (v+0.5)pi/H; x right, y down, z forward; fov ignored */
+  int32_t reserved;    /* 0 */
 } i2pc_unproject_params;
 
 /* Bytes of device workspace i2pc_unproject needs. */

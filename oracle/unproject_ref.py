@@ -298,6 +298,36 @@ def depth_to_point_cloud(image: np.ndarray, depth: np.ndarray, density: str = "m
     return pts, cols
 
 
+def depth_to_point_cloud_equirect(image: np.ndarray, depth: np.ndarray, density: str = "medium",
+                                  invert: bool = True, depth_scale: float = 10.0):
+    """Equirectangular variant (C4 panoramas; NOT in the reference -- parity unpinned beyond
+    this restatement).  Resize / normalisation exactly as depth_to_point_cloud (app.py:186-206);
+    the normalised depth times depth_scale is the range r along the ray of longitude
+    lon = (u + 0.5) 2pi / W - pi and latitude lat = pi/2 - (v + 0.5) pi / H:
+    x = (r cos lat) sin lon, y = -(r sin lat), z = (r cos lat) cos lon (float64, then float32),
+    the operation order i2pc_unproject evaluates with projection = 1."""
+    img_h, img_w = image.shape[:2]
+    if depth.shape[:2] != (img_h, img_w):
+        depth = resize_linear_cv2(depth, img_w, img_h)
+    d, _ = normalize_depth(depth, invert)
+    step = DENSITY_STEP[density]
+    vs = np.arange(0, img_h, step)
+    us = np.arange(0, img_w, step)
+    lon = (us.astype(np.float64) + 0.5) * (2.0 * np.pi / img_w) - np.pi
+    lat = np.pi / 2.0 - (vs.astype(np.float64) + 0.5) * (np.pi / img_h)
+    r = d[np.ix_(vs, us)].astype(np.float64) * float(depth_scale)
+    rh = r * np.cos(lat)[:, None]
+    x = rh * np.sin(lon)[None, :]
+    y = -(r * np.sin(lat)[:, None])
+    z = rh * np.cos(lon)[None, :]
+    pts = np.stack([x.ravel(), y.ravel(), z.ravel()], axis=1).astype(np.float32)
+    if image.ndim == 3 and image.shape[2] >= 3:
+        cols = image[np.ix_(vs, us)][..., :3].reshape(-1, 3)[:, ::-1].astype(np.float32)
+    else:
+        cols = np.full((pts.shape[0], 3), 128, dtype=np.float32)
+    return pts, cols
+
+
 def gis_bounds(points: np.ndarray) -> dict:
     """generate_gis_metadata bounds (app.py:393-400)."""
     return {

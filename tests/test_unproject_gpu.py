@@ -225,14 +225,15 @@ def test_c4_panorama_full_size_bands_and_oracle():
     assert _same_bits(whole.rgb[0].cpu().numpy().astype(np.float32), ec)
 
 
-def _band_check(dep, img, parts, density, depth_scale=12.0):
+def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole"):
     import threading
     g = _geom()
     dev = torch.device("cuda")
     H, W = img.shape[:2]
     tdep = torch.from_numpy(dep).to(dev)
     timg = torch.from_numpy(img).to(dev)
-    whole = g.unproject_batch(tdep[None], timg[None], density=density, depth_scale=depth_scale)
+    whole = g.unproject_batch(tdep[None], timg[None], density=density, depth_scale=depth_scale,
+                              projection=projection)
     torch.cuda.synchronize()
     step = g.DENSITY_STEP[density]
     bands = g.band_rows(H, parts, step)
@@ -261,7 +262,7 @@ def _band_check(dep, img, parts, density, depth_scale=12.0):
                 r0, r1 = bands[i]
                 ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
                 results[i] = g.unproject_band(tdep, timg[r0:r1], H, W, r0, r1, exchange_for(i), density=density,
-                                              depth_scale=depth_scale, workspace=ws)
+                                              depth_scale=depth_scale, workspace=ws, projection=projection)
                 torch.cuda.current_stream().synchronize()
         except Exception as e:   # pragma: no cover - reported below
             errs.append(e)
@@ -285,6 +286,30 @@ def _band_check(dep, img, parts, density, depth_scale=12.0):
     glob[1::2] = bb[:, 1::2].max(0)
     assert _same_bits(glob, whole.bbox[0].cpu().numpy())
     return whole
+
+
+@pytest.mark.parametrize("density", ["high", "low"])
+def test_equirect_projection_matches_oracle_and_bands(density):
+    """Equirectangular mode (C4 panoramas; not in the reference, so parity is against the
+    oracle's restatement only): selection / normalisation / colours bit-exact as in the pinhole
+    mode, xyz within 2 float32 ulps of the float64 oracle (device sin/cos vs libm's), and the
+    4-band split bit-identical to the whole image."""
+    dep = _smooth_depth(64, 128, 91)
+    img = _rgb(512, 1024, 92)
+    whole = _band_check(dep, img, 4, density, depth_scale=10.0, projection="equirect")
+    ep, ec = ref.depth_to_point_cloud_equirect(img, dep, density=density, depth_scale=10.0)
+    got = whole.xyz[0].cpu().numpy()
+    assert got.shape == ep.shape
+    ulp = np.spacing(np.maximum(np.abs(ep), np.float32(1e-30)).astype(np.float32))
+    assert np.all(np.abs(got - ep) <= 2 * ulp), float(np.max(np.abs(got - ep) / ulp))
+    assert _same_bits(whole.rgb[0].cpu().numpy().astype(np.float32), ec)
+    pin = _geom().unproject_batch(torch.from_numpy(dep).cuda()[None], torch.from_numpy(img).cuda()[None],
+                                  density=density, depth_scale=10.0)
+    assert _same_bits(whole.stats[0].cpu().numpy(), pin.stats[0].cpu().numpy())
+    # radius = depth: |xyz| equals the pinhole z (the normalised depth times the scale)
+    r = np.linalg.norm(got.astype(np.float64), axis=1)
+    np.testing.assert_allclose(r, pin.xyz[0, :, 2].cpu().numpy().astype(np.float64), rtol=1e-6, atol=1e-6)
+    print("parity", {"case": f"equirect {density}", "bit_exact_frac": float(np.mean(got == ep))})
 
 
 def test_band_rccl_exchange_single_rank_and_graph_capture():

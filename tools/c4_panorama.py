@@ -11,6 +11,12 @@ exchange is device-side (i2pc_unproject_band_rccl on an RCCL communicator of lib
 and --graph captures each rank's whole band call into a HIP graph); when ranks share a GPU
 it falls back to the host-callback exchange over gloo (correctness runs only).  Rank 0 prints one JSON line (points/s over the job, max
 over ranks), and --check compares every band bit-for-bit with the whole-image unprojection.
+
+--network runs the depth network too: rank 0 holds the whole panorama, preprocesses it to the
+Depth-Anything-V2-Small input (518 x 1036, keep-aspect /14), runs the network (seeded random
+weights) and broadcasts the 518 x 1036 depth over RCCL; every rank then unprojects its band
+(ms_per_image then covers network + broadcast + band unprojection).  --projection equirect
+back-projects the panorama on the sphere (i2pc.h; the reference only has the pinhole model).
 """
 import argparse
 import json
@@ -36,6 +42,8 @@ def main():
     ap.add_argument("--density", default="high")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each rank's band call as a HIP graph (RCCL mode)")
+    ap.add_argument("--network", action="store_true", help="depth from Depth-Anything-V2-Small on rank 0, broadcast")
+    ap.add_argument("--projection", default="pinhole", choices=["pinhole", "equirect"])
     a = ap.parse_args()
     rank, local, world = D.world()
     ngpu = torch.cuda.device_count()
@@ -60,13 +68,43 @@ def main():
     for y in range(r0, r1):
         band[y - r0] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
     timg = torch.from_numpy(band).to(dev)
+    net = None
+    if a.network:
+        from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL
+        from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+        if rank == 0:
+            full = np.empty((H, W, 3), np.uint8)
+            for y in range(H):
+                full[y] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
+            tfull = torch.from_numpy(full).to(dev)[None]
+            net = PointCloudPipeline(1, H, W, spec=DA_V2_SMALL, density=a.density, device=dev)
+            h, w = net.pre.out_h, net.pre.out_w
+            del full
+        hw = torch.tensor([h, w], device=dev)
+        if world > 1:
+            dist.broadcast(hw, 0)
+        h, w = int(hw[0]), int(hw[1])
+        tdep = torch.empty((h, w), dtype=torch.float32, device=dev)
+
+        def infer():
+            if rank == 0:
+                tdep.copy_(net.infer_depth(tfull)[0])
+            if world > 1:
+                dist.broadcast(tdep, 0)
+        infer()
     comm = D.RcclComm() if world > 1 and backend == "nccl" else (D.RcclComm(nranks=1, rank=0) if world == 1 else None)
     ex = D.band_exchange() if comm is None else None
     ws = torch.empty(G.workspace_bytes(1, H, W), dtype=torch.uint8, device=dev)
     res = None
 
+    def band_call():
+        return G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density, comm=comm, workspace=ws, out=res,
+                                projection=a.projection)
+
     def run():
-        return G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density, comm=comm, workspace=ws, out=res)
+        if a.network:
+            infer()
+        return band_call()
     for _ in range(max(1, a.warmup)):
         res = run()
     torch.cuda.synchronize()
@@ -74,8 +112,8 @@ def main():
     if a.graph and comm is not None:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            run()
-        step_fn = graph.replay
+            band_call()
+        step_fn = (lambda: (infer(), graph.replay())) if a.network else graph.replay
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -91,12 +129,14 @@ def main():
         full = np.empty((H, W, 3), np.uint8)
         for y in range(H):
             full[y] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
-        whole = G.unproject_batch(tdep[None], torch.from_numpy(full).to(dev)[None], density=a.density)
+        whole = G.unproject_batch(tdep[None], torch.from_numpy(full).to(dev)[None], density=a.density,
+                                  projection=a.projection)
         wn = (W + step - 1) // step
         p0 = (r0 // step) * wn
         ok = bool(torch.equal(whole.xyz[0][p0:p0 + res[0].shape[0]], res[0])
                   and torch.equal(whole.rgb[0][p0:p0 + res[1].shape[0]], res[1])
-                  and torch.equal(whole.stats[0], res[3]) and torch.equal(whole.bbox[0], bbox))
+                  and torch.equal(whole.stats[0].view(torch.int64), res[3].view(torch.int64))   # NaN-aware
+                  and torch.equal(whole.bbox[0], bbox))
         if world > 1:
             t = torch.tensor([int(ok)], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -109,6 +149,9 @@ def main():
                           "exchange": "RCCL on device (i2pc_unproject_band_rccl)" if comm is not None else "host callback",
                           "hip_graph": bool(a.graph and comm is not None), "ms_per_image": round(el / a.steps * 1e3, 3),
                           "image": [H, W], "depth": [h, w], "density": a.density, "points": n,
+                          "depth_source": "depth-anything-v2-small (seeded weights) on rank 0 + RCCL broadcast"
+                          if a.network else "synthetic smooth field + NaN",
+                          "projection": a.projection,
                           "bit_exact_vs_whole_image": ok, "stats": res[3].tolist(), "bbox": bbox.tolist()}))
     if comm is not None:
         comm.close()
