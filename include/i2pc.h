@@ -93,8 +93,10 @@ int i2pc_unproject(const float* depth, int dep_h, int dep_w,
  * which must all-reduce them in place across the ranks (ordered on `stream`):
  *   hist     : uint32 [hist_words] -> element-wise SUM over ranks
  *   counters : int64 [4][batch] or NULL -> rows 0-1 SUM, row 2 MIN, row 3 MAX
+ *              (row 0 = NaN count | -Inf count << 32, row 1 = non-finite count,
+ *               rows 2-3 = finite key range; passed at level 0 only)
  * and return 0 (non-zero aborts the call).  Every rank must make the same sequence of
- * calls (6 per image: 3 levels x 2 passes).
+ * calls (3 per image, one per selection level; band runs take the histogram levels).
  * image_band : uint8 [row1 - row0, img_w, channels]   the band's rows of the image
  * xyz_band   : float32 [Nb, 3], rgb_band uint8 [Nb, 3] with Nb = (ceil(row1/step) -
  *              row0/step) * ceil(img_w/step): the band's points, row-major, i.e. the
@@ -112,7 +114,7 @@ int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, const uint8_t*
                         void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange, void* user,
                         void* stream);
 
-/* The same band call with the exchange done on the device by RCCL (three all-reduces on
+/* The same band call with the exchange done on the device by RCCL (all-reduces on
  * `stream` per selection sweep: histogram SUM, counters SUM / MIN / MAX), so the call is
  * stream-ordered end to end and can be captured into a HIP graph.  `comm` comes from
  * i2pc_comm_create on every rank with the id rank 0 got from i2pc_comm_unique_id
