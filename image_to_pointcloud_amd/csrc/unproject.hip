@@ -43,6 +43,9 @@ constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
 constexpr int kSlowBlock = 1024;
 constexpr int kRangeChunks = 32;
+// Level 0 bins values (one bin ~ up to 2^31 keys near 0); levels 1-3 bin keys 2048 ways each:
+// 2^31 -> 2^20 -> 2^9 -> 1 key, so the last level always resolves.
+constexpr int kLastLevel = 3;
 constexpr int kLdsCand = 10240;  // candidate keys a resolve keeps in LDS
 constexpr int kWinKeys = 6144;   // expected full-resolution keys per level-0 window
 constexpr int kTileW = 1024;     // selection sweep column tile (4 columns per thread)
@@ -261,10 +264,49 @@ __device__ inline void bin_interval(uint32_t bn, uint32_t lo, uint32_t mult, uin
   a = (uint32_t)A;
   z = (uint32_t)(Z < A ? A : Z);
 }
-// level-0 binning origin / multiplier from the model-map key range
-__device__ __forceinline__ void level0_bins(uint32_t rlo, uint32_t rhi, uint32_t& lo, uint32_t& mult) {
-  if (rlo <= rhi) { lo = rlo; mult = bin_mult(rlo, rhi); }
-  else { lo = 0; mult = bin_mult(0u, 0xffffffffu); }   // no finite model value: any monotone binning
+// Level 0 bins VALUES linearly over the model map's finite range [lo, hi]:
+// bin = (v - lo) * 2048 / (hi - lo) in float32, clamped.  Float subtraction and multiplication
+// round monotonically, so the map is monotone in the value -- hence in the key -- and each bin
+// is a key interval (found by bisection, vbin_interval).  Linear-in-value bins keep ~n/2048 keys
+// per bin for depth-like data; linear-in-key bins would give most bins to the binades near 0
+// (a map with a few zero pixels puts 96 % of its key range below the smallest real depth).
+struct VBins {
+  float lo, inv;
+};
+__device__ __forceinline__ VBins level0_vbins(uint32_t rlo, uint32_t rhi) {
+  VBins vb{0.f, 0.f};
+  if (rlo <= rhi) {
+    vb.lo = key2f(rlo);
+    const float span = key2f(rhi) - vb.lo;
+    vb.inv = (span > 0.f && span < INFINITY) ? (float)(kBins - 1) / span : 0.f;
+  }
+  return vb;
+}
+// bin 0 holds the values <= the model map's minimum -- usually one key: the exact zeros a
+// network's final ReLU leaves are a spike no candidate list could hold, resolved here at once;
+// bins 1..2047 split (minimum, maximum] linearly
+__device__ __forceinline__ uint32_t vbin(float v, const VBins& vb) {
+  if (!(v > vb.lo)) return 0u;
+  const float t = (v - vb.lo) * vb.inv;
+  if (!(t > 0.f)) return 1u;                       // (also NaN: inv 0 with an infinite difference)
+  return t >= (float)(kBins - 2) ? (uint32_t)(kBins - 1) : 1u + (uint32_t)t;
+}
+// key interval of level-0 bin bn, clipped to the finite keys [clo, chi]
+__device__ inline void vbin_interval(uint32_t bn, const VBins& vb, uint32_t clo, uint32_t chi, uint32_t& a,
+                                     uint32_t& z) {
+  auto first = [&](uint32_t target) -> uint64_t {   // smallest key in [clo, chi] with vbin >= target
+    uint64_t lo = clo, hi = (uint64_t)chi + 1;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (vbin(key2f((uint32_t)mid), vb) >= target) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  };
+  const uint64_t A = bn == 0 ? clo : first(bn);
+  const uint64_t Z = bn + 1 >= (uint32_t)kBins ? (uint64_t)chi : first(bn + 1) - 1;
+  a = (uint32_t)A;
+  z = (uint32_t)(Z < A ? A : Z);
 }
 
 constexpr uint32_t kKeyPosInf = 0xff800000u;   // f2key(+inf); larger keys are +NaN payloads
@@ -372,8 +414,7 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(const float* depth, int B
     }
   }
   __syncthreads();
-  uint32_t lo, mult;
-  level0_bins(rr[0], rr[1], lo, mult);
+  const VBins vb = level0_vbins(rr[0], rr[1]);
   // each thread bins a contiguous run of the chunk (neighbouring values share bins: one LDS
   // atomic per run of equal bins), loads issued 8 at a time
   const float* D = depth + (size_t)b * m;
@@ -389,7 +430,7 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(const float* depth, int B
     for (int k = 0; k < 8; ++k) v[k] = D[min(i + k, t1 - 1)];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int bn = (i + k < t1 && isfinite(v[k])) ? (int)bin_of(f2key(v[k]), lo, mult) : -1;
+      const int bn = (i + k < t1 && isfinite(v[k])) ? (int)vbin(v[k], vb) : -1;
       if (bn != run && run >= 0) atomicAdd(&lh[run], cnt);
       cnt = (bn == run ? cnt : 0u) + 1u;
       run = bn;
@@ -491,8 +532,9 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
   bool scomp[kSlots];
   // level 0: windows of level-0 bins whose keys are compacted (k_window); empty = [1, 0]
   int wlo[3] = {1, 1, 1}, whi[3] = {0, 0, 0}, nwin = 0;
+  VBins vb0{0.f, 0.f};
   if (LEVEL == 0) {
-    level0_bins(S->rlo, S->rhi, slo[0], smult[0]);
+    vb0 = level0_vbins(S->rlo, S->rhi);
     nwin = (int)S->nwin;
 #pragma unroll
     for (int w = 0; w < 3; ++w)
@@ -578,7 +620,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
         }
         kmin = min(kmin, fin ? key : 0xffffffffu);
         kmax = max(kmax, fin ? key : 0u);
-        hb = fin ? (int)bin_of(key, slo[0], smult[0]) : -1;
+        hb = fin ? (int)vbin(val, vb0) : -1;
         cq = (hb >= wlo[0] && hb <= whi[0]) ? 0 : (hb >= wlo[1] && hb <= whi[1]) ? 1 : (hb >= wlo[2] && hb <= whi[2]) ? 2 : -1;
       } else {
 #pragma unroll
@@ -1003,7 +1045,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
     __syncthreads();
     if (threadIdx.x == 0) {
       s.nslot = 1;
-      level0_bins(s.rlo, s.rhi, s.slo[0], s.smult[0]);
+      s.slo[0] = 0;                      // (level 0 bins values: vbin / vbin_interval)
+      s.smult[0] = 0;
       s.smode[0] = SM_HIST;
       if (s.nonfinite_count == 0) {
         pct_ranks(s.n, s.rank);
@@ -1053,10 +1096,11 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
           const int t = tq[k];
           tcnt[t] = lh[rbin[k]];
           tbin[t] = rbin[k];
-          bin_interval(rbin[k], s.slo[q], s.smult[q], clo[q], chi[q], s.tlo[t], s.thi[t]);
+          if (LEVEL == 0) vbin_interval(rbin[k], level0_vbins(s.rlo, s.rhi), clo[q], chi[q], s.tlo[t], s.thi[t]);
+          else bin_interval(rbin[k], s.slo[q], s.smult[q], clo[q], chi[q], s.tlo[t], s.thi[t]);
           s.rank[t] = rrem[k];
         }
-        if (LEVEL == 1 && nq > 1) {
+        if (LEVEL >= 1 && LEVEL < kLastLevel && nq > 1) {
           // unresolved targets of this slot whose bins lie within kBins keys of each other share
           // the level-2 slot (one key per bin there, so it resolves them all): the group's
           // interval spans their bins, ranks re-based by the counts of the bins before them
@@ -1163,7 +1207,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
     s.nslot = (uint32_t)nslot;
     if (s.phase != PH_SLOW) {
       if (all) finish_targets(s);
-      else s.phase = LEVEL == 2 ? PH_SLOW : PH_SEL;   // (a level-2 interval is one key wide: not reached)
+      else s.phase = LEVEL == kLastLevel ? PH_SLOW : PH_SEL;   // (a last-level interval is one key wide)
     }
     st[b] = s;
   }
@@ -1963,6 +2007,7 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
   if ((rc = select_level<0>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   if ((rc = select_level<1>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   if ((rc = select_level<2>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
+  if ((rc = select_level<3>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
   return check_launch("select");
 }

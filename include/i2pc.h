@@ -96,7 +96,7 @@ int i2pc_unproject(const float* depth, int dep_h, int dep_w,
  *              (row 0 = NaN count | -Inf count << 32, row 1 = non-finite count,
  *               rows 2-3 = finite key range; passed at level 0 only)
  * and return 0 (non-zero aborts the call).  Every rank must make the same sequence of
- * calls (3 per image, one per selection level; band runs take the histogram levels).
+ * calls (4 per image, one per selection level; band runs take the histogram levels).
  * image_band : uint8 [row1 - row0, img_w, channels]   the band's rows of the image
  * xyz_band   : float32 [Nb, 3], rgb_band uint8 [Nb, 3] with Nb = (ceil(row1/step) -
  *              row0/step) * ceil(img_w/step): the band's points, row-major, i.e. the

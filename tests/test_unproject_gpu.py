@@ -288,6 +288,26 @@ def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole"
     return whole
 
 
+@pytest.mark.parametrize("zero_frac,shape", [(0.03, (384, 384, 1024, 1024)), (0.03, (96, 128, 600, 800)),
+                                              (0.5, (384, 384, 1024, 1024)), (0.9, (64, 64, 300, 300))])
+def test_selection_with_a_spike_of_equal_values(zero_frac, shape):
+    """Depth maps whose p2 (or p98) rank falls inside a block of exactly equal values -- a ReLU
+    network's zero floor: the target's level-0 bin holds more keys than a candidate list, so the
+    histogram levels must resolve it.  Whole-image and 3-band results bit-exact with the oracle."""
+    h, w, H, W = shape
+    dep = _smooth_depth(h, w, 101)
+    rng = np.random.Generator(np.random.PCG64(102))
+    blocks = 0
+    while (dep == 0).mean() < zero_frac:       # square zero blocks -> exact zeros after the resize
+        y, x = rng.integers(0, h - 7), rng.integers(0, w - 7)
+        dep[y:y + 8, x:x + 8] = 0.0
+        blocks += 1
+    img = _rgb(H, W, 103)
+    whole = _band_check(dep, img, 3, "high", depth_scale=10.0)
+    ep, ec = ref.depth_to_point_cloud(img, dep, density="high", depth_scale=10.0, loop=False)
+    assert _same_bits(whole.xyz[0].cpu().numpy(), ep), _first_diff(whole.xyz[0].cpu().numpy(), ep)
+
+
 @pytest.mark.parametrize("density", ["high", "low"])
 def test_equirect_projection_matches_oracle_and_bands(density):
     """Equirectangular mode (C4 panoramas; not in the reference, so parity is against the

@@ -1,6 +1,6 @@
 """Selection-state dump after one geometry call: per image the level-0 windows, candidate
 counts and the targets' key intervals (SelState words; layout of csrc/unproject.hip).
-    python tools/debug_select.py [B] [--nan] [--band]"""
+    python tools/debug_select.py [B] [--nan] [--band] [--net]   (--net: DPT-Large depth of random images)"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
@@ -19,6 +19,18 @@ if "--nan" in sys.argv:
     dep[:, 7, 11] = np.nan
 img = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev)
 d = torch.from_numpy(dep).to(dev)
+if "--net" in sys.argv:
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    import bench
+    img = bench._images(B, H, 0, dev)          # the bench's images (PCG64 seeds 1000 + i)
+    pipe = PointCloudPipeline(B, H, W, device=dev)
+    d = pipe.infer_depth(img).clone()
+    torch.cuda.synchronize()
+    x = d[0].flatten().double().cpu().numpy()
+    q = np.percentile(x, [0, 1, 2, 5, 25, 50, 75, 95, 98, 99, 100])
+    print("depth[0] percentiles 0/1/2/5/25/50/75/95/98/99/100:", np.array2string(q, precision=5))
+    hist, _ = np.histogram(x, bins=2048, range=(x.min(), x.max()))
+    print("model map: max L0-bin share", hist.max() / x.size, "bins holding 50%:", int(np.searchsorted(np.cumsum(np.sort(hist)[::-1]), x.size / 2)) + 1)
 ws = torch.zeros(geometry.workspace_bytes(B, H, W), dtype=torch.uint8, device=dev)
 if band:
     comm = RcclComm(nranks=1, rank=0)
@@ -30,6 +42,9 @@ W32 = 108
 st = ws[: B * W32 * 4].view(torch.int32).cpu().numpy().view(np.uint32).reshape(B, W32)
 for b in range(B):
     r = st[b]
+    if "--net" in sys.argv and r[9] == 0 and all(x == 0xffffffff for x in r[50:54]) and B > 4:
+        print(f"b{b} ok phase={r[0]} wbin={list(map(int, r[12:16]))} ccount={list(map(int, r[76:78]))}")
+        continue
     print(f"b{b} phase={r[0]} n={r[1]} nan={r[2]} nonfin={r[3]} ntgt={r[8]} nslot={r[9]} nwin={r[10]} fill={r[11]} "
           f"wbin={list(map(int, r[12:18]))} ninf={int(r[18])},{int(r[19])} ccount={list(map(int, r[76:80]))}")
     print("   tlo", [hex(x) for x in r[30:40]])
