@@ -85,7 +85,7 @@ struct alignas(16) SelState {
   float med;
   int32_t mode;            // 0: float64 branch, 1: float32 min/max branch, 2: constant
   uint32_t err;
-  uint32_t pad1;
+  uint32_t level;          // last selection level that worked on the image (diagnostics)
   double p2, p98, den64;
   float lo32, hi32, den32, pad2;
   uint32_t bbox_key[6];
@@ -390,10 +390,10 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
   }
 }
 
-// Level-0 histogram of each model-resolution map (finite values, the level-0 binning), into
+// Level-0 histogram of a sample of each full-resolution map (finite values, the level-0 binning), into
 // histogram slot 3 (unused at level 0): the estimate k_window predicts the target bins from.
-__global__ __launch_bounds__(kBlock) void k_model_hist(const float* depth, int B, int m, SelState* st, uint32_t* hist,
-                                                       const uint32_t* rpart) {
+__global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* hist,
+                                                       const uint32_t* rpart, int stride) {
   __shared__ uint32_t lh[kBins];
   __shared__ uint32_t rr[2];
   const int b = blockIdx.x % B, c = blockIdx.x / B;
@@ -415,21 +415,30 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(const float* depth, int B
   }
   __syncthreads();
   const VBins vb = level0_vbins(rr[0], rr[1]);
-  // each thread bins a contiguous run of the chunk (neighbouring values share bins: one LDS
-  // atomic per run of equal bins), loads issued 8 at a time
-  const float* D = depth + (size_t)b * m;
-  const int per = (m + kRangeChunks - 1) / kRangeChunks;
-  const int i0 = c * per, i1 = min(m, i0 + per);
+  // the histogram of a regular sample of the FULL-resolution map (every stride-th row and
+  // column, values recomputed with the cv2 taps): its quantiles are the full map's up to
+  // sampling noise, unlike the model pixels' (a zero floor of isolated model pixels all but
+  // vanishes in the resize).  Each thread bins a contiguous run of samples (neighbours share
+  // bins: one LDS atomic per run).
+  const int nsx = (g.W + stride - 1) / stride, nsy = (g.H + stride - 1) / stride, ns = nsx * nsy;
+  const int per = (ns + kRangeChunks - 1) / kRangeChunks;
+  const int i0 = c * per, i1 = min(ns, i0 + per);
   const int tper = (per + kBlock - 1) / kBlock;
   const int t0 = i0 + threadIdx.x * tper, t1 = min(i1, t0 + tper);
   int run = -1;
   uint32_t cnt = 0;
-  for (int i = t0; i < t1; i += 8) {
-    float v[8];
+  for (int i = t0; i < t1; i += 4) {
+    float v[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = D[min(i + k, t1 - 1)];
+    for (int k = 0; k < 4; ++k) {
+      // jittered lattice: the offset inside each stride x stride cell cycles with the cell, so
+      // every residue of the cv2 tap pattern (single-tap columns/rows included) is sampled
+      const int si = min(i + k, t1 - 1), sy = si / nsx, sx = si - sy * nsx;
+      const int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
+      v[k] = sample(g, b, min(sy * stride + jy, g.H - 1), min(sx * stride + jx, g.W - 1));
+    }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 4; ++k) {
       const int bn = (i + k < t1 && isfinite(v[k])) ? (int)vbin(v[k], vb) : -1;
       if (bn != run && run >= 0) atomicAdd(&lh[run], cnt);
       cnt = (bn == run ? cnt : 0u) + 1u;
@@ -878,8 +887,8 @@ __device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint3
   __syncthreads();
 }
 
-// Speculative level-0 windows.  The full-resolution map is a bilinear resize of the model
-// map, so its p2 / p98 fall near the model map's: around the model map's bin of each quantile,
+// Speculative level-0 windows.  k_model_hist's full-resolution sample has the map's quantiles up
+// to sampling noise: around the sample's bin of each quantile,
 // a run of level-0 bins expected to hold about kWinKeys full-resolution keys becomes a window
 // whose keys the level-0 sweep compacts.  When a target's bin lies inside a window (and the
 // window did not overflow), the level-0 resolve selects the exact key from those candidates
@@ -923,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist,
     if (lane >= o) x += y;
   }
   if (lane == 63) wsum[wv] = x;
-  // a model map holding NaN / Inf adds a window at its median (the nanmedian fill)
+  // a sample holding NaN / Inf adds a window at its median (the nanmedian fill); m = samples
   const int nq = (uint32_t)m > mtot ? 3 : 2;
   if (threadIdx.x < 6) wb[threadIdx.x] = (threadIdx.x & 1) ? 0u : (uint32_t)kBins;
   __syncthreads();
@@ -937,7 +946,10 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist,
     for (int i = 0; i < per; ++i) {
       const int bn = threadIdx.x * per + i;
       const double c1 = c + mh[bn];
-      if (c1 > r - h && c <= r + h) { atomicMin(&wb[2 * k], (uint32_t)bn); atomicMax(&wb[2 * k + 1], (uint32_t)bn); }
+      // a bin that alone outgrows the window (a spike such as the zero floor) stays out of it
+      // unless it holds the rank itself (then no window can help; the levels take over)
+      const bool fits = (double)mh[bn] * scale <= (double)kWinKeys || (c <= r && r < c1);
+      if (c1 > r - h && c <= r + h && fits) { atomicMin(&wb[2 * k], (uint32_t)bn); atomicMax(&wb[2 * k + 1], (uint32_t)bn); }
       c = c1;
     }
   }
@@ -1041,6 +1053,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
   if (s.phase != (LEVEL == 0 ? PH_INIT : PH_SEL)) return;
   uint32_t* gh = hist + (size_t)b * kSlots * kBins;
   uint32_t clo[kSlots], chi[kSlots];
+  if (threadIdx.x == 0) s.level = LEVEL;
   if (LEVEL == 0) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2000,9 +2013,11 @@ static int select_level(const Geo& g, SelState* st, uint32_t* hist, uint32_t* ca
 
 static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, const uint32_t* rpart,
                          uint32_t cap, int B, const Sweep& sw, hipStream_t s, const Exchange* x = nullptr) {
-  hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g.depth, B, g.dh * g.dw, st, hist,
-                     rpart);
-  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, hist, cap, B, x ? 0 : 1, g.dh * g.dw);
+  // full-resolution sample of ~64 K points per image for the level-0 estimate
+  const int stride = std::max(1, (int)std::sqrt((double)g.H * g.W / 65536.0));
+  const int ns = ((g.H + stride - 1) / stride) * ((g.W + stride - 1) / stride);
+  hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g, B, st, hist, rpart, stride);
+  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, hist, cap, B, x ? 0 : 1, ns);
   int rc;
   if ((rc = select_level<0>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   if ((rc = select_level<1>(g, st, hist, cand, cap, B, sw, s, x))) return rc;

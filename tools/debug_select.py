@@ -26,6 +26,8 @@ if "--net" in sys.argv:
     pipe = PointCloudPipeline(B, H, W, device=dev)
     d = pipe.infer_depth(img).clone()
     torch.cuda.synchronize()
+    if os.environ.get("DBG_SAVE"):
+        np.save(os.environ["DBG_SAVE"], d[[int(x) for x in os.environ.get("DBG_IDX", "6").split(",")]].cpu().numpy())
     x = d[0].flatten().double().cpu().numpy()
     q = np.percentile(x, [0, 1, 2, 5, 25, 50, 75, 95, 98, 99, 100])
     print("depth[0] percentiles 0/1/2/5/25/50/75/95/98/99/100:", np.array2string(q, precision=5))
@@ -43,9 +45,9 @@ st = ws[: B * W32 * 4].view(torch.int32).cpu().numpy().view(np.uint32).reshape(B
 for b in range(B):
     r = st[b]
     if "--net" in sys.argv and r[9] == 0 and all(x == 0xffffffff for x in r[50:54]) and B > 4:
-        print(f"b{b} ok phase={r[0]} wbin={list(map(int, r[12:16]))} ccount={list(map(int, r[76:78]))}")
+        print(f"b{b} ok phase={r[0]} level={r[85]} wbin={list(map(int, r[12:16]))} ccount={list(map(int, r[76:78]))}")
         continue
-    print(f"b{b} phase={r[0]} n={r[1]} nan={r[2]} nonfin={r[3]} ntgt={r[8]} nslot={r[9]} nwin={r[10]} fill={r[11]} "
+    print(f"b{b} phase={r[0]} level={r[85]} n={r[1]} nan={r[2]} nonfin={r[3]} ntgt={r[8]} nslot={r[9]} nwin={r[10]} fill={r[11]} "
           f"wbin={list(map(int, r[12:18]))} ninf={int(r[18])},{int(r[19])} ccount={list(map(int, r[76:80]))}")
     print("   tlo", [hex(x) for x in r[30:40]])
     print("   thi", [hex(x) for x in r[40:50]])
