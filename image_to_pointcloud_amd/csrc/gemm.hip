@@ -1277,6 +1277,220 @@ __global__ __launch_bounds__(512) void k_gemm_q(Args p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong persistent 256 x 256 x 64 bf16 engine (k_gemm_8p), dense A.
+//
+// LDS: two K-tile buffers of four 16-KB quarters (A-q0, A-q1, B-q0, B-q1 as in k_gemm_q:
+// the 64-row halves mp of both 128-row wave halves, the 32-column halves np of every wave's
+// 64 columns) + per-(parity, wave-row) 1-KB bias copies.  A K-tile is four phases, one
+// (mp, np) quadrant of every wave's 128 x 64 output each, in the order (0,0) (0,1) (1,1) (1,0):
+// phase 1 reads A-q0 + B-q0, phase 2 B-q1, phase 3 A-q1, phase 4 nothing new (A-q1 and the
+// B-q0 fragments from phase 1 stay in registers).  Each phase is two barrier intervals,
+//   R: ds_read the phase's fragments | issue one quarter (2 LDS-DMA per wave) | vmcnt(8) | s_barrier
+//   M: lgkmcnt(0) | 16 MFMAs at priority 1 | s_barrier
+// and wave-row 1 (waves 4-7) runs one interval behind wave-row 0 (one extra barrier at the
+// start; wave-row 0 takes one at the end), so on every SIMD one wave's MFMAs overlap the
+// other's LDS reads and DMA issue.
+// The quarter stream: element e = quarter [A-q0, B-q0, B-q1, A-q1][e & 3] of K-tile e >> 2
+// (counted over the CU's whole tile sequence, buffer = K-tile & 1); global phase k issues
+// element k + 5 (the prologue issues 0..5).  A phase's vmcnt(8) leaves the four youngest
+// elements in flight, i.e. it retires element k + 1, which is first read in phase k + 2 at
+// the earliest (RAW: DMA data is ordered for a ds_read by the issuer's vmcnt and a barrier
+// both wave-rows pass afterwards; with the one-interval stagger a wait in phase k's R
+// interval precedes every read in phases > k).  Refills land at least two phases after the
+// last read of the quarter they overwrite (WAR: the lagging wave-row retires a phase-p read
+// before the barrier that ends interval 2p + 1; the earliest refill is issued in interval
+// 2p + 3).  An epilogue (register-direct, E_ALL memory operations incl. the next tile's
+// bias load) sits between two phases; the four phases after it wait vmcnt(8 + E_ALL).
+// Phases whose element does not exist (the last tile's tail) wait vmcnt(0).
+// The accumulation order of every acc[i][j] is k_gemm_p's (k ascending, s = 0 then 1 per
+// K-tile), so both engines are bit-identical.
+// per-tile operand descriptors: A from the tile's first row (rows past M read as zero), W panel
+struct TileRs { rsrc_t a, w; int m0, n0; };
+__device__ __forceinline__ TileRs tile_rs_8p(const Args& p, int tile) {
+  int tm, tn;
+  grouped(p, tile, tm, tn);
+  TileRs r;
+  r.m0 = tm * 256;
+  r.n0 = tn * 256;
+  r.a = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.A) + (int64_t)r.m0 * p.lda * 2), 0,
+      (uint32_t)((int64_t)(p.M - r.m0) * p.lda * 2), 0x00020000);
+  r.w = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(p.W) + (int64_t)r.n0 * p.ldw * 2), 0,
+      (uint32_t)(256 * p.ldw * 2), 0x00020000);
+  return r;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void k_gemm_8p(Args p) {
+  constexpr int RM = 8, RN = 4, ROWB = 128, QB = 128 * ROWB;
+  constexpr int NRL = EpiCount<EPI>::loads * RN / 4, NS = EpiCount<EPI>::stores;
+  constexpr int E_ALL = RM * (NRL + NS) + 1;
+  constexpr int W_POST = 8 + E_ALL > 63 ? 63 : 8 + E_ALL;
+  constexpr int BIAS_OFF = 8 * QB;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int lrow = lane >> 3, pchunk = lane & 7;
+
+  const int T = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, xl = blockIdx.x >> 3, xq = G >> 3, xr = G & 7;
+  int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + xl;
+  if (t >= T) return;
+
+  // lane parts of this wave's quarter rows (r = wid * 16 + j * 8 + lrow), XOR swizzle on the source
+  const int chunk16 = (pchunk ^ lrow) << 4;
+  uint32_t a_lane[2][2], w_lane[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wid * 16 + j * 8 + lrow;
+      a_lane[q][j] = (uint32_t)((r >> 6) * 128 + q * 64 + (r & 63)) * (uint32_t)(p.lda * 2) + chunk16;
+      w_lane[q][j] = (uint32_t)((r >> 5) * 64 + q * 32 + (r & 31)) * (uint32_t)(p.ldw * 2) + chunk16;
+    }
+  const rsrc_t b_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.bias), 0, p.bias ? p.N * 4 : 0, 0x00020000);
+  auto tile_rs = [&](int tile) { return tile_rs_8p(p, tile); };
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  // quarter (0 A-q0, 1 A-q1, 2 B-q0, 3 B-q1) of the K-tile at k0 into buffer buf
+  auto issue = [&](int buf, int quarter, const TileRs& tr, int k0) {
+    uint8_t* dst = smem + (buf * 4 + quarter) * QB + wid * 16 * ROWB;
+    if (quarter < 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(tr.a, (lds_ptr_t)(dst + j * 8 * ROWB), 16, a_lane[quarter][j], k0 * 2, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(tr.w, (lds_ptr_t)(dst + j * 8 * ROWB), 16, w_lane[quarter - 2][j], k0 * 2, 0, 0);
+    }
+  };
+  // the tile's 256 bias values, one copy per wave-row: wave (wm, wn) loads columns wn * 64 + lane
+  auto load_bias = [&](int par, int n0) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, (lds_ptr_t)(smem + BIAS_OFF + (par * 2 + wm) * 1024 + wn * 256), 4,
+                                              (n0 + wn * 64 + lane) * 4, 0, 0, 0);
+  };
+  auto frag = [&](int buf, int quarter, int row, int s) {
+    const uint8_t* base = smem + (buf * 4 + quarter) * QB + row * ROWB;
+    return *reinterpret_cast<const bf16x8*>(base + (((4 * s + fq) ^ (row & 7)) << 4));
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const rsrc_t c_rs = make_rsrc(p.C);
+  const rsrc_t r_rs = make_rsrc(p.res);
+  const rsrc_t r2_rs = make_rsrc(p.res2);
+  const int nk = p.K / BK;   // >= 2 (plan)
+
+  TileRs cur = tile_rs(t);
+  // prologue: bias, elements 0..5 (K-tile 0 whole, K-tile 1's A-q0 and B-q0)
+  load_bias(0, cur.n0);
+  issue(0, 0, cur, 0); issue(0, 2, cur, 0); issue(0, 3, cur, 0); issue(0, 1, cur, 0);
+  issue(1, 0, cur, BK); issue(1, 2, cur, BK);
+  I2PC_WAIT_VM(8);
+  barrier();
+  if (wm == 1) barrier();
+
+  int g = 0, tpar = 0, post = 0;
+  for (;;) {
+    const int t_next = t + G;
+    const bool has_next = t_next < T;
+    const TileRs nxt = tile_rs(has_next ? t_next : t);
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = g & 1;
+      // K-tiles kt + 1 (phases 1, 2) and kt + 2 (phases 3, 4): this tile's, the next tile's, or none
+      const bool e1_here = kt + 1 < nk, e2_here = kt + 2 < nk;
+      const bool e1 = e1_here || has_next, e2 = e2_here || has_next;
+      const TileRs& tr1 = e1_here ? cur : nxt;
+      const TileRs& tr2 = e2_here ? cur : nxt;
+      const int k1 = (e1_here ? kt + 1 : kt + 1 - nk) * BK;
+      const int k2 = (e2_here ? kt + 2 : kt + 2 - nk) * BK;
+      bf16x8 af[4][2], b0[2][2], b1[2][2];
+      // a phase's R-interval tail: the wait for element k + 1, then the barrier
+      auto r_wait = [&](bool issued) {
+        if (!issued) I2PC_WAIT_VM(0);
+        else if (post > 0) wait_vm<W_POST>();
+        else I2PC_WAIT_VM(8);
+        if (post > 0) --post;
+        barrier();
+      };
+      auto mfma_quad = [&](auto mpc, auto npc, bf16x8 (&bq)[2][2]) {
+        constexpr int MP = decltype(mpc)::value, NP = decltype(npc)::value;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[MP * 4 + i][NP * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j][s], af[i][s], acc[MP * 4 + i][NP * 2 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        barrier();
+      };
+      // ---- phase 1: (0, 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) af[i][s] = frag(buf, 0, wm * 64 + i * 16 + frow, s);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b0[j][s] = frag(buf, 2, wn * 32 + j * 16 + frow, s);
+      if (e1) issue(buf ^ 1, 3, tr1, k1);
+      r_wait(e1);
+      mfma_quad(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, b0);
+      // ---- phase 2: (0, 1)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) b1[j][s] = frag(buf, 3, wn * 32 + j * 16 + frow, s);
+      if (e1) issue(buf ^ 1, 1, tr1, k1);
+      r_wait(e1);
+      mfma_quad(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, b1);
+      // ---- phase 3: (1, 1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) af[i][s] = frag(buf, 1, wm * 64 + i * 16 + frow, s);
+      if (e2) issue(buf, 0, tr2, k2);
+      r_wait(e2);
+      mfma_quad(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, b1);
+      // ---- phase 4: (1, 0)
+      if (e2) issue(buf, 2, tr2, k2);
+      r_wait(e2);
+      mfma_quad(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}, b0);
+      ++g;
+    }
+    // ---- epilogue of tile (cur.m0, cur.n0): register-direct, counted
+    epilogue_p<RM, RN, EPI, false>(p, acc, cur.m0 + wm * 128, cur.n0 + wn * 64,
+                                   reinterpret_cast<const float*>(smem + BIAS_OFF + (tpar * 2 + wm) * 1024) + wn * 64, c_rs,
+                                   r_rs, r2_rs, c_rs);
+    if (!has_next) break;
+    load_bias(tpar ^ 1, nxt.n0);
+    t = t_next;
+    cur = nxt;
+    tpar ^= 1;
+    post = 4;
+  }
+  if (wm == 0) barrier();   // wave-row 0 is one barrier short of wave-row 1
+}
+
 #undef I2PC_WAIT_VM
 #undef I2PC_LDS_BARRIER
 
@@ -1329,6 +1543,25 @@ static void launch_p(const Args& p, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
 }
 
+template <int EPI>
+static void launch_8p(const Args& p, hipStream_t s) {
+  Args q = p;
+  q.A = p.A + (int64_t)p.a_o * p.lda;
+  q.a_o = 0;
+  q.tiles_m = (p.M + 255) / 256;
+  q.tiles_n = p.N / 256;
+  q.group_m = group_m_for(q.tiles_m);
+  const int smem = 8 * 128 * 128 + 4 * 1024;
+  auto kern = pers::k_gemm_8p<EPI>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int grid = std::min(q.tiles_m * q.tiles_n, num_cus());
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
+}
+
 template <bool CONV, bool RELU_A, int EPI>
 static void launch_q(const Args& p, hipStream_t s) {
   Args q = p;
@@ -1357,15 +1590,19 @@ static void launch_q(const Args& p, hipStream_t s) {
 // Which kernel a call runs: the persistent 256-column engine when the epilogue is one it
 // implements and every byte offset fits its 31-bit buffer range; else the tile kernel.
 struct Plan {
-  int kind;      // 0 tile kernel, 1 persistent engine
+  int kind;      // 0 tile kernel, 1 persistent engine, 2 ping-pong persistent engine
   int bm, bn, epi;
 };
 
 // 0 auto, 1 tile kernel only, 2 persistent engine wherever its epilogue applies;
 // initial value from I2PC_GEMM_P (0 -> 1, 2 -> 2)
+// 3 = automatic without the ping-pong engine, 4 = ping-pong engine wherever it applies
+// (else the persistent engine wherever its epilogue applies)
 static int g_engine = [] {
   const char* e = getenv("I2PC_GEMM_P");
-  return !e ? 0 : atoi(e) == 0 ? 1 : atoi(e) == 2 ? 2 : 0;
+  if (!e) return 0;
+  const int v = atoi(e);
+  return v == 0 ? 1 : (v >= 2 && v <= 4) ? v : 0;
 }();
 
 static int64_t max_row(const Args& p) {
@@ -1418,8 +1655,11 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
     // stage and epilogue behind the neighbouring tiles); at one or two tiles per CU the
     // tile kernel's 128 x 128 configurations quantise better (profiles/r01_gemm_engines.txt).
     const int64_t tiles = (int64_t)((p.M + best - 1) / best) * (p.N / 256);
-    if (pforce == 2 || tiles >= 3 * ncu) {
-      pl = Plan{1, best, 256, epi};
+    // the ping-pong engine (k_gemm_8p): dense A, plain / fp32-residual epilogues, K >= 128
+    const bool can8 = !conv && !relu && (epi == pers::EPI_PLAIN || epi == pers::EPI_RESF32) && p.K >= 128;
+    if (pforce == 4 && can8) return Plan{2, 256, 256, epi};
+    if (pforce == 2 || pforce == 4 || tiles >= 3 * ncu) {
+      pl = Plan{pforce == 0 && can8 ? 2 : 1, best, 256, epi};
       return pl;
     }
   }
@@ -1482,6 +1722,14 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
 
 template <bool CONV, bool RELU_A>
 static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
+  if (pl.kind == 2) {
+    if constexpr (!CONV && !RELU_A) {
+      if (pl.epi == pers::EPI_PLAIN) launch_8p<pers::EPI_PLAIN>(p, s);
+      else launch_8p<pers::EPI_RESF32>(p, s);
+      return check_launch("gemm_8p");
+    }
+    return set_error(I2PC_EUNSUPPORTED, "gemm: no ping-pong variant");
+  }
   if (pl.kind == 1) return run_persistent<CONV, RELU_A>(pl, p, s);
   if (pl.kind < 0) return set_error(I2PC_EUNSUPPORTED, "gemm: N=%d must be a multiple of 32", p.N);
   if (pl.bm == 256 && pl.epi == 64) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
@@ -1499,7 +1747,9 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu) {
   static thread_local char buf[96];
   const char* c = conv ? "true" : "false";
   const char* r = relu ? "true" : "false";
-  if (pl.kind == 1) {
+  if (pl.kind == 2) {
+    snprintf(buf, sizeof buf, "k_gemm_8p<%s>", pl.epi == pers::EPI_PLAIN ? "plain" : "res_f32");
+  } else if (pl.kind == 1) {
     static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT"};
     if (g_quarter && pl.epi != pers::EPI_CT) snprintf(buf, sizeof buf, "k_gemm_q<%s, %s, %s>", c, r, epis[pl.epi]);
     else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
@@ -1683,7 +1933,9 @@ extern "C" const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* d) {
 
 extern "C" int i2pc_gemm_set_engine(int mode) {
   clear_error();
-  I2PC_REQUIRE(mode >= 0 && mode <= 2, "gemm engine mode %d (0 auto, 1 tile kernel only, 2 persistent wherever it applies)", mode);
+  I2PC_REQUIRE(mode >= 0 && mode <= 4,
+               "gemm engine mode %d (0 auto, 1 tile kernel only, 2 persistent wherever it applies, 3 auto without the "
+               "ping-pong engine, 4 ping-pong engine wherever it applies)", mode);
   gemm::g_engine = mode;
   return I2PC_OK;
 }

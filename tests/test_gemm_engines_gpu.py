@@ -1,4 +1,5 @@
-"""The persistent 256-column GEMM engine against the tile kernel (bit-exact) and torch fp32.
+"""The persistent 256-column GEMM engines (single-stage k_gemm_p, ping-pong k_gemm_8p) against the
+tile kernel (bit-exact) and torch fp32.
 
 Both engines accumulate the same MFMA sequence and apply the epilogue in the same
 fp32 order (bias, activation, residual, second residual, bf16 rounding), so their
@@ -26,11 +27,12 @@ def _bf(x):
 
 
 def _both(fn):
-    """(persistent engine forced, tile kernel) outputs; the automatic choice must equal both."""
+    """(persistent engine forced, tile kernel) outputs; the ping-pong engine (k_gemm_8p, forced
+    wherever it applies) and the automatic choice must equal both."""
     ops = _ops()
     outs = []
     try:
-        for mode in (1, 2):
+        for mode in (1, 2, 4):
             ops.set_gemm_engine(mode)
             outs.append(fn().clone())
     finally:
@@ -38,6 +40,8 @@ def _both(fn):
     auto = fn()
     torch.cuda.synchronize()
     assert torch.equal(auto, outs[0]), "automatic engine choice differs from the tile kernel"
+    assert torch.equal(outs[2], outs[0]), \
+        f"ping-pong engine differs from the tile kernel: {(outs[2].float() - outs[0].float()).abs().max().item()}"
     return outs[1], outs[0]
 
 
@@ -57,10 +61,13 @@ def test_linear_plain_engines_bitexact(M, N, K, act):
     b = torch.randn(N, generator=g).to(dev)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     got, ref = _both(lambda: ops.linear(x, w, bias=b, act=act, out=out))
-    ops.set_gemm_engine(2)
     try:
+        ops.set_gemm_engine(2)
         lab = ops.gemm_kernel_label(_desc_of(ops, x, w, b, out))
         assert "k_gemm_p" in lab or "k_gemm_q" in lab, "persistent engine not selected"
+        ops.set_gemm_engine(4)
+        lab = ops.gemm_kernel_label(_desc_of(ops, x, w, b, out))
+        assert ("k_gemm_8p" in lab) == (K >= 128), lab
     finally:
         ops.set_gemm_engine(0)
     assert torch.equal(got, ref), f"engines differ: {(got.float() - ref.float()).abs().max().item()}"
