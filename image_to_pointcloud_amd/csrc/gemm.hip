@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace i2pc {
@@ -1596,8 +1597,8 @@ struct Plan {
 
 // 0 auto, 1 tile kernel only, 2 persistent engine wherever its epilogue applies;
 // initial value from I2PC_GEMM_P (0 -> 1, 2 -> 2)
-// 3 = automatic without the ping-pong engine, 4 = ping-pong engine wherever it applies
-// (else the persistent engine wherever its epilogue applies)
+// 3 = automatic with the ping-pong engine where the persistent engine would run, 4 = ping-pong
+// engine wherever it applies (else the persistent engine wherever its epilogue applies)
 static int g_engine = [] {
   const char* e = getenv("I2PC_GEMM_P");
   if (!e) return 0;
@@ -1659,7 +1660,9 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
     const bool can8 = !conv && !relu && (epi == pers::EPI_PLAIN || epi == pers::EPI_RESF32) && p.K >= 128;
     if (pforce == 4 && can8) return Plan{2, 256, 256, epi};
     if (pforce == 2 || pforce == 4 || tiles >= 3 * ncu) {
-      pl = Plan{pforce == 0 && can8 ? 2 : 1, best, 256, epi};
+      // the single-stage engine by default: in the DPT-Large step the ping-pong engine measured
+      // 1.6 % slower end to end (tools/ab_pipeline.py), though equal or faster in isolation
+      pl = Plan{pforce == 3 && can8 ? 2 : 1, best, 256, epi};
       return pl;
     }
   }
@@ -1720,8 +1723,42 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
   return check_launch("gemm");
 }
 
+// Round quantisation of the persistent engines: T 256 x 256 tiles take ceil(T / CUs) rounds.
+// When a whole number of rounds covers whole M-tile rows and the remaining rows fit one round
+// of 256 x 128 tiles (half the work each), run those rows as a second, BN = 128 launch
+// (e.g. M = 18464, N = 3072: 3 rounds + a half round instead of 4).  Plain dense epilogue
+// with a linear output row map only; the two parts compute every output exactly as one launch
+// would (same per-output accumulation order).  I2PC_GEMM_TAIL=0 disables it.
+static int g_tail = [] { const char* e = getenv("I2PC_GEMM_TAIL"); return e ? atoi(e) : 1; }();
+static bool tail_split(const Args& p, int& ma) {
+  if (!g_tail || p.o_g != 0 || p.a_g != 0 || p.ct_s > 0 || p.N % 256 != 0) return false;
+  const int64_t tn = p.N / 256, tm = (p.M + 255) / 256, T = tm * tn, G = num_cus();
+  const int64_t rounds = T / G;
+  if (T % G == 0 || rounds < 1 || (rounds * G) % tn != 0) return false;
+  const int64_t mt = rounds * G / tn;
+  if (mt >= tm) return false;
+  const int64_t half_tiles = (tm - mt) * 2 * tn;
+  if (half_tiles > G) return false;
+  ma = (int)(mt * 256);
+  return true;
+}
+
 template <bool CONV, bool RELU_A>
 static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
+  if constexpr (!CONV && !RELU_A) {
+    int ma = 0;
+    if ((pl.kind == 1 || pl.kind == 2) && pl.epi == pers::EPI_PLAIN && !g_quarter && tail_split(p, ma)) {
+      Args pa = p, pb = p;
+      pa.M = ma;
+      pb.M = p.M - ma;
+      pb.a_o = p.a_o + ma;
+      pb.o_o = p.o_o + ma;
+      if (pl.kind == 2) launch_8p<pers::EPI_PLAIN>(pa, s);
+      else launch_p<256, false, false, pers::EPI_PLAIN>(pa, s);
+      launch_p<256, false, false, pers::EPI_PLAIN, 128>(pb, s);
+      return check_launch("gemm (tail split)");
+    }
+  }
   if (pl.kind == 2) {
     if constexpr (!CONV && !RELU_A) {
       if (pl.epi == pers::EPI_PLAIN) launch_8p<pers::EPI_PLAIN>(p, s);
@@ -1934,8 +1971,14 @@ extern "C" const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* d) {
 extern "C" int i2pc_gemm_set_engine(int mode) {
   clear_error();
   I2PC_REQUIRE(mode >= 0 && mode <= 4,
-               "gemm engine mode %d (0 auto, 1 tile kernel only, 2 persistent wherever it applies, 3 auto without the "
+               "gemm engine mode %d (0 auto, 1 tile kernel only, 2 persistent wherever it applies, 3 auto with the "
                "ping-pong engine, 4 ping-pong engine wherever it applies)", mode);
   gemm::g_engine = mode;
   return I2PC_OK;
+}
+
+// process-wide tuning knobs (i2pc_set_tuning): "gemm_tail" (round-quantisation split on/off)
+bool i2pc_gemm_tune(const char* name, int value) {
+  if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
+  return false;
 }

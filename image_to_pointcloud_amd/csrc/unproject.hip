@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <cmath>
 
 #pragma clang fp contract(off)
@@ -496,6 +497,8 @@ struct Sweep {
   int row_end;   // one past the last output row swept
   int ntiles;    // selection sweeps: column tiles of kTileW per row block (others: 1)
   int raw;       // selection sweeps: raw model rows staged in LDS before interpolation
+  int tpr;       // k_unproject_rows: threads per point row (a multiple of 64; kBlock / tpr rows per pass)
+  int nt;        // k_unproject_rows: non-temporal output stores
 };
 
 __device__ __forceinline__ void map_rows(int bid, int B, int nrb, int& b, int& rb) { map_block(bid, B, nrb, b, rb); }
@@ -1774,6 +1777,229 @@ __global__ __launch_bounds__(kBlock) void k_unproject_fast(Geo g, const SelState
   }
 }
 
+// Wave-uniform copies (SGPRs) of values every lane loaded from the same address: the branches
+// on them become scalar and the fp64 constants stay out of VGPRs.
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+__device__ __forceinline__ double uni(double x) {
+  const uint64_t u = __double_as_longlong(x);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// Row-sweep unprojection (fast path with a resized map): workgroup = image b x point rows
+// [r0, r1) x one column tile of 4 * tpr points (tpr = threads per row, a multiple of 64, so a
+// wave stays inside one row; kBlock / tpr rows per pass); thread t owns points 4c..4c+3
+// (c = t % tpr) of the tile in rows r0 + t / tpr + k * (kBlock / tpr), so its x taps,
+// (u - cx) and column offsets are computed once.  The model rows the
+// block spans are staged in LDS and interpolated horizontally once (cv2's first pass, the
+// right-border single tap copied exactly) into per-thread 16-B slots; a point then costs one
+// 16-B LDS read per model row pair, the vertical blend, the nanmedian fill, the normalisation
+// (uniform branch) and the projection.  RGB of the next row is in flight while a row is
+// computed; each wave's 256 points leave through LDS as contiguous 1 KB / 256 B stores.
+// Same arithmetic, in the same order, as k_unproject_fast / k_unproject (bit-identical).
+constexpr int kRowsPT = 8;   // k_unproject_rows: point rows per thread and workgroup (rows_plan)
+
+template <int STEP>
+__global__ __launch_bounds__(kBlock) void k_unproject_rows(Geo g, const SelState* st, const uint8_t* img, int B,
+                                                           Sweep sw, int invert, Cam cam, float* xyz, uint8_t* rgb,
+                                                           SelState* stw) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
+  __shared__ uint32_t red[6][4];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int b, blk;
+  map_rows(blockIdx.x, B, sw.nrb * sw.ntiles, b, blk);
+  b = uni(b);
+  const int rb = uni(blk / sw.ntiles), ct = uni(blk - (blk / sw.ntiles) * sw.ntiles);
+  const SelState* S = st + b;
+  Norm nm;
+  nm.mode = uni(S->mode);
+  nm.invert = invert;
+  nm.p2 = uni(S->p2);
+  nm.p98 = uni(S->p98);
+  nm.den64 = uni(S->den64);
+  nm.rden64 = uni(S->rden64);
+  nm.lo32 = uni(S->lo32);
+  nm.hi32 = uni(S->hi32);
+  nm.den32 = uni(S->den32);
+  const bool fill = uni((int)S->has_med) != 0;
+  const float med = uni(S->med);
+  const int Hn = cam.N / cam.Wn;
+  const int r0 = sw.row0 + rb * sw.R;
+  const int r1 = min(min(Hn, sw.row_end), r0 + sw.R);
+  const int tpr = sw.tpr, rpp = kBlock / tpr;
+  const int c0 = ct * 4 * tpr;
+  const int ncol = min(4 * tpr, cam.Wn - c0);
+  const int lo = ytap(g, r0 * STEP).i0;
+  const int nrows = ytap(g, (r1 - 1) * STEP).i1 - lo + 1;
+  // LDS: [horizontally interpolated rows: lds_rows x kBlock float4] then, in turn, the raw model
+  // rows (until the horizontal pass is done) and each wave's store staging (rows_plan)
+  float4* hrow = reinterpret_cast<float4*>(smem_u);   // [row][thread]
+  float* raw = reinterpret_cast<float*>(hrow + sw.lds_rows * kBlock);
+  float4* sx = reinterpret_cast<float4*>(raw) + wid * 192;                          // 3 KB per wave
+  uint32_t* sc = reinterpret_cast<uint32_t*>(reinterpret_cast<float4*>(raw) + 4 * 192) + wid * 192;
+
+  const int tcol = (int)threadIdx.x % tpr, trow = (int)threadIdx.x / tpr;
+  const int t4 = 4 * tcol;
+  const bool act = trow < rpp && t4 < ncol;
+  const int ub = c0 + (act ? t4 : 0);                  // first point column of this thread
+  const int rfirst = trow < rpp ? r0 + trow : r1;   // waves past rpp * tpr threads: idle
+  const int nrt = rfirst < r1 ? (r1 - rfirst + rpp - 1) / rpp : 0;   // rows of this thread (<= kRowsPT)
+  const size_t img_base = (size_t)b * g.H * g.W;
+  auto load_rgb = [&](int row, uint32_t (&q)[4][3]) {
+    const int v = row * STEP;
+    if (STEP == 1) {
+      const uint32_t* p32 = reinterpret_cast<const uint32_t*>(img + (img_base + (size_t)v * g.W + ub) * 3);
+      q[0][0] = p32[0]; q[0][1] = p32[1]; q[0][2] = p32[2];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint8_t* px = img + (img_base + (size_t)v * g.W + (ub + j) * STEP) * 3;
+        q[j][0] = px[0]; q[j][1] = px[1]; q[j][2] = px[2];
+      }
+    }
+  };
+  // STEP 1: the RGB of all of this thread's rows is requested first, so the HBM latency of the
+  // cold image overlaps the model-row staging and the horizontal pass; else one row ahead
+  constexpr int PF = STEP == 1 ? kRowsPT : 1;
+  uint32_t qa[PF][4][3];
+  if (STEP == 1) {
+#pragma unroll
+    for (int k = 0; k < PF; ++k)
+      if (k < nrt) load_rgb(rfirst + k * rpp, qa[k]);
+  } else if (nrt > 0) {
+    load_rgb(rfirst, qa[0]);
+  }
+  stage_floats(raw, g.depth + ((size_t)b * g.dh + lo) * g.dw, nrows * g.dw);
+  __syncthreads();
+  int ui[4];
+  double du[4];
+  Tap tx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ui[j] = (ub + j) * STEP;
+    du[j] = (double)ui[j] - cam.cx;
+    tx[j] = xtap(g, ui[j]);
+  }
+  // cv2's horizontal pass over the staged rows, this thread's four columns
+  for (int r = 0; r < nrows; ++r) {
+    const float* rr = raw + r * g.dw;
+    float h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a0 = rr[tx[j].i0];
+      h[j] = tx[j].i1 < 0 ? a0 : a0 * tx[j].w0 + rr[tx[j].i1] * tx[j].w1;
+    }
+    hrow[r * kBlock + threadIdx.x] = make_float4(h[0], h[1], h[2], h[3]);
+  }
+  __syncthreads();   // the raw rows are dead: their LDS becomes the store staging
+
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int k = 0; k < kRowsPT; ++k) {
+    if (k >= nrt) break;
+    const int row = rfirst + k * rpp;
+    uint32_t q[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) q[j][c] = qa[STEP == 1 ? k : 0][j][c];
+    if (STEP != 1 && k + 1 < nrt) load_rgb(row + rpp, qa[0]);
+    const int v = row * STEP;
+    const Tap ty = ytap(g, v);
+    const float4 h0 = hrow[(ty.i0 - lo) * kBlock + threadIdx.x];
+    const float4 h1 = hrow[(ty.i1 - lo) * kBlock + threadIdx.x];
+    const float hv0[4] = {h0.x, h0.y, h0.z, h0.w}, hv1[4] = {h1.x, h1.y, h1.z, h1.w};
+    const double dv = (double)v - cam.cy;
+    uint32_t pc[4][3];   // [point][r,g,b] (source is BGR)
+    if (STEP == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int byte = 3 * j + (2 - c);
+          pc[j][c] = (q[0][byte >> 2] >> (8 * (byte & 3))) & 0xffu;
+        }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { pc[j][0] = q[j][2]; pc[j][1] = q[j][1]; pc[j][2] = q[j][0]; }
+    }
+    float px[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float val = hv0[j] * ty.w0 + hv1[j] * ty.w1;
+      if (fill && !isfinite(val)) val = med;
+      const double d = normalize(val, nm);
+      if (cam.proj == 1) {
+        project(d, v, ui[j], cam, px[j][0], px[j][1], px[j][2]);
+      } else {                                             // project(), pinhole, (u - cx) hoisted
+        const double zd = d * cam.scale;
+        const double zz = zd != 0.0 ? zd : 1e-6;
+        px[j][0] = (float)div_rn(du[j] * zz, cam.f, cam.rf);
+        px[j][1] = (float)div_rn(dv * zz, cam.f, cam.rf);
+        px[j][2] = (float)zd;
+      }
+    }
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { mn[c] = fminf(mn[c], px[j][c]); mx[c] = fmaxf(mx[c], px[j][c]); }
+    }
+    // the wave's 256 consecutive points through LDS: contiguous 1 KB (xyz) / 256 B (rgb) stores
+    float4* wx = sx;
+    uint32_t* wc = sc;
+    wx[lane * 3 + 0] = make_float4(px[0][0], px[0][1], px[0][2], px[1][0]);
+    wx[lane * 3 + 1] = make_float4(px[1][1], px[1][2], px[2][0], px[2][1]);
+    wx[lane * 3 + 2] = make_float4(px[2][2], px[3][0], px[3][1], px[3][2]);
+    wc[lane * 3 + 0] = pc[0][0] | (pc[0][1] << 8) | (pc[0][2] << 16) | (pc[1][0] << 24);
+    wc[lane * 3 + 1] = pc[1][1] | (pc[1][2] << 8) | (pc[2][0] << 16) | (pc[2][1] << 24);
+    wc[lane * 3 + 2] = pc[2][2] | (pc[3][0] << 8) | (pc[3][1] << 16) | (pc[3][2] << 24);
+    __builtin_amdgcn_wave_barrier();
+    const int wp = (tcol >> 6) * 256;                          // first point of this wave in the tile
+    const size_t o = (size_t)b * cam.N + (size_t)row * cam.Wn + c0 + wp;
+    float4* dx = reinterpret_cast<float4*>(xyz + o * 3);
+    uint32_t* dc = reinterpret_cast<uint32_t*>(rgb + o * 3);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int f = k * 64 + lane;
+      if (wp + (f / 3) * 4 < ncol) {      // streamed once: non-temporal (sw.nt) or default policy
+        const float4 vx = wx[f];
+        if (sw.nt) {
+          __builtin_nontemporal_store(vx.x, &dx[f].x);
+          __builtin_nontemporal_store(vx.y, &dx[f].y);
+          __builtin_nontemporal_store(vx.z, &dx[f].z);
+          __builtin_nontemporal_store(vx.w, &dx[f].w);
+          __builtin_nontemporal_store(wc[f], &dc[f]);
+        } else {
+          dx[f] = vx;
+          dc[f] = wc[f];
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  uint32_t kk[6];
+  for (int c = 0; c < 3; ++c) {
+    const bool any = mn[c] <= mx[c];
+    kk[2 * c] = any ? f2key(mn[c]) : 0xffffffffu;
+    kk[2 * c + 1] = any ? f2key(mx[c]) : 0u;
+  }
+  for (int c = 0; c < 6; ++c) {
+    uint32_t x = (c & 1) ? wave_max_u32(kk[c]) : wave_min_u32(kk[c]);
+    if (lane == 0) red[c][wid] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int c = threadIdx.x;
+    uint32_t x = red[c][0];
+    for (int w = 1; w < kBlock / 64; ++w) x = (c & 1) ? max(x, red[c][w]) : min(x, red[c][w]);
+    uint32_t* dst = &stw[b].bbox_key[c];
+    if (c & 1) { if (x) atomicMax(dst, x); }
+    else { if (x != 0xffffffffu) atomicMin(dst, x); }
+  }
+}
+
 // Smooth path (app.py:209-214): materialise the normalised field, blur, unproject.
 __global__ void k_norm_field(Geo g, const SelState* st, int B, int invert, double* field) {
   const size_t n = (size_t)g.H * g.W;
@@ -1929,6 +2155,35 @@ static Sweep plan_sweep(int rows_out, int step, int dh, int dw, int H, bool same
 }
 
 static size_t sweep_lds(const Sweep& sw, int dw) { return sw.lds_rows ? (size_t)sw.lds_rows * dw * sizeof(float) : 0; }
+
+// k_unproject_rows knobs (I2PC_UNP_ROWS / _NT / _RPT, or i2pc_set_tuning "unp_rows" / "unp_nt" / "unp_rpt")
+static int env_int(const char* name, int dflt) { const char* e = getenv(name); return e ? atoi(e) : dflt; }
+static int g_unp_rows = env_int("I2PC_UNP_ROWS", 1);
+static int g_unp_nt = env_int("I2PC_UNP_NT", 1);
+static int g_unp_rpt = env_int("I2PC_UNP_RPT", kRowsPT);
+
+// k_unproject_rows geometry: column tiles of 4 * tpr points (tpr a multiple of 64, <= kBlock),
+// 8192 points per workgroup where the rows allow, LDS = staged model rows + one 16-B slot per
+// thread and model row (<= 64 KiB; false: use k_unproject_fast).  I2PC_UNP_ROWS=0 disables it.
+static bool rows_plan(int Hn, int step, int dh, int dw, int H, int Wn, int prow0, int prow1, Sweep& sr, size_t& lds) {
+  const int enabled = g_unp_rows, nt = g_unp_nt, rpt = std::max(1, std::min(kRowsPT, g_unp_rpt));
+  if (!enabled) return false;
+  const int tpr = std::min(kBlock, (((std::min(Wn, 4 * kBlock) + 3) / 4 + 63) / 64) * 64);
+  const int rpp = kBlock / tpr;
+  int target = std::max(rpp, std::min(rpt * rpp, (8192 / (4 * tpr)) / rpp * rpp));
+  for (; target >= 1; target = target > rpp ? target / 2 : target - rpp) {
+    sr = plan_sweep(Hn, step, dh, dw, H, false, target, prow0, prow1);
+    if (sr.lds_rows <= 0) return false;
+    lds = (size_t)sr.lds_rows * kBlock * 16 +
+          std::max(((size_t)sr.lds_rows * dw * sizeof(float) + 15) / 16 * 16, (size_t)(kBlock / 64) * 192 * 20);
+    if (lds <= 64 * 1024) break;
+  }
+  if (target < 1 || lds > 64 * 1024) return false;
+  sr.tpr = tpr;
+  sr.nt = nt;
+  sr.ntiles = (Wn + 4 * tpr - 1) / (4 * tpr);
+  return true;
+}
 
 // Tile-parallel mode: the level-0 counters a sweep accumulates, out of / back into the
 // per-image state, as int64 [4][B] = {nan counts, non-finite counts, min key, max key}
@@ -2138,6 +2393,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   const size_t unp_lds = sweep_lds(sunp, dep_w);
   const double* field = nullptr;
   const bool fast = !params->smooth && channels == 3 && cam.N % 4 == 0 && cam.Wn % 4 == 0;
+  Sweep sr{};
+  size_t lr = 0;
   if (params->smooth) {
     double* f0 = reinterpret_cast<double*>(ws + L.field);
     double* f1 = reinterpret_cast<double*>(ws + L.tmp);
@@ -2149,6 +2406,16 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
     field = f0;
     hipLaunchKernelGGL((k_unproject<true>), dim3(batch * sunp.nrb), dim3(kBlock), 0, s, g, st, field, image,
                        channels, batch, sunp, params->invert, cam, xyz, rgb, st);
+  } else if (fast && !g.same && rows_plan(Hn, step, dep_h, dep_w, img_h, cam.Wn, prow0, prow1, sr, lr)) {
+    prof_mark(0, s);
+    const dim3 grid(batch * sr.nrb * sr.ntiles), block(kBlock);
+    if (step == 1)
+      hipLaunchKernelGGL((k_unproject_rows<1>), grid, block, lr, s, g, st, image, batch, sr, params->invert, cam, xyz, rgb, st);
+    else if (step == 2)
+      hipLaunchKernelGGL((k_unproject_rows<2>), grid, block, lr, s, g, st, image, batch, sr, params->invert, cam, xyz, rgb, st);
+    else
+      hipLaunchKernelGGL((k_unproject_rows<4>), grid, block, lr, s, g, st, image, batch, sr, params->invert, cam, xyz, rgb, st);
+    prof_mark(1, s);
   } else if (fast) {
     // 8 rows of 1024 points (or the equivalent) per workgroup
     static const int pts_per_wg = [] { const char* e = getenv("I2PC_UNP_PTS"); return e ? atoi(e) : 8192; }();
@@ -2245,4 +2512,11 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
   hipLaunchKernelGGL(k_preview, dim3(blocks), dim3(256), 0, s, depth, st, batch, n, invert ? 1 : 0, lut_bgr, out_bgr);
   if (stats) hipLaunchKernelGGL(k_finalize, dim3((batch + 63) / 64), dim3(64), 0, s, st, batch, nullptr, stats);
   return check_launch("depth_preview");
+}
+
+bool i2pc_unproject_tune(const char* name, int value) {
+  if (std::strcmp(name, "unp_rows") == 0) { i2pc::unproj::g_unp_rows = value; return true; }
+  if (std::strcmp(name, "unp_nt") == 0) { i2pc::unproj::g_unp_nt = value; return true; }
+  if (std::strcmp(name, "unp_rpt") == 0) { i2pc::unproj::g_unp_rpt = value; return true; }
+  return false;
 }

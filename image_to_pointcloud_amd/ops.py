@@ -40,6 +40,7 @@ class GemmDesc(ctypes.Structure):
 _lib.register("i2pc_gemm", ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p])
 _lib.register("i2pc_gemm_kernel_name", ctypes.c_char_p, [ctypes.POINTER(GemmDesc)])
 _lib.register("i2pc_gemm_set_engine", ctypes.c_int, [ctypes.c_int])
+_lib.register("i2pc_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
 _lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
                                                ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_attention", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -116,8 +117,14 @@ def gemm_kernel_label(desc: GemmDesc) -> str:
     return _lib.load().i2pc_gemm_kernel_name(ctypes.byref(desc)).decode()
 
 
+def set_tuning(name: str, value: int) -> None:
+    """Kernel-selection knob (i2pc_set_tuning): gemm_tail, unp_rows, unp_nt, unp_rpt."""
+    _lib.call("i2pc_set_tuning", name.encode(), int(value))
+
+
 def set_gemm_engine(mode: int) -> None:
-    """0 = automatic, 1 = tile kernel only, 2 = persistent engine wherever its epilogue applies."""
+    """0 = automatic, 1 = tile kernel only, 2 = persistent engine wherever its epilogue applies,
+    3 = automatic with the ping-pong engine, 4 = ping-pong engine wherever it applies."""
     _lib.call("i2pc_gemm_set_engine", int(mode))
 
 

@@ -276,8 +276,20 @@ const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* desc);
 /* GEMM engine selection (process-wide): 0 = automatic (the persistent 256-column
  * engine for calls with >= 3 tiles per CU whose epilogue it implements, else the
  * tile kernel), 1 = tile kernel only, 2 = persistent engine wherever its epilogue
- * applies.  All produce bit-identical results; tests use this to cross-check them. */
+ * applies, 3 = automatic with the ping-pong persistent engine (k_gemm_8p: dense A,
+ * plain / fp32-residual epilogues, K >= 128) where the persistent engine would run,
+ * 4 = ping-pong engine wherever it applies (else as 2).  All produce bit-identical
+ * results; tests use this to cross-check them. */
 int i2pc_gemm_set_engine(int mode);
+
+/* Process-wide kernel-selection knobs for A/B measurement (not part of the drop-in surface;
+ * every setting computes the same results bit for bit).  Names: "gemm_tail" (1 = split the
+ * last round of a persistent GEMM into 256 x 128 tiles where that saves a round), "unp_rows"
+ * (1 = row-sweep unprojection kernel), "unp_nt" (1 = non-temporal point stores), "unp_rpt"
+ * (point rows per thread of the row-sweep kernel, 1..8).  Defaults come from the I2PC_GEMM_TAIL /
+ * I2PC_UNP_ROWS / I2PC_UNP_NT / I2PC_UNP_RPT environment variables, else 1, 1, 1, 8.  A HIP graph
+ * keeps the kernels it captured: re-capture after changing a knob. */
+int i2pc_set_tuning(const char* name, int value);
 
 /* LayerNorm over the last dim: x fp32 [rows][dim] (row stride ldx) -> y bf16 [rows][dim]
  * (row stride ldy); gamma/beta fp32 [dim]; two-pass mean/variance in fp32.

@@ -1,6 +1,6 @@
 """A/B of GEMM engine modes on the DPT-Large (batch 32) linear shapes, interleaved rounds in one
-process (cdna_hip_programming.md rule 24): mode 3 = single-stage persistent k_gemm_p where the
-automatic plan picks a persistent engine, mode 0 = automatic (ping-pong k_gemm_8p there).
+process (cdna_hip_programming.md rule 24): mode 0 = automatic (single-stage persistent k_gemm_p
+where a persistent engine runs), mode 3 = the same plan with the ping-pong k_gemm_8p there.
 Random operands; prints the median / min per mode and the bit-equality of the two outputs."""
 import math, os, statistics, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -11,7 +11,7 @@ dev = torch.device("cuda")
 M = 32 * 577
 shapes = [("qkv", M, 3072, 1024, None), ("fc1", M, 4096, 1024, "gelu"), ("o", M, 1024, 1024, None),
           ("fc2", M, 1024, 4096, None), ("big", 8192, 8192, 4096, None)]
-modes = [int(m) for m in os.environ.get("AB_MODES", "3,0").split(",")]
+modes = [int(m) for m in os.environ.get("AB_MODES", "0,3").split(",")]
 g = torch.Generator(device="cpu").manual_seed(0)
 
 

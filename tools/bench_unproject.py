@@ -23,3 +23,17 @@ t = e0.elapsed_time(e1) / 20 * 1e-3
 N = out.xyz.shape[1]
 byts = B * (4.0 * h * w + 18.0 * N)
 print(f"B={B} {dens}: {t*1e6:.1f} us/call, {B*N/t/1e6:.0f} Mpts/s, algorithmic {byts/t/1e9:.0f} GB/s ({byts/t/8e12*100:.1f}% of 8 TB/s)")
+
+# cold caches: a 1 GiB write between calls evicts the L2s and the 256 MiB Infinity Cache, as the
+# network does between two unprojections inside the pipeline step
+flush = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+ts = []
+for _ in range(10):
+    flush.zero_()
+    a = torch.cuda.Event(enable_timing=True); c = torch.cuda.Event(enable_timing=True)
+    a.record()
+    geometry.unproject_batch(d, img, density=dens, out=out)
+    c.record(); torch.cuda.synchronize()
+    ts.append(a.elapsed_time(c) * 1e-3)
+t = sorted(ts)[len(ts) // 2]
+print(f"B={B} {dens} cold: {t*1e6:.1f} us/call (median of 10), {B*N/t/1e6:.0f} Mpts/s, algorithmic {byts/t/1e9:.0f} GB/s")
