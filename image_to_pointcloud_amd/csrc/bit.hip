@@ -28,15 +28,17 @@ __device__ __forceinline__ bf16_t f2bf(float x) {
 
 // out[m][k] for m = (b, oy, ox), k = (ky * 7 + kx) * 3 + c (< 147, zero beyond): input pixel
 // (oy * 2 - pt + ky, ox * 2 - pl + kx) of channel c, zero outside the image
+// I: flat index type, uint32_t when the index space stays below 2^31 (32-bit divisions)
+template <typename I>
 __global__ __launch_bounds__(256) void k_stem_im2col(const float* __restrict__ x, int B, int H, int W, int OH, int OW,
                                                      int pt, int pl, int ks, int kp, bf16_t* __restrict__ out) {
   const int KK = ks * ks * 3;
-  const int64_t total = (int64_t)B * OH * OW * (kp / 8);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / (kp / 8);
-    const int k0 = (int)(i - m * (kp / 8)) * 8;
-    const int b = (int)(m / ((int64_t)OH * OW));
-    const int rem = (int)(m - (int64_t)b * OH * OW);
+  const I total = (I)B * (I)OH * (I)OW * (I)(kp / 8);
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    const I m = i / (I)(kp / 8);
+    const int k0 = (int)(i - m * (I)(kp / 8)) * 8;
+    const int b = (int)(m / ((I)OH * (I)OW));
+    const int rem = (int)(m - (I)b * (I)OH * (I)OW);
     const int oy = rem / OW, ox = rem - (rem / OW) * OW;
     uint32_t w[4];
 #pragma unroll
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(256) void k_stem_im2col(const float* __restrict__ x
       }
       w[e / 2] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     }
-    *reinterpret_cast<uint4*>(out + m * kp + k0) = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint4*>(out + (int64_t)m * kp + k0) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
@@ -239,15 +241,16 @@ __global__ __launch_bounds__(256) void k_gn_apply(GnOperand a, GnOperand r, int 
 
 // 3x3 stride-2 max over the zero-padded map (pad pt top / pl left, zero beyond the
 // bottom/right edge as DynamicPad2d pads there), 8 channels per thread
+template <typename I>
 __global__ __launch_bounds__(256) void k_maxpool(const bf16_t* __restrict__ x, int B, int H, int W, int C, int OH, int OW,
                                                  int pt, int pl, bf16_t* __restrict__ y) {
-  const int cv = C / 8;
-  const int64_t total = (int64_t)B * OH * OW * cv;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  const I cv = (I)(C / 8);
+  const I total = (I)B * (I)OH * (I)OW * cv;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % cv) * 8;
-    const int64_t pix = i / cv;
-    const int b = (int)(pix / ((int64_t)OH * OW));
-    const int rem = (int)(pix - (int64_t)b * OH * OW);
+    const I pix = i / cv;
+    const int b = (int)(pix / ((I)OH * (I)OW));
+    const int rem = (int)(pix - (I)b * (I)OH * (I)OW);
     const int oy = rem / OW, ox = rem - (rem / OW) * OW;
     float m[8];
     bool any_pad = false;
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(256) void k_maxpool(const bf16_t* __restrict__ x, i
     o.y = (uint32_t)f2bf(m[2]) | ((uint32_t)f2bf(m[3]) << 16);
     o.z = (uint32_t)f2bf(m[4]) | ((uint32_t)f2bf(m[5]) << 16);
     o.w = (uint32_t)f2bf(m[6]) | ((uint32_t)f2bf(m[7]) << 16);
-    *reinterpret_cast<uint4*>(y + pix * C + c0) = o;
+    *reinterpret_cast<uint4*>(y + (int64_t)pix * C + c0) = o;
   }
 }
 
@@ -292,8 +295,12 @@ extern "C" int i2pc_bit_stem_im2col(const float* pixels, int batch, int h, int w
   I2PC_REQUIRE(pixels && out && batch > 0 && h > 0 && w > 0 && out_h > 0 && out_w > 0, "bad arguments");
   I2PC_REQUIRE(k_pitch % 8 == 0 && k_pitch >= ksize * ksize * 3, "k_pitch %d must be >= %d and %% 8", k_pitch, ksize * ksize * 3);
   const int64_t work = (int64_t)batch * out_h * out_w * (k_pitch / 8);
-  hipLaunchKernelGGL(k_stem_im2col, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), pixels, batch, h, w, out_h,
-                     out_w, pad_top, pad_left, ksize, k_pitch, static_cast<bf16_t*>(out));
+  if (work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 31))
+    hipLaunchKernelGGL(k_stem_im2col<uint32_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), pixels, batch, h,
+                       w, out_h, out_w, pad_top, pad_left, ksize, k_pitch, static_cast<bf16_t*>(out));
+  else
+    hipLaunchKernelGGL(k_stem_im2col<int64_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), pixels, batch, h,
+                       w, out_h, out_w, pad_top, pad_left, ksize, k_pitch, static_cast<bf16_t*>(out));
   return check_launch("bit_stem_im2col");
 }
 
@@ -342,7 +349,13 @@ extern "C" int i2pc_maxpool3s2(const void* x, int batch, int h, int w, int c, in
   clear_error();
   I2PC_REQUIRE(x && y && batch > 0 && h > 0 && w > 0 && c % 8 == 0 && out_h > 0 && out_w > 0, "bad arguments");
   const int64_t work = (int64_t)batch * out_h * out_w * (c / 8);
-  hipLaunchKernelGGL(k_maxpool, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), static_cast<const bf16_t*>(x), batch,
-                     h, w, c, out_h, out_w, pad_top, pad_left, static_cast<bf16_t*>(y));
+  if (work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 31))
+    hipLaunchKernelGGL(k_maxpool<uint32_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                       static_cast<const bf16_t*>(x), batch, h, w, c, out_h, out_w, pad_top, pad_left,
+                       static_cast<bf16_t*>(y));
+  else
+    hipLaunchKernelGGL(k_maxpool<int64_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                       static_cast<const bf16_t*>(x), batch, h, w, c, out_h, out_w, pad_top, pad_left,
+                       static_cast<bf16_t*>(y));
   return check_launch("maxpool3s2");
 }

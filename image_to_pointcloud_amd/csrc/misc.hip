@@ -93,10 +93,14 @@ __global__ __launch_bounds__(256) void k_layernorm_any(const float* __restrict__
 // Bilinear resize of an NHWC bf16 map to (H, W) with torch's upsample_bilinear2d
 // source-index rules (float scale; align_corners: s = (in-1)/(out-1) * dst, else
 // s = max(in/out * (dst + 0.5) - 0.5, 0)); 8 channels per lane (16 B loads).
+// I: the flat index type -- uint32_t whenever B*H*W*c/8 < 2^31 (every DPT map), so the three
+// index divisions per 16-B output are 32-bit instead of the emulated 64-bit sequences that made
+// this kernel VALU-bound (2.1-2.6 TB/s)
+template <typename I>
 __global__ __launch_bounds__(256) void k_resize(const bf16_t* __restrict__ x, int B, int h, int w, int c, int H, int W,
                                                 int align, const bf16_t* __restrict__ add, bf16_t* __restrict__ y) {
-  const int cv = c / 8;
-  const int64_t total = (int64_t)B * H * W * cv;
+  const I cv = (I)(c / 8);
+  const I total = (I)B * (I)H * (I)W * cv;
   float sh, sw;
   if (align) {
     sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
@@ -105,13 +109,13 @@ __global__ __launch_bounds__(256) void k_resize(const bf16_t* __restrict__ x, in
     sh = (float)h / (float)H;
     sw = (float)w / (float)W;
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
     const int ch = (int)(i % cv);
-    int64_t pix = i / cv;
-    const int ox = (int)(pix % W);
-    pix /= W;
-    const int oy = (int)(pix % H);
-    const int b = (int)(pix / H);
+    I pix = i / cv;
+    const int ox = (int)(pix % (I)W);
+    pix /= (I)W;
+    const int oy = (int)(pix % (I)H);
+    const int b = (int)(pix / (I)H);
     const float fy = align ? sh * oy : fmaxf(sh * (oy + 0.5f) - 0.5f, 0.f);
     const float fx = align ? sw * ox : fmaxf(sw * (ox + 0.5f) - 0.5f, 0.f);
     const int y0 = (int)fy, x0 = (int)fx;
@@ -128,7 +132,7 @@ const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
     const uint32_t* p10 = reinterpret_cast<const uint32_t*>(&a10);
     const uint32_t* p11 = reinterpret_cast<const uint32_t*>(&a11);
     uint4 addv = make_uint4(0, 0, 0, 0);
-    if (add) addv = *reinterpret_cast<const uint4*>(add + i * 8);
+    if (add) addv = *reinterpret_cast<const uint4*>(add + (int64_t)i * 8);
     const uint32_t* pa = reinterpret_cast<const uint32_t*>(&addv);
     uint4 out;
     uint32_t* po = reinterpret_cast<uint32_t*>(&out);
@@ -145,7 +149,7 @@ const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
       if (add) r += g2(pa[k]);
       po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
     }
-    *reinterpret_cast<uint4*>(y + i * 8) = out;
+    *reinterpret_cast<uint4*>(y + (int64_t)i * 8) = out;
   }
 }
 
@@ -228,9 +232,15 @@ extern "C" int i2pc_resize_bilinear(const void* x, int batch, int h, int w, int 
   I2PC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && out_h > 0 && out_w > 0,
                "resize_bilinear: bad shape (c %% 8 == 0)");
   const int64_t work = (int64_t)batch * out_h * out_w * (c / 8);
-  hipLaunchKernelGGL(k_resize, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), static_cast<const bf16_t*>(x),
-                     batch, h, w, c, out_h, out_w, align_corners ? 1 : 0, static_cast<const bf16_t*>(add),
-                     static_cast<bf16_t*>(y));
+  // 32-bit indices when the flat index and its grid-stride successor stay below 2^31
+  if (work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 31))
+    hipLaunchKernelGGL(k_resize<uint32_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                       static_cast<const bf16_t*>(x), batch, h, w, c, out_h, out_w, align_corners ? 1 : 0,
+                       static_cast<const bf16_t*>(add), static_cast<bf16_t*>(y));
+  else
+    hipLaunchKernelGGL(k_resize<int64_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                       static_cast<const bf16_t*>(x), batch, h, w, c, out_h, out_w, align_corners ? 1 : 0,
+                       static_cast<const bf16_t*>(add), static_cast<bf16_t*>(y));
   return check_launch("resize_bilinear");
 }
 
