@@ -366,3 +366,59 @@ def test_band_rccl_exchange_single_rank_and_graph_capture():
     assert _same_bits(out[0].cpu().numpy(), whole.xyz[0].cpu().numpy())
     assert _same_bits(out[1].cpu().numpy(), whole.rgb[0].cpu().numpy())
     comm.close()
+
+
+@pytest.mark.parametrize("shape,density", [((60, 90, 120, 720), "high"),        # 180 threads/row -> tpr 192, one idle wave
+                                           ((50, 257, 40, 2056), "high"),       # 3 column tiles, the last 8 points
+                                           ((64, 80, 300, 1200), "medium"),     # step 2: 600 points/row, tpr 192
+                                           ((40, 40, 77, 1040), "low"),         # step 4: 260 points/row, tpr 128
+                                           ((96, 128, 200, 256), "high")])      # 64 threads/row, 4 rows per pass
+@pytest.mark.parametrize("rpt", [8, 3, 1])
+def test_row_kernel_layouts_match_fast_kernel_and_oracle(shape, density, rpt):
+    """k_unproject_rows over its thread layouts (threads per row 64/128/192/256, idle waves,
+    partial column tiles, steps 1/2/4, 1-8 rows per thread) against k_unproject_fast
+    (i2pc_set_tuning('unp_rows', 0)) bit for bit, and the oracle; NaN fill and invert on."""
+    from image_to_pointcloud_amd import ops
+    h, w, H, W = shape
+    g = _geom()
+    dev = torch.device("cuda")
+    B = 3
+    deps = np.stack([_smooth_depth(h, w, 40 + i) for i in range(B)])
+    deps[1, 3, 4] = np.nan
+    imgs = np.stack([_rgb(H, W, 50 + i) for i in range(B)])
+    outs = []
+    try:
+        for rows in (1, 0):
+            ops.set_tuning("unp_rows", rows)
+            ops.set_tuning("unp_rpt", rpt)
+            pb = g.unproject_batch(torch.from_numpy(deps).to(dev), torch.from_numpy(imgs).to(dev), density=density,
+                                   invert=True, depth_scale=7.5)
+            outs.append((pb.xyz.cpu().numpy(), pb.rgb.cpu().numpy(), pb.bbox.cpu().numpy()))
+    finally:
+        ops.set_tuning("unp_rows", 1)
+        ops.set_tuning("unp_rpt", 8)
+    for a, b in zip(outs[0], outs[1]):
+        assert _same_bits(a, b), _first_diff(a, b)
+    for i in (0, 1):
+        with np.errstate(all="ignore"):
+            ep, ec = ref.depth_to_point_cloud(imgs[i], deps[i], density=density, invert=True, depth_scale=7.5,
+                                              loop=False)
+        assert _same_bits(outs[0][0][i], ep), (i, _first_diff(outs[0][0][i], ep))
+        assert _same_bits(outs[0][1][i].astype(np.float32), ec)
+
+
+def test_row_kernel_equirect_matches_fast_kernel():
+    from image_to_pointcloud_amd import ops
+    g = _geom()
+    dev = torch.device("cuda")
+    dep = torch.from_numpy(_smooth_depth(64, 128, 7)[None]).to(dev)
+    img = torch.from_numpy(_rgb(256, 1100, 8)[None]).to(dev)
+    outs = []
+    try:
+        for rows in (1, 0):
+            ops.set_tuning("unp_rows", rows)
+            pb = g.unproject_batch(dep, img, density="high", projection="equirect")
+            outs.append(pb.xyz.cpu().numpy())
+    finally:
+        ops.set_tuning("unp_rows", 1)
+    assert _same_bits(outs[0], outs[1]), _first_diff(outs[0], outs[1])
