@@ -131,7 +131,7 @@ def _kernel_profile(pipe, images, reps=5):
 
 def _pmc_traffic(tag: str):
     """HBM bytes per launch by kernel label from the newest profiles/r*_<tag>_pmc_traffic.json
-    (tools/gpu_profile.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench,
+    (tools/gpu.sh profile: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench,
     gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or ({}, None)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc_traffic.json")))
