@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 namespace i2pc {
 namespace attn {
@@ -236,9 +237,12 @@ __device__ __forceinline__ v4s tr_read(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
+// lazy != 0: skip the alpha exponential and the O / l rescale of a tile when no query row of the
+// wave raised its running max -- alpha would be exp2(0) = 1 exactly, so the skip is bit-exact
+// (the usual case after the first tiles: the max of a row settles early)
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restrict__ qkv, int B, int T, int NH,
-                                                           float scale_log2, bf16_t* __restrict__ out) {
+                                                           float scale_log2, bf16_t* __restrict__ out, int lazy) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * kTileBytes];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -334,7 +338,9 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
       const float m_new = fmaxf(m_run, mx);
       // raw v_exp_f32 (ocml's exp2f adds 4 VALU ops per call for denormal results, which
       // only matter for probabilities < 2^-126 of a sum >= 1)
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+      const bool rescale = !lazy || __ballot(m_new != m_run) != 0;   // wave-uniform
+      float alpha = 1.f;
+      if (rescale) alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
       const float mc = m_new * c;
       m_run = m_new;
       float ls = 0.f;
@@ -351,9 +357,13 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
           ls += p0 + p1;
           pk[k2][r >> 1] = pack_bf16(p0, p1);
         }
-      l_run = l_run * alpha + ls;
+      if (rescale) {
+        l_run = l_run * alpha + ls;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+      } else {
+        l_run = l_run + ls;
+      }
       // O^T += V^T P^T over 16-key steps; V^T fragments by transposed reads
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
@@ -405,6 +415,13 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
 
 using namespace i2pc;
 
+// lazy rescale on by default (I2PC_ATTN_LAZY / i2pc_set_tuning "attn_lazy")
+static int g_lazy = [] { const char* e = getenv("I2PC_ATTN_LAZY"); return e ? atoi(e) : 1; }();
+bool i2pc_attention_tune(const char* name, int value) {
+  if (std::strcmp(name, "attn_lazy") == 0) { g_lazy = value; return true; }
+  return false;
+}
+
 extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scale, void* out, void* stream) {
   clear_error();
   I2PC_REQUIRE(qkv && out, "NULL pointer");
@@ -419,12 +436,12 @@ extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads,
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
   else if (occ == 2)
     hipLaunchKernelGGL(attn::k_attention_tr<2>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
-                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   else if (occ == 4)
     hipLaunchKernelGGL(attn::k_attention_tr<4>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
-                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   else
     hipLaunchKernelGGL(attn::k_attention_tr<3>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
-                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out));
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   return check_launch("attention");
 }

@@ -144,6 +144,32 @@ def test_attention(dev, B, T, H):
     _close(got, ref, rel=1.2e-2, mx=3e-2)
 
 
+@pytest.mark.parametrize("B,T,H,spike", [(2, 577, 16, 0), (2, 577, 16, 1), (1, 1370, 6, 1), (2, 130, 12, 1)])
+def test_attention_lazy_rescale_bit_exact(dev, B, T, H, spike):
+    """The lazy softmax rescale (attn_lazy, skip when no row's max rose) equals the always-rescale
+    kernel bit for bit.  spike: keys whose scores jump at later tiles, so the rescale branch is
+    taken mid-sequence for some rows and skipped for others (cdna_hip_programming.md rule 26)."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(T + H)
+    qkv = torch.randn(B * T, 3, H, 64, generator=g) * 1.5
+    if spike:
+        q = qkv[:, 0]
+        for kt in (T // 3, (2 * T) // 3, T - 1):          # late keys aligned with some queries
+            qkv[kt::T, 1] = q[(kt * 7) % T::T] * 3.0
+    qkv = _bf(qkv.reshape(B * T, 3 * H * 64)).to(dev)
+    outs = []
+    try:
+        for lazy in (0, 1):
+            ops.set_tuning("attn_lazy", lazy)
+            outs.append(ops.attention(qkv, B, T, H, 0.125).clone())
+    finally:
+        ops.set_tuning("attn_lazy", 1)
+    assert torch.equal(outs[0], outs[1])
+    q, k, v = qkv.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    _close(outs[1], ref, rel=1.2e-2, mx=3e-2)
+
+
 @pytest.mark.parametrize("B,H,W,C", [(2, 12, 12, 256), (1, 5, 7, 64), (1, 192, 192, 128)])
 def test_upsample2x_align_corners(dev, B, H, W, C):
     ops = _ops()
