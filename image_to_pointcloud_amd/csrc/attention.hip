@@ -240,7 +240,11 @@ __device__ __forceinline__ v4s tr_read(const uint8_t* p) {
 // lazy != 0: skip the alpha exponential and the O / l rescale of a tile when no query row of the
 // wave raised its running max -- alpha would be exp2(0) = 1 exactly, so the skip is bit-exact
 // (the usual case after the first tiles: the max of a row settles early)
-template <int OCC>
+// SC: the exponent arguments as single v_fma_f32 (inline asm, so the SLP vectorizer cannot pair
+// them) instead of one v_pk_fma_f32 per pair -- packed FP32 ops cost extra issue cycles beside
+// MFMAs (MI355X_MICROARCH.md, filler prices); the same fused operation, so bit-identical
+
+template <int OCC, bool SC = false>
 __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restrict__ qkv, int B, int T, int NH,
                                                            float scale_log2, bf16_t* __restrict__ out, int lazy) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * kTileBytes];
@@ -350,8 +354,15 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           typedef float f32x2 __attribute__((ext_vector_type(2)));
-          const f32x2 e = __builtin_elementwise_fma(f32x2{st[k2][r], st[k2][r + 1]}, f32x2{c, c},
-                                                    f32x2{-mc, -mc});     // one v_pk_fma_f32 per pair
+          f32x2 e;
+          if constexpr (SC) {
+            const float nmc = -mc;
+            asm("v_fma_f32 %0, %1, %2, %3" : "=v"(e.x) : "v"(st[k2][r]), "v"(c), "v"(nmc));
+            asm("v_fma_f32 %0, %1, %2, %3" : "=v"(e.y) : "v"(st[k2][r + 1]), "v"(c), "v"(nmc));
+          } else {
+            e = __builtin_elementwise_fma(f32x2{st[k2][r], st[k2][r + 1]}, f32x2{c, c},
+                                          f32x2{-mc, -mc});     // one v_pk_fma_f32 per pair
+          }
           const float p0 = __builtin_amdgcn_exp2f(e.x);
           const float p1 = __builtin_amdgcn_exp2f(e.y);
           ls += p0 + p1;
@@ -417,8 +428,11 @@ using namespace i2pc;
 
 // lazy rescale on by default (I2PC_ATTN_LAZY / i2pc_set_tuning "attn_lazy")
 static int g_lazy = [] { const char* e = getenv("I2PC_ATTN_LAZY"); return e ? atoi(e) : 1; }();
+// scalar exponent FMAs (I2PC_ATTN_SCALAR / "attn_scalar")
+static int g_scalar = [] { const char* e = getenv("I2PC_ATTN_SCALAR"); return e ? atoi(e) : 1; }();
 bool i2pc_attention_tune(const char* name, int value) {
   if (std::strcmp(name, "attn_lazy") == 0) { g_lazy = value; return true; }
+  if (std::strcmp(name, "attn_scalar") == 0) { g_scalar = value; return true; }
   return false;
 }
 
@@ -439,6 +453,9 @@ extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads,
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   else if (occ == 4)
     hipLaunchKernelGGL(attn::k_attention_tr<4>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
+  else if (g_scalar)
+    hipLaunchKernelGGL((attn::k_attention_tr<3, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   else
     hipLaunchKernelGGL(attn::k_attention_tr<3>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),

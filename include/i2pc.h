@@ -287,8 +287,9 @@ int i2pc_gemm_set_engine(int mode);
  * last round of a persistent GEMM into 256 x 128 tiles where that saves a round), "unp_rows"
  * (1 = row-sweep unprojection kernel), "unp_nt" (1 = non-temporal point stores), "unp_rpt"
  * (point rows per thread of the row-sweep kernel, 1..8), "attn_lazy" (1 = skip the softmax rescale of
- * a key tile that raised no row's running max).  Defaults come from the I2PC_GEMM_TAIL /
- * I2PC_UNP_ROWS / I2PC_UNP_NT / I2PC_UNP_RPT / I2PC_ATTN_LAZY environment variables, else 1, 1, 1, 8, 1.  A HIP graph
+ * a key tile that raised no row's running max), "attn_scalar" (1 = unpacked exponent FMAs).  Defaults come from the I2PC_GEMM_TAIL /
+ * I2PC_UNP_ROWS / I2PC_UNP_NT / I2PC_UNP_RPT / I2PC_ATTN_LAZY / I2PC_ATTN_SCALAR environment variables,
+ * else 1, 1, 1, 8, 1, 1.  A HIP graph
  * keeps the kernels it captured: re-capture after changing a knob. */
 int i2pc_set_tuning(const char* name, int value);
 

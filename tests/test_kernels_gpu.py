@@ -146,8 +146,8 @@ def test_attention(dev, B, T, H):
 
 @pytest.mark.parametrize("B,T,H,spike", [(2, 577, 16, 0), (2, 577, 16, 1), (1, 1370, 6, 1), (2, 130, 12, 1)])
 def test_attention_lazy_rescale_bit_exact(dev, B, T, H, spike):
-    """The lazy softmax rescale (attn_lazy, skip when no row's max rose) equals the always-rescale
-    kernel bit for bit.  spike: keys whose scores jump at later tiles, so the rescale branch is
+    """The lazy softmax rescale (attn_lazy, skip when no row's max rose), the scalar exponent FMAs
+    (attn_scalar) equal the plain kernel bit for bit.  spike: keys whose scores jump at later tiles, so the rescale branch is
     taken mid-sequence for some rows and skipped for others (cdna_hip_programming.md rule 26)."""
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(T + H)
@@ -159,12 +159,15 @@ def test_attention_lazy_rescale_bit_exact(dev, B, T, H, spike):
     qkv = _bf(qkv.reshape(B * T, 3 * H * 64)).to(dev)
     outs = []
     try:
-        for lazy in (0, 1):
+        for lazy, scalar in ((0, 0), (1, 0), (1, 1)):
             ops.set_tuning("attn_lazy", lazy)
+            ops.set_tuning("attn_scalar", scalar)
             outs.append(ops.attention(qkv, B, T, H, 0.125).clone())
     finally:
         ops.set_tuning("attn_lazy", 1)
-    assert torch.equal(outs[0], outs[1])
+        ops.set_tuning("attn_scalar", 1)
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     q, k, v = qkv.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).permute(0, 2, 1, 3).reshape(B * T, H * 64)
     _close(outs[1], ref, rel=1.2e-2, mx=3e-2)
