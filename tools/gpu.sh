@@ -33,8 +33,9 @@ PY
 check() {
   export I2PC_PARITY_LOG=gpurun_out/parity.jsonl
   rm -f "$I2PC_PARITY_LOG"
-  local K=${1:+-k "$1"}
-  timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread -rP $K \
+  local K=()
+  [ -n "$1" ] && K=(-k "$1")
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread -rP "${K[@]}" \
     > gpurun_out/gputests.log 2>&1
   local rc=$?
   tail -5 gpurun_out/gputests.log
