@@ -242,7 +242,8 @@ __device__ __forceinline__ v4s tr_read(const uint8_t* p) {
 // (the usual case after the first tiles: the max of a row settles early)
 // SC: the exponent arguments as single v_fma_f32 (inline asm, so the SLP vectorizer cannot pair
 // them) instead of one v_pk_fma_f32 per pair -- packed FP32 ops cost extra issue cycles beside
-// MFMAs (MI355X_MICROARCH.md, filler prices); the same fused operation, so bit-identical
+// MFMAs (MI355X_MICROARCH.md, filler prices) -- and the row max across the two lane halves by
+// v_permlane32_swap instead of ds_bpermute; the same operations, so bit-identical
 
 template <int OCC, bool SC = false>
 __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restrict__ qkv, int B, int T, int NH,
@@ -338,7 +339,12 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
       for (int k2 = 0; k2 < 2; ++k2)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[k2][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      if constexpr (SC) {   // the two 32-lane halves' maxima by v_permlane32_swap (VALU, no LDS round trip)
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      } else {
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+      }
       const float m_new = fmaxf(m_run, mx);
       // raw v_exp_f32 (ocml's exp2f adds 4 VALU ops per call for denormal results, which
       // only matter for probabilities < 2^-126 of a sum >= 1)
