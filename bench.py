@@ -290,6 +290,11 @@ def main():
                         "flops_per_launch": d["flops"] / d["n"],
                         "share_of_step": round(d["t"] / (ms * 1e-3), 3)}
             roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name)
+            if name.startswith("k_gemm_p"):
+                roofline["note"] = ("avg_us is per i2pc_gemm call: the persistent launch plus, where the round-"
+                                    "quantisation split applies (QKV), its 256x128 tail launch; rocprofv3 lists them "
+                                    "as k_gemm_p<..., 256, ...> and k_gemm_p<..., 128, ...>; traffic is the main "
+                                    "launch's")
         else:
             ach = d["bytes"] / (d["t"]) / 1e9
             roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
