@@ -1606,6 +1606,10 @@ static int g_engine = [] {
   return v == 0 ? 1 : (v >= 2 && v <= 4) ? v : 0;
 }();
 
+static int g_tail = [] { const char* e = getenv("I2PC_GEMM_TAIL"); return e ? atoi(e) : 1; }();
+// the persistent engine for N % 256 != 0, N % 128 == 0 (256 x 128 tiles; I2PC_GEMM_BN128 / "gemm_bn128")
+static int g_bn128 = [] { const char* e = getenv("I2PC_GEMM_BN128"); return e ? atoi(e) : 1; }();
+
 static int64_t max_row(const Args& p) {
   const int64_t m = p.M - 1;
   return p.o_g > 0 ? (m / p.o_g) * p.o_gs + (p.o_g - 1) + p.o_o : m + p.o_o;
@@ -1617,7 +1621,9 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   Plan pl{0, 0, 0, -1};
   // persistent engine
   int epi = -1;
-  if (p.N % 256 == 0 && !p.rbias && !p.tbl && force == 0 && pforce != 1) {
+  // N a multiple of 128 only (e.g. the DPT head's first conv, 256 -> 128): 256 x 128 tiles
+  const int pbn = p.N % 256 == 0 ? 256 : (p.N % 128 == 0 && g_bn128) ? 128 : 0;
+  if (pbn && !p.rbias && !p.tbl && force == 0 && pforce != 1) {
     const bool ct = p.ct_s > 0;
     if (ct) epi = (!p.res && !p.res2 && !p.c_f32 && p.ct_c % 8 == 0) ? pers::EPI_CT : -1;
     else if (!p.res && !p.res2 && !p.c_f32) epi = pers::EPI_PLAIN;
@@ -1630,6 +1636,7 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
     if (conv && (epi == pers::EPI_RESF32 || epi == pers::EPI_CT)) epi = -1;
     if (conv && relu && epi != pers::EPI_PLAIN) epi = -1;
     if (!conv && p.a_g != 0) epi = -1;
+    if (pbn == 128 && (epi != pers::EPI_PLAIN || relu)) epi = -1;   // instantiated BN = 128 variants
     if (epi >= 0) {
       const int64_t esz = p.c_f32 ? 4 : 2;
       const int64_t abytes = conv ? (int64_t)p.cb * p.ch * p.cw * p.cc * 2 : (int64_t)(p.M + 320) * p.lda * 2;
@@ -1647,7 +1654,7 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
     int best = 256;
     int64_t best_cost = -1;
     for (int bm : {256}) {   // 320 spills registers (scratch would break the counted waits)
-      const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * (p.N / 256);
+      const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * (p.N / pbn);
       const int64_t cost = (tiles + ncu - 1) / ncu * bm;
       if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = bm; }
     }
@@ -1655,6 +1662,15 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
     // The persistent engine pays where a CU runs several tiles (it hides each tile's first
     // stage and epilogue behind the neighbouring tiles); at one or two tiles per CU the
     // tile kernel's 128 x 128 configurations quantise better (profiles/r01_gemm_engines.txt).
+    const int64_t tiles = (int64_t)((p.M + best - 1) / best) * (p.N / pbn);
+    if (pbn == 128) {
+      if (pforce == 2 || pforce == 4 || tiles >= 3 * ncu) return Plan{1, best, 128, epi};
+      epi = -1;
+    }
+  }
+  if (epi >= 0) {
+    const int64_t ncu = num_cus();
+    const int best = 256;
     const int64_t tiles = (int64_t)((p.M + best - 1) / best) * (p.N / 256);
     // the ping-pong engine (k_gemm_8p): dense A, plain / fp32-residual epilogues, K >= 128
     const bool can8 = !conv && !relu && (epi == pers::EPI_PLAIN || epi == pers::EPI_RESF32) && p.K >= 128;
@@ -1707,6 +1723,13 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
       return check_launch("gemm_q");
     }
   }
+  if (pl.bn == 128) {   // plan: EPI_PLAIN, no ReLU on A
+    if constexpr (!RELU_A) {
+      launch_p<256, CONV, false, EPI_PLAIN, 128>(p, s);
+      return check_launch("gemm");
+    }
+    return set_error(I2PC_EUNSUPPORTED, "gemm: no persistent BN=128 variant with ReLU on A");
+  }
   if constexpr (!CONV && !RELU_A) {
     if (pl.epi == EPI_PLAIN) launch_p<256, false, false, EPI_PLAIN>(p, s);
     else if (pl.epi == EPI_RESF32) launch_p<256, false, false, EPI_RESF32>(p, s);
@@ -1729,7 +1752,6 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
 // (e.g. M = 18464, N = 3072: 3 rounds + a half round instead of 4).  Plain dense epilogue
 // with a linear output row map only; the two parts compute every output exactly as one launch
 // would (same per-output accumulation order).  I2PC_GEMM_TAIL=0 disables it.
-static int g_tail = [] { const char* e = getenv("I2PC_GEMM_TAIL"); return e ? atoi(e) : 1; }();
 static bool tail_split(const Args& p, int& ma) {
   if (!g_tail || p.o_g != 0 || p.a_g != 0 || p.ct_s > 0 || p.N % 256 != 0) return false;
   const int64_t tn = p.N / 256, tm = (p.M + 255) / 256, T = tm * tn, G = num_cus();
@@ -1789,6 +1811,7 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu) {
   } else if (pl.kind == 1) {
     static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT"};
     if (g_quarter && pl.epi != pers::EPI_CT) snprintf(buf, sizeof buf, "k_gemm_q<%s, %s, %s>", c, r, epis[pl.epi]);
+    else if (pl.bn == 128) snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s, 128>", pl.bm, c, r, epis[pl.epi]);
     else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
   } else if (pl.kind == 0) {
     const int wm = pl.bn == 32 ? 4 : 2, wn = pl.bn == 256 ? 4 : pl.bn == 32 ? 1 : 2;
@@ -1980,5 +2003,6 @@ extern "C" int i2pc_gemm_set_engine(int mode) {
 // process-wide tuning knobs (i2pc_set_tuning): "gemm_tail" (round-quantisation split on/off)
 bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
+  if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
   return false;
 }

@@ -283,14 +283,18 @@ const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* desc);
 int i2pc_gemm_set_engine(int mode);
 
 /* Process-wide kernel-selection knobs for A/B measurement (not part of the drop-in surface;
- * every setting computes the same results bit for bit).  Names: "gemm_tail" (1 = split the
- * last round of a persistent GEMM into 256 x 128 tiles where that saves a round), "unp_rows"
- * (1 = row-sweep unprojection kernel), "unp_nt" (1 = non-temporal point stores), "unp_rpt"
- * (point rows per thread of the row-sweep kernel, 1..8), "attn_lazy" (1 = skip the softmax rescale of
- * a key tile that raised no row's running max), "attn_scalar" (1 = unpacked exponent FMAs).  Defaults come from the I2PC_GEMM_TAIL /
- * I2PC_UNP_ROWS / I2PC_UNP_NT / I2PC_UNP_RPT / I2PC_ATTN_LAZY / I2PC_ATTN_SCALAR environment variables,
- * else 1, 1, 1, 8, 1, 1.  A HIP graph
- * keeps the kernels it captured: re-capture after changing a knob. */
+ * every setting computes the same results bit for bit):
+ *   "gemm_tail"   1 = split the last round of a persistent GEMM into 256 x 128 tiles where that
+ *                 saves a round
+ *   "gemm_bn128"  1 = the persistent engine with 256 x 128 tiles for N % 256 != 0, N % 128 == 0
+ *   "unp_rows"    1 = the row-sweep unprojection kernel
+ *   "unp_nt"      1 = non-temporal point stores
+ *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
+ *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
+ *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
+ * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _UNP_ROWS / _UNP_NT / _UNP_RPT / _ATTN_LAZY /
+ * _ATTN_SCALAR environment variables, else 1, 1, 1, 1, 8, 1, 1.  A HIP graph keeps the kernels
+ * it captured: re-capture after changing a knob. */
 int i2pc_set_tuning(const char* name, int value);
 
 /* LayerNorm over the last dim: x fp32 [rows][dim] (row stride ldx) -> y bf16 [rows][dim]

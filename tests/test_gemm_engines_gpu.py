@@ -51,7 +51,7 @@ def _fro(got, ref):
 
 
 @pytest.mark.parametrize("M,N,K,act", [(8200, 2048, 1024, None), (18464, 3072, 64, "gelu"), (9000, 1024, 192, None), (4100, 4096, 512, "gelu"),
-                                       (300, 256, 512, None), (257, 512, 128, "relu")])
+                                       (300, 256, 512, None), (257, 512, 128, "relu"), (20000, 384, 512, "gelu")])
 def test_linear_plain_engines_bitexact(M, N, K, act):
     ops = _ops()
     dev = torch.device("cuda")
@@ -67,7 +67,7 @@ def test_linear_plain_engines_bitexact(M, N, K, act):
         assert "k_gemm_p" in lab or "k_gemm_q" in lab, "persistent engine not selected"
         ops.set_gemm_engine(4)
         lab = ops.gemm_kernel_label(_desc_of(ops, x, w, b, out))
-        assert ("k_gemm_8p" in lab) == (K >= 128), lab
+        assert ("k_gemm_8p" in lab) == (K >= 128 and N % 256 == 0), lab
     finally:
         ops.set_gemm_engine(0)
     assert torch.equal(got, ref), f"engines differ: {(got.float() - ref.float()).abs().max().item()}"
@@ -110,7 +110,7 @@ def _pack_conv(w):
 
 
 @pytest.mark.parametrize("B,H,W,C,Co,stride", [(20, 64, 64, 256, 256, 1), (4, 48, 48, 512, 256, 2),
-                                                (3, 37, 29, 256, 256, 1)])
+                                                (3, 37, 29, 256, 256, 1), (8, 96, 96, 256, 128, 1)])
 def test_conv_engines_bitexact(B, H, W, C, Co, stride):
     ops = _ops()
     dev = torch.device("cuda")
