@@ -251,6 +251,75 @@ __global__ __launch_bounds__(256) void k_gn_apply(GnOperand a, GnOperand r, int 
   }
 }
 
+// The same im2col with the input window staged in LDS: a workgroup owns 64 consecutive output
+// pixels of one output row; it loads the ks input rows x (2 * 63 + ks) columns x 3 channels they
+// read (coalesced along x, zero outside the image) once, then writes the 64 x kp output chunks
+// (16 B per thread, consecutive threads consecutive chunks).  The per-lane gathers of
+// k_stem_im2col read 8 scattered floats per 16-B output.  Same values (bit-identical).
+constexpr int kStemOX = 64, kStemMaxK = 7;
+constexpr int kStemCols = 2 * (kStemOX - 1) + kStemMaxK;
+__global__ __launch_bounds__(256) void k_stem_im2col_lds(const float* __restrict__ x, int B, int H, int W, int OH, int OW,
+                                                         int pt, int pl, int ks, int kp, bf16_t* __restrict__ out) {
+  __shared__ float win[3 * kStemMaxK * kStemCols];   // [c][row][col]
+  __shared__ int koff[256];                           // window offset of k, -1 beyond ks*ks*3
+  const int segs = (OW + kStemOX - 1) / kStemOX;
+  const int seg = blockIdx.x % segs;
+  const int oy = (blockIdx.x / segs) % OH;
+  const int b = blockIdx.x / (segs * OH);
+  const int ox0 = seg * kStemOX;
+  const int nox = min(kStemOX, OW - ox0);
+  const int iy0 = oy * 2 - pt, ix0 = ox0 * 2 - pl;
+  const int ncols = 2 * (nox - 1) + ks;
+  const int KK = ks * ks * 3;
+  if ((int)threadIdx.x < kp) {
+    const int k = threadIdx.x;
+    const int tap = k / 3, c = k - tap * 3;
+    const int ky = tap / ks, kx = tap - ky * ks;
+    koff[k] = k < KK ? (c * ks + ky) * kStemCols + kx : -1;
+  }
+  // every (c, row) of the window by the first kStemCols threads, all loads in flight before the
+  // first LDS write (a per-row load -> store loop serialised 21 memory latencies per workgroup)
+  if ((int)threadIdx.x < kStemCols) {
+    const int col = threadIdx.x;
+    const int ix = ix0 + col;
+    const bool cin = col < ncols && (unsigned)ix < (unsigned)W;
+    float v[3 * kStemMaxK];
+#pragma unroll
+    for (int rowi = 0; rowi < 3 * kStemMaxK; ++rowi) {
+      v[rowi] = 0.f;
+      if (rowi < 3 * ks) {
+        const int c = rowi / ks, r = rowi - c * ks;
+        const int iy = iy0 + r;
+        if (cin && (unsigned)iy < (unsigned)H) v[rowi] = x[(((int64_t)b * 3 + c) * H + iy) * W + ix];
+      }
+    }
+#pragma unroll
+    for (int rowi = 0; rowi < 3 * kStemMaxK; ++rowi)
+      if (rowi < 3 * ks) win[rowi * kStemCols + col] = v[rowi];
+  }
+  __syncthreads();
+  // thread t: chunk kc = t % cpm of output pixels ml = t / cpm + j * (256 / cpm) (consecutive
+  // threads write consecutive 16-B chunks)
+  const int cpm = kp / 8;
+  const int per = 256 / cpm;
+  const int ml0 = threadIdx.x / cpm, kc = threadIdx.x - ml0 * cpm;
+  if (ml0 >= per) return;
+  int off[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) off[e] = koff[kc * 8 + e];
+  bf16_t* ob = out + (((int64_t)b * OH + oy) * OW + ox0) * kp + kc * 8;
+  for (int ml = ml0; ml < nox; ml += per) {
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const float v0 = off[e] >= 0 ? win[off[e] + 2 * ml] : 0.f;
+      const float v1 = off[e + 1] >= 0 ? win[off[e + 1] + 2 * ml] : 0.f;
+      w[e / 2] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+    }
+    *reinterpret_cast<uint4*>(ob + (int64_t)ml * kp) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // 3x3 stride-2 max over the zero-padded map (pad pt top / pl left, zero beyond the
 // bottom/right edge as DynamicPad2d pads there), 8 channels per thread
 template <typename I>
@@ -307,7 +376,11 @@ extern "C" int i2pc_bit_stem_im2col(const float* pixels, int batch, int h, int w
   I2PC_REQUIRE(pixels && out && batch > 0 && h > 0 && w > 0 && out_h > 0 && out_w > 0, "bad arguments");
   I2PC_REQUIRE(k_pitch % 8 == 0 && k_pitch >= ksize * ksize * 3, "k_pitch %d must be >= %d and %% 8", k_pitch, ksize * ksize * 3);
   const int64_t work = (int64_t)batch * out_h * out_w * (k_pitch / 8);
-  if (work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 31))
+  if (ksize <= kStemMaxK && k_pitch <= 256)
+    hipLaunchKernelGGL(k_stem_im2col_lds, dim3(batch * out_h * ((out_w + kStemOX - 1) / kStemOX)), dim3(256), 0,
+                       as_stream(stream), pixels, batch, h, w, out_h, out_w, pad_top, pad_left, ksize, k_pitch,
+                       static_cast<bf16_t*>(out));
+  else if (work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 31))
     hipLaunchKernelGGL(k_stem_im2col<uint32_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), pixels, batch, h,
                        w, out_h, out_w, pad_top, pad_left, ksize, k_pitch, static_cast<bf16_t*>(out));
   else

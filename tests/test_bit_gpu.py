@@ -59,3 +59,25 @@ def test_stem_conv_same_padding():
     assert (oh, ow) == (192, 192)
     err = (_nchw(got) - ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("B,H,W,ks,kp", [(2, 384, 384, 7, 152), (1, 37, 45, 7, 152), (3, 130, 257, 7, 192),
+                                         (1, 20, 20, 3, 32)])
+def test_stem_im2col_exact(B, H, W, ks, kp):
+    """im2col rows bit-exact against torch unfold of the SAME-padded input (k = (ky*ks + kx)*3 + c,
+    zero beyond ks*ks*3), covering partial 64-pixel output segments."""
+    from image_to_pointcloud_amd import ops
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(H * W + ks)
+    pix = torch.randn(B, 3, H, W, generator=g).to(dev)
+    cols, (oh, ow) = ops.stem_im2col(pix, ksize=ks, k_pitch=kp)
+    _, pt = ops.same_pad(H, ks, 2)
+    _, pl = ops.same_pad(W, ks, 2)
+    ph = max((oh - 1) * 2 + ks - H - pt, 0)
+    pw = max((ow - 1) * 2 + ks - W - pl, 0)
+    xp = F.pad(pix, [pl, pw, pt, ph])
+    u = F.unfold(xp, ks, stride=2)[..., : oh * ow]                   # [B, 3*ks*ks, L], (c, ky, kx)
+    u = u.view(B, 3, ks * ks, oh * ow).permute(0, 3, 2, 1).reshape(B * oh * ow, ks * ks * 3)
+    ref = torch.zeros(B * oh * ow, kp, device=dev)
+    ref[:, : ks * ks * 3] = u
+    assert torch.equal(cols, ref.to(torch.bfloat16))
