@@ -152,10 +152,22 @@ __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __
     const uint8_t* src = img + (int64_t)(ylo + c0) * row_bytes + a0;
     __syncthreads();                       // the previous chunk's taps are read
     if (vec) {
+      // up to 8 loads per thread in flight before their LDS stores (a load -> store loop
+      // serialised one memory latency per iteration)
       const int u = wb >> 4;
-      for (int i = threadIdx.x; i < cr * u; i += blockDim.x) {
-        const int r = i / u, c = i - r * u;
-        reinterpret_cast<uint4*>(stg)[i] = reinterpret_cast<const uint4*>(src + (int64_t)r * row_bytes)[c];
+      const int n = cr * u;
+      constexpr int U = 8;
+      for (int i0 = threadIdx.x; i0 < n; i0 += U * blockDim.x) {
+        uint4 q[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {   // unconditional (index clamped): no per-load branch + wait
+          const int i = min(i0 + k * (int)blockDim.x, n - 1);
+          const int r = i / u, c = i - r * u;
+          q[k] = reinterpret_cast<const uint4*>(src + (int64_t)r * row_bytes)[c];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)     // clamped too (past n: the last element's own value again)
+          reinterpret_cast<uint4*>(stg)[min(i0 + k * (int)blockDim.x, n - 1)] = q[k];
       }
     } else {
       for (int i = threadIdx.x; i < cr * wb; i += blockDim.x) {

@@ -470,9 +470,10 @@ __device__ __forceinline__ void stage_floats(float* dst, const float* src, int n
       float4 r[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) r[k] = s4[min(base + k * 256 + (int)threadIdx.x, n4 - 1)];
+      // stores clamped too (past the end: the last element's own value again), so hipcc cannot
+      // sink each load into a predicated store block and wait for it there
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (base + k * 256 + (int)threadIdx.x < n4) d4[base + k * 256 + threadIdx.x] = r[k];
+      for (int k = 0; k < 4; ++k) d4[min(base + k * 256 + (int)threadIdx.x, n4 - 1)] = r[k];
     }
   } else {
     for (int base = 0; base < n; base += 8 * 256) {
@@ -480,8 +481,7 @@ __device__ __forceinline__ void stage_floats(float* dst, const float* src, int n
 #pragma unroll
       for (int k = 0; k < 8; ++k) r[k] = src[min(base + k * 256 + (int)threadIdx.x, n - 1)];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (base + k * 256 + (int)threadIdx.x < n) dst[base + k * 256 + threadIdx.x] = r[k];
+      for (int k = 0; k < 8; ++k) dst[min(base + k * 256 + (int)threadIdx.x, n - 1)] = r[k];
     }
   }
 }
