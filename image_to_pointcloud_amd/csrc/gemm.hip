@@ -84,6 +84,7 @@ struct Args {
   const uint32_t* Ws; int64_t ldws;    // W scales
   uint32_t* Cs; int64_t ldcs;          // fp8 output scales (EPI_Q8), dwords per row
   uint32_t as_bytes, ws_bytes;
+  int kspan;   // split-K (tile kernel): K-steps per blockIdx.y slice, 0 = the whole K
 };
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
@@ -437,8 +438,15 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   STAMP(0);
-  const int nk = p.K / KB;
-  stage(0, 0);
+  // split-K: slice blockIdx.y covers K-steps [kt0, kt0 + nk) and writes its raw fp32 partial
+  // sums to slab blockIdx.y of the workspace (the host passes a plain fp32 epilogue)
+  int nk = p.K / KB, kt0 = 0;
+  if (p.kspan > 0) {
+    kt0 = blockIdx.y * p.kspan;
+    nk = min(nk - kt0, p.kspan);
+    p.C = static_cast<float*>(p.C) + (int64_t)blockIdx.y * p.M * p.N;
+  }
+  stage(0, kt0 * KB);
   __syncthreads();   // waits vmcnt(0): tile 0 landed
   STAMP(1);
 
@@ -446,7 +454,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   const int fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * KB);
+    if (kt + 1 < nk) stage(cur ^ 1, (kt0 + kt + 1) * KB);
     const uint8_t* sA = smem + cur * STAGE;
     const uint8_t* sW = sA + A_BYTES;
 #pragma unroll
@@ -487,7 +495,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
 }
 
 template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>
-static void launch(const Args& p, hipStream_t s) {
+static void launch(const Args& p, hipStream_t s, int splits = 1) {
   Args q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = p.N / BN;
@@ -499,7 +507,28 @@ static void launch(const Args& p, hipStream_t s) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(q.tiles_m * q.tiles_n), dim3(64 * WM * WN), smem, s, q);
+  hipLaunchKernelGGL(kern, dim3(q.tiles_m * q.tiles_n, splits), dim3(64 * WM * WN), smem, s, q);
+}
+
+// Split-K reduction: out = epilogue(sum over slabs z = 0..splits-1 of ws[z][m][n], in that
+// order), 4 columns per thread (epilogue4: the tile kernel's epilogue arithmetic).  M * N / 4
+// < 2^31 (plan).
+__global__ __launch_bounds__(256) void k_splitk_reduce(Args p, const float* __restrict__ ws, int splits) {
+  const uint32_t n4 = (uint32_t)p.N >> 2;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= (uint32_t)p.M * n4) return;
+  const uint32_t m = i / n4;
+  const uint32_t n = (i - m * n4) * 4u;
+  const int64_t slab = (int64_t)p.M * p.N;
+  const float* src = ws + (int64_t)m * p.N + n;
+  float4 a = *reinterpret_cast<const float4*>(src);
+#pragma unroll 4
+  for (int z = 1; z < splits; ++z) {
+    const float4 b = *reinterpret_cast<const float4*>(src + z * slab);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  float v[4] = {a.x, a.y, a.z, a.w};
+  epilogue4(p, (int)m, (int)n, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -1610,6 +1639,10 @@ static int g_tail = [] { const char* e = getenv("I2PC_GEMM_TAIL"); return e ? at
 // the persistent engine for N % 256 != 0, N % 128 == 0 (256 x 128 tiles; I2PC_GEMM_BN128 / "gemm_bn128")
 static int g_bn128 = [] { const char* e = getenv("I2PC_GEMM_BN128"); return e ? atoi(e) : 1; }();
 
+// split-K for calls the tile kernel would run with few tiles and a long K (I2PC_GEMM_SPLITK /
+// "gemm_splitk"; needs the caller's workspace, i2pc_gemm_ws)
+static int g_splitk = [] { const char* e = getenv("I2PC_GEMM_SPLITK"); return e ? atoi(e) : 1; }();
+
 static int64_t max_row(const Args& p) {
   const int64_t m = p.M - 1;
   return p.o_g > 0 ? (m / p.o_g) * p.o_gs + (p.o_g - 1) + p.o_o : m + p.o_o;
@@ -1701,6 +1734,63 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   else if (p.N % 32 == 0) pl = Plan{0, 128, 32, 64};
   else pl = Plan{-1, 0, 0, 0};
   return pl;
+}
+
+// Split-K plan: when the tile kernel was chosen, K >= 4096 and even 256 x 256 (N % 256 == 0, else
+// 128 x 128) tiles fill at most half the CUs, split K into `splits` slices of `kspan` K-steps (at least 4)
+// so tiles x splits <= CUs: one round of shorter K-loops, then k_splitk_reduce sums the fp32
+// slabs in slice order and applies the epilogue.  E.g. the 12 x 12 neck conv of DPT-Large
+// (M 4608, N 256, K 9216): 18 tiles of 144 K-steps -> 14 slices of 11.
+struct SplitPlan {
+  int splits = 0, kspan = 0, bm = 0, bn = 0;
+  int64_t bytes = 0;
+};
+
+static SplitPlan split_for(const Args& p, const Plan& pl) {
+  SplitPlan sp;
+  if (!g_splitk || pl.kind != 0 || (g_engine != 0 && g_engine != 3)) return sp;   // automatic modes only
+  int bm, bn;
+  if (p.N % 256 == 0) bm = bn = 256;
+  else if (p.N % 128 == 0) bm = bn = 128;
+  else return sp;
+  const int64_t ncu = num_cus();
+  const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * (p.N / bn);
+  if (tiles * 2 > ncu || (int64_t)p.M * (p.N / 4) >= (int64_t)1 << 31) return sp;
+  const int nk = p.K / 64;
+  // K >= 4096 only: at K = 1024-2304 the slab traffic and the second launch ate the gain
+  // (DPT-Large neck, tools/gemm_census.py: K 2304 47 -> 59 us, the CLS readout 21 -> 25 us)
+  if (nk < (g_splitk > 1 ? g_splitk : 64)) return sp;   // knob value > 1: minimum K-steps instead
+  const int s0 = (int)std::min<int64_t>(ncu / tiles, nk / 4);
+  if (s0 < 2) return sp;
+  sp.kspan = (nk + s0 - 1) / s0;
+  sp.splits = (nk + sp.kspan - 1) / sp.kspan;
+  if (sp.splits < 2) return SplitPlan{};
+  sp.bm = bm;
+  sp.bn = bn;
+  sp.bytes = (int64_t)sp.splits * p.M * p.N * 4;
+  return sp;
+}
+
+template <bool CONV, bool RELU_A>
+static int run_split(const SplitPlan& sp, const Args& p, float* ws, hipStream_t s) {
+  Args q = p;   // raw partial sums: no bias / act / residuals, dense fp32 rows of N
+  q.bias = nullptr;
+  q.rbias = nullptr;
+  q.tbl = nullptr;
+  q.act = 0;
+  q.res = nullptr;
+  q.res2 = nullptr;
+  q.C = ws;
+  q.c_f32 = 1;
+  q.ldc = p.N;
+  q.o_g = q.o_gs = q.o_o = 0;
+  q.ct_s = 0;
+  q.kspan = sp.kspan;
+  if (sp.bm == 256) launch<256, 256, 2, 4, 64, CONV, RELU_A>(q, s, sp.splits);
+  else launch<128, 128, 2, 2, 64, CONV, RELU_A>(q, s, sp.splits);
+  const int64_t n = (int64_t)p.M * (p.N / 4);
+  hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, ws, sp.splits);
+  return check_launch("gemm (split-K)");
 }
 
 // I2PC_GEMM_Q=1: the quarter-pipelined engine (k_gemm_q) replaces k_gemm_p wherever the
@@ -1802,8 +1892,14 @@ static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
   return check_launch("gemm");
 }
 
-static const char* plan_name(const Plan& pl, bool conv, bool relu) {
+static const char* plan_name(const Plan& pl, bool conv, bool relu, const SplitPlan& sp = SplitPlan{}) {
   static thread_local char buf[96];
+  if (sp.splits > 1) {
+    const int wm = 2, wn = sp.bn == 256 ? 4 : 2;
+    snprintf(buf, sizeof buf, "k_gemm<%d, %d, %d, %d, 64, %s, %s> split-K %d", sp.bm, sp.bn, wm, wn,
+             conv ? "true" : "false", relu ? "true" : "false", sp.splits);
+    return buf;
+  }
   const char* c = conv ? "true" : "false";
   const char* r = relu ? "true" : "false";
   if (pl.kind == 2) {
@@ -1930,7 +2026,7 @@ static int make_args(const i2pc_gemm_desc* d, gemm::Args& p) {
   return I2PC_OK;
 }
 
-extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) {
+extern "C" int i2pc_gemm_ws(const i2pc_gemm_desc* d, void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   gemm::Args p;
   const int rc = make_args(d, p);
@@ -1938,8 +2034,24 @@ extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) {
   hipStream_t s = as_stream(stream);
   const bool conv = d->conv != 0, relu = d->conv_relu_in != 0;
   const gemm::Plan pl = gemm::plan_for(p, conv, relu);
+  const gemm::SplitPlan sp = gemm::split_for(p, pl);
+  if (sp.splits > 1 && workspace && (int64_t)workspace_bytes >= sp.bytes) {
+    I2PC_REQUIRE(reinterpret_cast<uintptr_t>(workspace) % 16 == 0, "gemm workspace must be 16-byte aligned");
+    float* ws = static_cast<float*>(workspace);
+    if (conv) return relu ? gemm::run_split<true, true>(sp, p, ws, s) : gemm::run_split<true, false>(sp, p, ws, s);
+    return relu ? gemm::run_split<false, true>(sp, p, ws, s) : gemm::run_split<false, false>(sp, p, ws, s);
+  }
   if (conv) return relu ? gemm::run_plan<true, true>(pl, p, s) : gemm::run_plan<true, false>(pl, p, s);
   return relu ? gemm::run_plan<false, true>(pl, p, s) : gemm::run_plan<false, false>(pl, p, s);
+}
+
+extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) { return i2pc_gemm_ws(d, nullptr, 0, stream); }
+
+extern "C" size_t i2pc_gemm_workspace_bytes(const i2pc_gemm_desc* d) {
+  gemm::Args p;
+  if (make_args(d, p) != I2PC_OK) return 0;
+  const gemm::SplitPlan sp = gemm::split_for(p, gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0));
+  return sp.splits > 1 ? (size_t)sp.bytes : 0;
 }
 
 static int make_args8(const i2pc_gemm_fp8_desc* d8, gemm::Args& p) {
@@ -1988,7 +2100,8 @@ extern "C" const char* i2pc_gemm_fp8_kernel_name(const i2pc_gemm_fp8_desc* d8) {
 extern "C" const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* d) {
   gemm::Args p;
   if (make_args(d, p) != I2PC_OK) return "invalid";
-  return gemm::plan_name(gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0), d->conv != 0, d->conv_relu_in != 0);
+  const gemm::Plan pl = gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0);
+  return gemm::plan_name(pl, d->conv != 0, d->conv_relu_in != 0, gemm::split_for(p, pl));
 }
 
 extern "C" int i2pc_gemm_set_engine(int mode) {
@@ -2004,5 +2117,6 @@ extern "C" int i2pc_gemm_set_engine(int mode) {
 bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
+  if (std::strcmp(name, "gemm_splitk") == 0) { i2pc::gemm::g_splitk = value; return true; }
   return false;
 }

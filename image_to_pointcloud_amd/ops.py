@@ -38,6 +38,8 @@ class GemmDesc(ctypes.Structure):
 
 
 _lib.register("i2pc_gemm", ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p])
+_lib.register("i2pc_gemm_ws", ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p, ctypes.c_size_t, c_void_p])
+_lib.register("i2pc_gemm_workspace_bytes", ctypes.c_size_t, [ctypes.POINTER(GemmDesc)])
 _lib.register("i2pc_gemm_kernel_name", ctypes.c_char_p, [ctypes.POINTER(GemmDesc)])
 _lib.register("i2pc_gemm_set_engine", ctypes.c_int, [ctypes.c_int])
 _lib.register("i2pc_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
@@ -118,7 +120,8 @@ def gemm_kernel_label(desc: GemmDesc) -> str:
 
 
 def set_tuning(name: str, value: int) -> None:
-    """Kernel-selection knob (i2pc_set_tuning): gemm_tail, unp_rows, unp_nt, unp_rpt."""
+    """Kernel-selection knob (i2pc_set_tuning): gemm_tail, gemm_bn128, gemm_splitk, unp_rows, unp_nt,
+    unp_rpt, attn_lazy, attn_scalar."""
     _lib.call("i2pc_set_tuning", name.encode(), int(value))
 
 
@@ -144,11 +147,15 @@ def gemm_bytes(d: GemmDesc, esz: float = 2.0, c_esz: float = None) -> float:
 
 
 def gemm(desc: GemmDesc) -> None:
+    """i2pc_gemm_ws with a split-K workspace from torch's stream-ordered caching allocator when
+    the call splits (inside a graph capture it comes from the graph's pool, so replays own it)."""
+    nb = _lib.load().i2pc_gemm_workspace_bytes(ctypes.byref(desc))
+    ws = _torch().empty(nb, dtype=_torch().uint8, device="cuda") if nb else None
     if profile is None:
-        _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
+        _lib.call("i2pc_gemm_ws", ctypes.byref(desc), _p(ws), nb, _stream())
         return
     with _Timed(gemm_kernel_label(desc), 2.0 * desc.m * desc.n * desc.k, gemm_bytes(desc)):
-        _lib.call("i2pc_gemm", ctypes.byref(desc), _stream())
+        _lib.call("i2pc_gemm_ws", ctypes.byref(desc), _p(ws), nb, _stream())
 
 
 def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=False,

@@ -212,6 +212,15 @@ typedef struct i2pc_gemm_desc {
 
 int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
 
+/* i2pc_gemm with a caller-owned device workspace (16-byte aligned) for split-K: calls the
+ * tile kernel would run on at most half the CUs with a long K (e.g. the 12x12 and 24x24 neck
+ * convs, K = 9216) are split into K slices whose fp32 partial sums go to the workspace and
+ * are then reduced in slice order with the same epilogue.  i2pc_gemm_workspace_bytes(desc)
+ * is the size that call uses (0 = no split; a smaller or NULL workspace runs unsplit).
+ * Automatic engine modes (0, 3) only; knob "gemm_splitk" (i2pc_set_tuning) turns it off. */
+int i2pc_gemm_ws(const i2pc_gemm_desc* desc, void* workspace, size_t workspace_bytes, void* stream);
+size_t i2pc_gemm_workspace_bytes(const i2pc_gemm_desc* desc);
+
 /* MX fp8 GEMM / implicit-GEMM convolution (the DPT-Hybrid fp8 path, BASELINE configs[4]):
  * the same contract as i2pc_gemm with A and W in OCP e4m3fn (1 byte per element; lda, ldw
  * and ldc in ELEMENTS = bytes) and one E8M0 scale per 32 consecutive k:
@@ -283,17 +292,20 @@ const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* desc);
 int i2pc_gemm_set_engine(int mode);
 
 /* Process-wide kernel-selection knobs for A/B measurement (not part of the drop-in surface;
- * every setting computes the same results bit for bit):
+ * every setting but gemm_splitk computes the same results bit for bit):
  *   "gemm_tail"   1 = split the last round of a persistent GEMM into 256 x 128 tiles where that
  *                 saves a round
  *   "gemm_bn128"  1 = the persistent engine with 256 x 128 tiles for N % 256 != 0, N % 128 == 0
+ *   "gemm_splitk" 1 = split-K for few-tile long-K calls given a workspace (i2pc_gemm_ws); the one
+ *                 knob that changes results: the fp32 partial sums are added in another order
+ *                 (within the network parity tolerance, tests/test_gemm_engines_gpu.py)
  *   "unp_rows"    1 = the row-sweep unprojection kernel
  *   "unp_nt"      1 = non-temporal point stores
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
  *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
- * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _UNP_ROWS / _UNP_NT / _UNP_RPT / _ATTN_LAZY /
- * _ATTN_SCALAR environment variables, else 1, 1, 1, 1, 8, 1, 1.  A HIP graph keeps the kernels
+ * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _UNP_ROWS / _UNP_NT / _UNP_RPT /
+ * _ATTN_LAZY / _ATTN_SCALAR environment variables, else 1, 1, 1, 1, 1, 8, 1, 1.  A HIP graph keeps the kernels
  * it captured: re-capture after changing a knob. */
 int i2pc_set_tuning(const char* name, int value);
 

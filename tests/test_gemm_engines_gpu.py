@@ -1,5 +1,5 @@
 """The persistent 256-column GEMM engines (single-stage k_gemm_p, ping-pong k_gemm_8p) against the
-tile kernel (bit-exact) and torch fp32.
+tile kernel (bit-exact) and torch fp32; split-K against the unsplit tile kernel and torch fp32.
 
 Both engines accumulate the same MFMA sequence and apply the epilogue in the same
 fp32 order (bias, activation, residual, second residual, bf16 rounding), so their
@@ -8,6 +8,7 @@ outputs must be identical bit for bit.  Shapes cover several tiles per workgroup
 partial last M-tile, K = 64 (one K-step per tile), and every epilogue the engine
 implements.  torch tolerance: relative Frobenius error <= 8e-3.
 """
+import ctypes
 import math
 
 import pytest
@@ -37,9 +38,15 @@ def _both(fn):
             outs.append(fn().clone())
     finally:
         ops.set_gemm_engine(0)
-    auto = fn()
+    try:   # split-K (automatic modes) adds partial sums in another order: compared below
+        ops.set_tuning("gemm_splitk", 0)
+        auto = fn().clone()
+    finally:
+        ops.set_tuning("gemm_splitk", 1)
+    split = fn()
     torch.cuda.synchronize()
     assert torch.equal(auto, outs[0]), "automatic engine choice differs from the tile kernel"
+    assert _fro(split, outs[0]) <= 2e-3, f"split-K vs unsplit: {_fro(split, outs[0])}"
     assert torch.equal(outs[2], outs[0]), \
         f"ping-pong engine differs from the tile kernel: {(outs[2].float() - outs[0].float()).abs().max().item()}"
     return outs[1], outs[0]
@@ -160,3 +167,82 @@ def test_conv_transpose_engines_bitexact(s, C):
     assert torch.equal(got, ref)
     r = F.conv_transpose2d(x.float().permute(0, 3, 1, 2), _bf(w).float(), b, stride=s).permute(0, 2, 3, 1)
     assert _fro(got, r) <= 8e-3
+
+
+def _label_of_conv(ops, x, w, k, stride, relu_in):
+    B, H, W, C = x.shape
+    OH, OW = (H + 2 - k) // stride + 1, (W + 2 - k) // stride + 1
+    d = ops.GemmDesc()
+    d.a, d.m, d.n, d.k = x.data_ptr(), B * OH * OW, w.shape[0], w.shape[1]
+    d.conv, d.conv_batch, d.conv_h, d.conv_w, d.conv_c = 1, B, H, W, C
+    d.conv_oh, d.conv_ow, d.conv_k, d.conv_stride, d.conv_pad, d.conv_relu_in = OH, OW, k, stride, 1, int(relu_in)
+    d.w, d.ldw = w.data_ptr(), w.stride(0)
+    d.c, d.ldc = x.data_ptr(), w.shape[0]
+    return ops.gemm_kernel_label(d), ops._lib.load().i2pc_gemm_workspace_bytes(ctypes.byref(d))
+
+
+@pytest.mark.parametrize("B,H,C,Co,stride,mode", [(32, 12, 1024, 256, 1, "plain"), (32, 24, 1024, 256, 1, "plain"),
+                                                  (32, 24, 1024, 1024, 2, "plain"), (32, 12, 512, 256, 1, "relu"),
+                                                  (32, 12, 512, 256, 1, "res2"), (7, 24, 512, 128, 1, "plain")])
+def test_conv_split_k(B, H, C, Co, stride, mode):
+    """Few-tile long-K convs of the DPT neck (12x12 / 24x24 maps, K = 9 * Cin) run split-K: the
+    label says so, the workspace size is what the plan needs, results are deterministic, within
+    2e-3 (relative Frobenius) of the unsplit tile kernel and 8e-3 of torch fp32."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(B + H + C + Co)
+    x = _bf(torch.randn(B, H, H, C, generator=g)).to(dev)
+    w = (torch.randn(Co, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    b = (torch.randn(Co, generator=g) * 0.1).to(dev)
+    wp = _pack_conv(w)
+    OH = (H - 1) // stride + 1
+    r1 = _bf(torch.randn(B, OH, OH, Co, generator=g)).to(dev)
+    r2 = _bf(torch.randn(B, OH, OH, Co, generator=g)).to(dev)
+    relu_in = mode == "relu"
+    kw = dict(bias=b, stride=stride, relu_in=relu_in, act="relu" if relu_in else None)
+    if mode == "res2":
+        kw.update(res=r1, res2=r2)
+    lab, nb = _label_of_conv(ops, x, wp, 3, stride, relu_in)
+    assert "split-K" in lab and nb > 0, lab
+    got = ops.conv2d(x, wp, **kw).clone()
+    again = ops.conv2d(x, wp, **kw)
+    assert torch.equal(got, again), "split-K is not deterministic"
+    try:
+        ops.set_tuning("gemm_splitk", 0)
+        assert "split-K" not in _label_of_conv(ops, x, wp, 3, stride, relu_in)[0]
+        unsplit = ops.conv2d(x, wp, **kw).clone()
+    finally:
+        ops.set_tuning("gemm_splitk", 1)
+    e_unsplit = _fro(got, unsplit)
+    xin = F.relu(x.float()) if relu_in else x.float()
+    r = F.conv2d(xin.permute(0, 3, 1, 2), _bf(w).float(), b, stride=stride, padding=1).permute(0, 2, 3, 1)
+    if relu_in:
+        r = F.relu(r)
+    if mode == "res2":
+        r = r + r1.float() + r2.float()
+    e_ref = _fro(got, r)
+    print(f"split-K {lab}: vs unsplit {e_unsplit:.2e}, vs torch fp32 {e_ref:.2e}")
+    assert e_unsplit <= 2e-3 and e_ref <= 8e-3
+
+
+@pytest.mark.parametrize("M,N,K,act", [(300, 256, 4096, "gelu"), (32, 1024, 1024, None)])
+def test_linear_split_k(M, N, K, act):
+    """A dense few-tile long-K GEMM splits (16 slices here); K = 1024 (the CLS readout) does not."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    x = _bf(torch.randn(M, K, generator=g)).to(dev)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    lab = ops.gemm_kernel_label(_desc_of(ops, x, w, b, out))
+    assert ("split-K" in lab) == (K >= 4096), lab
+    got = ops.linear(x, w, bias=b, act=act, out=out).clone()
+    try:
+        ops.set_tuning("gemm_splitk", 0)
+        unsplit = ops.linear(x, w, bias=b, act=act, out=out).clone()
+    finally:
+        ops.set_tuning("gemm_splitk", 1)
+    y = x.float() @ w.float().T + b
+    y = F.gelu(y) if act == "gelu" else y
+    assert _fro(got, unsplit) <= 2e-3 and _fro(got, y) <= 8e-3

@@ -10,6 +10,7 @@
 #   full                       check + profile of C2 (dpt-large-bf16) and C5 (dpt-hybrid-fp8, batch 64)
 #   bench                      the default bench line (with the CPU baseline), as the driver runs it
 #   ab-pipe [args]             tools/ab_pipeline.py: kernel-selection knobs A/B on the bench pipeline, one process
+#   census [args]              tools/gemm_census.py: every network launch with shape, kernel and rate
 #   ab-gemm                    GEMM engine tests + tools/bench_gemm_ab.py (engine modes, interleaved)
 #   unp                        geometry parity tests, unprojection microbench (warm / cold) per kernel variant
 #   trace-unp [B] [density]    kernel durations of the unprojection microbench (kernel trace only)
@@ -93,6 +94,9 @@ case "$TASK" in
   ab-pipe)
     timeout -k 10 600 python -u tools/ab_pipeline.py "$@" > gpurun_out/ab_pipe.log 2>&1; rc=$?
     grep -v amdgpu.ids gpurun_out/ab_pipe.log; exit $rc ;;
+  census)
+    timeout -k 10 300 python -u tools/gemm_census.py "$@" > gpurun_out/census.txt 2>&1; rc=$?
+    grep -v amdgpu.ids gpurun_out/census.txt; exit $rc ;;
   ab-gemm)
     timeout -k 10 300 python -u -m pytest tests/test_gemm_engines_gpu.py -x -q --timeout 120 --timeout-method thread \
       > gpurun_out/eng.log 2>&1 || { tail -15 gpurun_out/eng.log; exit 1; }
