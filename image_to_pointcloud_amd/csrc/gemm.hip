@@ -1642,6 +1642,9 @@ static int g_bn128 = [] { const char* e = getenv("I2PC_GEMM_BN128"); return e ? 
 // split-K for calls the tile kernel would run with few tiles and a long K (I2PC_GEMM_SPLITK /
 // "gemm_splitk"; needs the caller's workspace, i2pc_gemm_ws)
 static int g_splitk = [] { const char* e = getenv("I2PC_GEMM_SPLITK"); return e ? atoi(e) : 1; }();
+// split-K tile: 0 = 256 x 256 x 64 (one block per CU), 1 = 128 x 128 x 32 (32 KB of LDS: ~4 blocks
+// per CU cover each other's load latency)
+static int g_split_tile = [] { const char* e = getenv("I2PC_GEMM_SPLIT_TILE"); return e ? atoi(e) : 0; }();
 
 static int64_t max_row(const Args& p) {
   const int64_t m = p.M - 1;
@@ -1742,31 +1745,33 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
 // slabs in slice order and applies the epilogue.  E.g. the 12 x 12 neck conv of DPT-Large
 // (M 4608, N 256, K 9216): 18 tiles of 144 K-steps -> 14 slices of 11.
 struct SplitPlan {
-  int splits = 0, kspan = 0, bm = 0, bn = 0;
+  int splits = 0, kspan = 0, bm = 0, bn = 0, kb = 64;
   int64_t bytes = 0;
 };
 
 static SplitPlan split_for(const Args& p, const Plan& pl) {
   SplitPlan sp;
   if (!g_splitk || pl.kind != 0 || (g_engine != 0 && g_engine != 3)) return sp;   // automatic modes only
-  int bm, bn;
-  if (p.N % 256 == 0) bm = bn = 256;
+  int bm, bn, kb = 64, slots = 1;
+  if (g_split_tile == 1 && p.N % 128 == 0) { bm = bn = 128; kb = 32; slots = 4; }
+  else if (p.N % 256 == 0) bm = bn = 256;
   else if (p.N % 128 == 0) bm = bn = 128;
   else return sp;
-  const int64_t ncu = num_cus();
+  const int64_t ncu = num_cus() * slots;
   const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * (p.N / bn);
   if (tiles * 2 > ncu || (int64_t)p.M * (p.N / 4) >= (int64_t)1 << 31) return sp;
-  const int nk = p.K / 64;
+  if (p.K < (g_splitk > 1 ? g_splitk * 64 : 4096)) return sp;
+  const int nk = p.K / kb;
   // K >= 4096 only: at K = 1024-2304 the slab traffic and the second launch ate the gain
   // (DPT-Large neck, tools/gemm_census.py: K 2304 47 -> 59 us, the CLS readout 21 -> 25 us)
-  if (nk < (g_splitk > 1 ? g_splitk : 64)) return sp;   // knob value > 1: minimum K-steps instead
-  const int s0 = (int)std::min<int64_t>(ncu / tiles, nk / 4);
+  const int s0 = (int)std::min<int64_t>(ncu / tiles, nk / (256 / kb));   // slices of >= 256 K
   if (s0 < 2) return sp;
   sp.kspan = (nk + s0 - 1) / s0;
   sp.splits = (nk + sp.kspan - 1) / sp.kspan;
   if (sp.splits < 2) return SplitPlan{};
   sp.bm = bm;
   sp.bn = bn;
+  sp.kb = kb;
   sp.bytes = (int64_t)sp.splits * p.M * p.N * 4;
   return sp;
 }
@@ -1787,6 +1792,7 @@ static int run_split(const SplitPlan& sp, const Args& p, float* ws, hipStream_t 
   q.ct_s = 0;
   q.kspan = sp.kspan;
   if (sp.bm == 256) launch<256, 256, 2, 4, 64, CONV, RELU_A>(q, s, sp.splits);
+  else if (sp.kb == 32) launch<128, 128, 2, 2, 32, CONV, RELU_A>(q, s, sp.splits);
   else launch<128, 128, 2, 2, 64, CONV, RELU_A>(q, s, sp.splits);
   const int64_t n = (int64_t)p.M * (p.N / 4);
   hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, ws, sp.splits);
@@ -1842,24 +1848,27 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
 // (e.g. M = 18464, N = 3072: 3 rounds + a half round instead of 4).  Plain dense epilogue
 // with a linear output row map only; the two parts compute every output exactly as one launch
 // would (same per-output accumulation order).  I2PC_GEMM_TAIL=0 disables it.
-static bool tail_split(const Args& p, int& ma) {
-  if (!g_tail || p.o_g != 0 || p.a_g != 0 || p.ct_s > 0 || p.N % 256 != 0) return false;
+// (Measured and dropped: FC1's remainder, M = 18464, N = 4096, as one round of the tile kernel's
+// 192 x 256 tiles instead of a fifth persistent round -- no gain end to end.)
+// Returns 0 (no split) or 1 (BN = 128 persistent remainder).
+static int tail_split(const Args& p, int& ma) {
+  if (!g_tail || p.o_g != 0 || p.a_g != 0 || p.ct_s > 0 || p.N % 256 != 0) return 0;
   const int64_t tn = p.N / 256, tm = (p.M + 255) / 256, T = tm * tn, G = num_cus();
   const int64_t rounds = T / G;
-  if (T % G == 0 || rounds < 1 || (rounds * G) % tn != 0) return false;
+  if (T % G == 0 || rounds < 1 || (rounds * G) % tn != 0) return 0;
   const int64_t mt = rounds * G / tn;
-  if (mt >= tm) return false;
-  const int64_t half_tiles = (tm - mt) * 2 * tn;
-  if (half_tiles > G) return false;
+  if (mt >= tm) return 0;
   ma = (int)(mt * 256);
-  return true;
+  const int64_t half_tiles = (tm - mt) * 2 * tn;
+  return half_tiles <= G ? 1 : 0;
 }
 
 template <bool CONV, bool RELU_A>
 static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
   if constexpr (!CONV && !RELU_A) {
     int ma = 0;
-    if ((pl.kind == 1 || pl.kind == 2) && pl.epi == pers::EPI_PLAIN && !g_quarter && tail_split(p, ma)) {
+    const int ts = (pl.kind == 1 || pl.kind == 2) && pl.epi == pers::EPI_PLAIN && !g_quarter ? tail_split(p, ma) : 0;
+    if (ts) {
       Args pa = p, pb = p;
       pa.M = ma;
       pb.M = p.M - ma;
@@ -1896,7 +1905,7 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu, const SplitPl
   static thread_local char buf[96];
   if (sp.splits > 1) {
     const int wm = 2, wn = sp.bn == 256 ? 4 : 2;
-    snprintf(buf, sizeof buf, "k_gemm<%d, %d, %d, %d, 64, %s, %s> split-K %d", sp.bm, sp.bn, wm, wn,
+    snprintf(buf, sizeof buf, "k_gemm<%d, %d, %d, %d, %d, %s, %s> split-K %d", sp.bm, sp.bn, wm, wn, sp.kb,
              conv ? "true" : "false", relu ? "true" : "false", sp.splits);
     return buf;
   }
@@ -2118,5 +2127,6 @@ bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
   if (std::strcmp(name, "gemm_splitk") == 0) { i2pc::gemm::g_splitk = value; return true; }
+  if (std::strcmp(name, "gemm_split_tile") == 0) { i2pc::gemm::g_split_tile = value; return true; }
   return false;
 }
