@@ -210,6 +210,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   const int rows = ni * 16;
   for (int r0 = 0; r0 < rows; r0 += RPP) {
     const int r = r0 + rr;
+    // TN = 96: 12 lanes per row, 5 rows per pass (60 lanes), and 48 rows are not a multiple of 5
+    if (LPR * RPP < 64 && (rr >= RPP || r >= rows)) continue;
     const int m = mrow0 + i0 * 16 + r;
     const int u0 = (2 * c8) ^ (r & SW), u1 = (2 * c8 + 1) ^ (r & SW);
     const float4 a = *reinterpret_cast<const float4*>(lds + r * TN + u0 * 4);
@@ -1644,6 +1646,8 @@ static int g_bn128 = [] { const char* e = getenv("I2PC_GEMM_BN128"); return e ? 
 static int g_splitk = [] { const char* e = getenv("I2PC_GEMM_SPLITK"); return e ? atoi(e) : 1; }();
 // split-K tile: 0 = 256 x 256 x 64 (one block per CU), 1 = 128 x 128 x 32 (32 KB of LDS: ~4 blocks
 // per CU cover each other's load latency)
+// 384 x 192 tiles for N % 192 == 0 calls that fit one round (I2PC_GEMM_TILE192 / "gemm_tile192")
+static int g_tile192 = [] { const char* e = getenv("I2PC_GEMM_TILE192"); return e ? atoi(e) : 1; }();
 static int g_split_tile = [] { const char* e = getenv("I2PC_GEMM_SPLIT_TILE"); return e ? atoi(e) : 0; }();
 
 static int64_t max_row(const Args& p) {
@@ -1732,6 +1736,10 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   else if (p.N % 256 == 0 && p.K >= 1024 && (int64_t)((p.M + 319) / 320) * (p.N / 256) <= num_cus() &&
            t256 > num_cus()) pl = Plan{0, 320, 256, 64};
   else if (p.N % 256 == 0 && t256 >= 512) pl = Plan{0, 256, 256, 64};
+  // N = 384 (Depth-Anything-V2-Small's FC2 / attention-out, M = 43840): one round of 384 x 192
+  // tiles (230) instead of four-plus rounds of 128 x 128
+  else if (p.N % 256 != 0 && p.N % 192 == 0 && (int64_t)((p.M + 383) / 384) * (p.N / 192) <= num_cus() &&
+           t128 > num_cus() && g_tile192) pl = Plan{0, 384, 192, 64};
   else if (p.N % 128 == 0 && t128 >= 512) pl = Plan{0, 128, 128, 64};
   else if (p.N % 64 == 0) pl = Plan{0, 128, 64, 64};
   else if (p.N % 32 == 0) pl = Plan{0, 128, 32, 64};
@@ -1894,6 +1902,7 @@ static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
   else if (pl.bm == 256) launch<256, 256, 2, 4, 32, CONV, RELU_A>(p, s);
   else if (pl.bm == 320) launch<320, 256, 2, 4, 64, CONV, RELU_A>(p, s);
   else if (pl.bm == 192) launch<192, 256, 2, 4, 64, CONV, RELU_A>(p, s);
+  else if (pl.bm == 384) launch<384, 192, 4, 2, 64, CONV, RELU_A>(p, s);
   else if (pl.bn == 128 && pl.epi == 64) launch<128, 128, 2, 2, 64, CONV, RELU_A>(p, s);
   else if (pl.bn == 128) launch<128, 128, 2, 2, 32, CONV, RELU_A>(p, s);
   else if (pl.bn == 64) launch<128, 64, 2, 2, 64, CONV, RELU_A>(p, s);
@@ -1919,7 +1928,7 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu, const SplitPl
     else if (pl.bn == 128) snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s, 128>", pl.bm, c, r, epis[pl.epi]);
     else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
   } else if (pl.kind == 0) {
-    const int wm = pl.bn == 32 ? 4 : 2, wn = pl.bn == 256 ? 4 : pl.bn == 32 ? 1 : 2;
+    const int wm = pl.bn == 32 || pl.bn == 192 ? 4 : 2, wn = pl.bn == 256 ? 4 : pl.bn == 32 ? 1 : 2;
     snprintf(buf, sizeof buf, "k_gemm<%d, %d, %d, %d, %d, %s, %s>", pl.bm, pl.bn, wm, wn, pl.epi, c, r);
   } else {
     snprintf(buf, sizeof buf, "unsupported");
@@ -2128,5 +2137,6 @@ bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
   if (std::strcmp(name, "gemm_splitk") == 0) { i2pc::gemm::g_splitk = value; return true; }
   if (std::strcmp(name, "gemm_split_tile") == 0) { i2pc::gemm::g_split_tile = value; return true; }
+  if (std::strcmp(name, "gemm_tile192") == 0) { i2pc::gemm::g_tile192 = value; return true; }
   return false;
 }

@@ -247,3 +247,37 @@ def test_linear_split_k(M, N, K, act):
     y = x.float() @ w.float().T + b
     y = F.gelu(y) if act == "gelu" else y
     assert _fro(got, unsplit) <= 2e-3 and _fro(got, y) <= 8e-3
+
+
+@pytest.mark.parametrize("M,N,K,res", [(43840, 384, 1536, True), (43840, 384, 384, True), (5000, 384, 640, False)])
+def test_tile_384x192_bitexact(M, N, K, res):
+    """Depth-Anything-V2-Small's N = 384 GEMMs (FC2, attention-out: fp32 residual) on one round of
+    384 x 192 tiles: bit-identical to the 128 x 128 tiles they replace, within 8e-3 of torch fp32."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    h = _bf(torch.randn(M, K, generator=g)).to(dev)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    x0 = torch.randn(M, N, generator=g).to(dev)
+
+    def run():
+        if res:
+            x = x0.clone()
+            ops.linear(h, w, bias=b, res=x, out=x)
+            return x
+        return ops.linear(h, w, bias=b, act="gelu").clone()
+    d = _desc_of(ops, h, w, b, x0)
+    lab = ops.gemm_kernel_label(d)
+    assert lab.startswith("k_gemm<384, 192") == (M >= 40000), lab
+    got = run()
+    try:
+        ops.set_tuning("gemm_tile192", 0)
+        assert not ops.gemm_kernel_label(d).startswith("k_gemm<384, 192")
+        ref = run()
+    finally:
+        ops.set_tuning("gemm_tile192", 1)
+    assert torch.equal(got, ref)
+    y = h.float() @ w.float().T + b
+    y = x0 + y if res else F.gelu(y)
+    assert _fro(got, y) <= 8e-3
