@@ -26,11 +26,13 @@ extern "C" const char* i2pc_last_error(void) { return i2pc::g_err; }
 bool i2pc_gemm_tune(const char* name, int value);        // gemm.hip
 bool i2pc_unproject_tune(const char* name, int value);   // unproject.hip
 bool i2pc_attention_tune(const char* name, int value);   // attention.hip
+bool i2pc_misc_tune(const char* name, int value);        // misc.hip
 
 extern "C" int i2pc_set_tuning(const char* name, int value) {
   i2pc::clear_error();
   I2PC_REQUIRE(name, "NULL tuning name");
-  if (i2pc_gemm_tune(name, value) || i2pc_unproject_tune(name, value) || i2pc_attention_tune(name, value))
+  if (i2pc_gemm_tune(name, value) || i2pc_unproject_tune(name, value) || i2pc_attention_tune(name, value) ||
+      i2pc_misc_tune(name, value))
     return I2PC_OK;
-  return i2pc::set_error(I2PC_EINVAL, "unknown tuning knob '%s' (gemm_tail, gemm_bn128, gemm_splitk, unp_rows, unp_nt, unp_rpt, attn_lazy, attn_scalar)", name);
+  return i2pc::set_error(I2PC_EINVAL, "unknown tuning knob '%s' (gemm_tail, gemm_bn128, gemm_splitk, unp_rows, unp_nt, unp_rpt, attn_lazy, attn_scalar, ln_f2)", name);
 }

@@ -5,6 +5,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace i2pc {
 namespace misc {
@@ -58,6 +59,41 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
     o.x = pack2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
     o.y = pack2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
     yr[i * 64 + lane] = o;
+  }
+}
+
+// dim % 128 == 0 but not % 256 (Depth-Anything-V2-Small's 384): one wave per row, V float2 per
+// lane, every load unconditional and in flight together (k_layernorm_any's runtime-bounded loop
+// predicates each load and waits for it: 3.7 TB/s at dim 384)
+template <int V>
+__global__ __launch_bounds__(256) void k_layernorm2(const float* __restrict__ x, int64_t ldx,
+                                                    const float* __restrict__ g, const float* __restrict__ b,
+                                                    float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float2* xr = reinterpret_cast<const float2*>(x + row * ldx);
+  float2 v[V];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = xr[i * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < V; ++i) s += v[i].x + v[i].y;
+  const float mean = wave_sum(s) / (float)dim;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const float a = v[i].x - mean, c = v[i].y - mean;
+    q += a * a + c * c;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)dim + eps);
+  const float2* g2 = reinterpret_cast<const float2*>(g);
+  const float2* b2 = reinterpret_cast<const float2*>(b);
+  uint32_t* yr = reinterpret_cast<uint32_t*>(y + row * ldy);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const float2 gg = g2[i * 64 + lane], bb = b2[i * 64 + lane];
+    yr[i * 64 + lane] = pack2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
   }
 }
 
@@ -199,6 +235,13 @@ static int grid_for(int64_t work, int per_block = 256) {
 using namespace i2pc;
 using namespace i2pc::misc;
 
+static int g_ln2 = 1;   // "ln_f2": the float2 row kernel for dim 384
+
+bool i2pc_misc_tune(const char* name, int value) {
+  if (std::strcmp(name, "ln_f2") == 0) { g_ln2 = value; return true; }
+  return false;
+}
+
 extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
                               int rows, int dim, void* y, int64_t ldy, void* stream) {
   clear_error();
@@ -208,6 +251,10 @@ extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, c
   hipStream_t s = as_stream(stream);
   const dim3 grid((rows + 3) / 4), block(256);
   bf16_t* yy = static_cast<bf16_t*>(y);
+  if (dim == 384 && g_ln2) {
+    hipLaunchKernelGGL(k_layernorm2<3>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy);
+    return check_launch("layernorm");
+  }
   if (dim % 256 != 0) {
     hipLaunchKernelGGL(k_layernorm_any, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy);
     return check_launch("layernorm");

@@ -131,6 +131,12 @@ def test_layernorm(dev, rows, dim):
     be = torch.randn(dim, generator=g).to(dev)
     got = ops.layernorm(x, ga, be, 1e-12)
     _close(got, F.layer_norm(x, (dim,), ga, be, 1e-12))
+    if dim == 384:   # the float2 row kernel against the generic one
+        try:
+            ops.set_tuning("ln_f2", 0)
+            _close(got, ops.layernorm(x, ga, be, 1e-12))
+        finally:
+            ops.set_tuning("ln_f2", 1)
 
 
 @pytest.mark.parametrize("B,T,H", [(2, 577, 16), (1, 37, 6), (3, 1, 4), (2, 130, 12), (1, 1370, 6)])
