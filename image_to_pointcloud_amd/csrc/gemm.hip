@@ -1863,7 +1863,9 @@ static int tail_split(const Args& p, int& ma) {
   if (!g_tail || p.o_g != 0 || p.a_g != 0 || p.ct_s > 0 || p.N % 256 != 0) return 0;
   const int64_t tn = p.N / 256, tm = (p.M + 255) / 256, T = tm * tn, G = num_cus();
   const int64_t rounds = T / G;
-  if (T % G == 0 || rounds < 1 || (rounds * G) % tn != 0) return 0;
+  if (T % G == 0 || rounds < 1) return 0;
+  // whole M-tile rows in the full rounds (a few slots of the last one may idle: DA-v2's FC1,
+  // N = 1536, 6 tiles per row, 1032 tiles: 170 rows in 4 rounds + 24 half tiles, not 5 rounds)
   const int64_t mt = rounds * G / tn;
   if (mt >= tm) return 0;
   ma = (int)(mt * 256);

@@ -59,7 +59,7 @@ def _fro(got, ref):
 
 @pytest.mark.parametrize("M,N,K,act", [(8200, 2048, 1024, None), (18464, 3072, 64, "gelu"), (9000, 1024, 192, None), (4100, 4096, 512, "gelu"),
                                        (300, 256, 512, None), (257, 512, 128, "relu"), (20000, 384, 512, "gelu"),
-                                       (18464, 4096, 1024, "gelu")])
+                                       (18464, 4096, 1024, "gelu"), (43840, 1536, 384, "gelu")])
 def test_linear_plain_engines_bitexact(M, N, K, act):
     ops = _ops()
     dev = torch.device("cuda")
