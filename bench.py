@@ -47,7 +47,13 @@ def _peak(label: str) -> float:
 
 def _args():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without a torch.distributed.run environment, N > 1 "
+                         "starts torch.distributed.run with N ranks as a child process and relays its output")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend at N > 1: nccl (= RCCL over xGMI, one GPU per rank) or gloo "
+                         "(ranks may share a GPU: rank r uses device r %% device_count; the point gather is "
+                         "staged through host memory)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32)
@@ -141,10 +147,16 @@ def _pmc_traffic(tag: str):
         return json.load(fh).get("kernels", {}), os.path.relpath(files[-1], ROOT)
 
 
-def _traffic(table, src, *names):
+def _traffic(table, src, *names, calls_per_step=None):
+    """PMC HBM bytes per CALL of a kernel label: the label's dispatches of one step summed (a GEMM
+    call may be a main and a tail launch) / the calls per step; the per-dispatch average when the
+    table predates per-step sums or the call count is unknown."""
     for n in names:
         if n in table:
-            return table[n]["hbm_bytes_per_launch"], f"{src}: {n}"
+            e = table[n]
+            if calls_per_step and "hbm_bytes_per_step" in e:
+                return round(e["hbm_bytes_per_step"] / calls_per_step), f"{src}: {n} (per call)"
+            return e["hbm_bytes_per_launch"], f"{src}: {n} (per dispatch)"
     return None, None
 
 
@@ -170,7 +182,8 @@ def _cpu_baseline(spec, size, density, images=3):
     from image_to_pointcloud_amd.pipeline import default_processor
 
     threads = os.cpu_count() or 1
-    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    threads = min(threads, int(cap)) if cap else threads
     torch.set_num_threads(threads)
     if spec.family == "depth-anything":
         from transformers import DepthAnythingConfig as Cfg, DepthAnythingForDepthEstimation as Net
@@ -206,13 +219,39 @@ def _cpu_baseline(spec, size, density, images=3):
     return {"value": n / (t_net + t_geo) / 1e6, "unit": "Mpoints/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
             "sample": f"{images} images {size}x{size}, density {density} ({n} points): Pillow-exact preprocessing + "
-                      f"transformers fp32 {spec.name} forward on {threads} threads ({t_net:.2f} s) + the reference "
+                      f"transformers fp32 {spec.name} forward on {threads} threads"
+                      + (f" (capped by OMP_NUM_THREADS={cap}, the job's CPU share, of {os.cpu_count()} host threads)"
+                         if cap and threads < (os.cpu_count() or 1) else "")
+                      + f" ({t_net:.2f} s) + the reference "
                       f"per-point Python loop, single-threaded ({t_geo:.2f} s)",
             "seconds": t_net + t_geo}
 
 
+def _launch_ranks(a) -> int:
+    """`--gpus N > 1` without a torch.distributed.run environment: start N ranks as a CHILD
+    torch.distributed.run (this process has not touched the GPU: no exec after HIP init) and
+    return its exit code; rank 0's JSON line reaches our stdout unchanged."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = _args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(_launch_ranks(a))
+    if env_world is not None and int(env_world) != a.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -220,8 +259,18 @@ def main():
     rank, local, world = D.world()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ndev = torch.cuda.device_count()
+        if a.backend == "nccl":
+            if local >= ndev:
+                print(f"bench.py: rank {rank} needs GPU {local}, {ndev} visible (nccl needs one GPU per rank; "
+                      f"--backend gloo lets ranks share one)", file=sys.stderr)
+                sys.exit(2)
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(ndev, 1)
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -274,7 +323,8 @@ def main():
     kernels = None
     if rank == 0 and not a.no_kernel_profile:
         per, geo_t, unp_t = _kernel_profile(pipe, images)
-        pmc, pmc_src = _pmc_traffic(f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}"))
+        pmc, pmc_src = _pmc_traffic(f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
+                                    + ("" if a.density == "high" else f"-{a.density}"))
         dom = max(per.items(), key=lambda kv: kv[1]["t"])
         name, d = dom
         # the bound of a kernel: whichever of its algorithmic FLOPs (at the dtype's dense MFMA peak)
@@ -289,12 +339,14 @@ def main():
                         "launches": d["n"], "avg_us": round(d["t"] / d["n"] * 1e6, 2),
                         "flops_per_launch": d["flops"] / d["n"],
                         "share_of_step": round(d["t"] / (ms * 1e-3), 3)}
-            roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name)
+            roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name, calls_per_step=d["n"])
+            roofline["algorithmic_bytes_per_launch"] = round(d["bytes"] / d["n"])
+            if roofline["traffic"]:
+                roofline["traffic_over_algorithmic"] = round(roofline["traffic"] / (d["bytes"] / d["n"]), 3)
             if name.startswith("k_gemm_p"):
-                roofline["note"] = ("avg_us is per i2pc_gemm call: the persistent launch plus, where the round-"
-                                    "quantisation split applies (QKV), its 256x128 tail launch; rocprofv3 lists them "
-                                    "as k_gemm_p<..., 256, ...> and k_gemm_p<..., 128, ...>; traffic is the main "
-                                    "launch's")
+                roofline["note"] = ("avg_us and traffic are per i2pc_gemm call: the persistent launch plus, where "
+                                    "the round-quantisation split applies (QKV), its 256x128 tail launch; rocprofv3 "
+                                    "lists them as k_gemm_p<..., 256, ...> and k_gemm_p<..., 128, ...>")
         else:
             ach = d["bytes"] / (d["t"]) / 1e9
             roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -303,7 +355,9 @@ def main():
                         "bytes_per_launch": d["bytes"] / d["n"], "share_of_step": round(d["t"] / (ms * 1e-3), 3)}
             if d["flops"]:
                 roofline["tflops"] = round(d["flops"] / d["t"] / 1e12, 1)
-            roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name)
+            roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name, calls_per_step=d["n"])
+            if roofline["traffic"]:
+                roofline["traffic_over_algorithmic"] = round(roofline["traffic"] / (d["bytes"] / d["n"]), 3)
         geo_bytes = B * (4.0 * pipe.pre.out_h * pipe.pre.out_w + 18.0 * pipe.points_per_image)
         roof_geo = {"kernel": "i2pc_unproject (select + unproject + bbox launches)", "bound": "hbm",
                     "achieved": round(geo_bytes / geo_t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -319,7 +373,8 @@ def main():
                 "bytes_per_launch": geo_bytes, "bytes_per_point": 18.0,
                 "note": "algorithmic bytes 4*h'*w' + 18*N per image (SURVEY 8d), one launch per batch"}
             step = {"high": 1, "medium": 2, "low": 4}[pipe.density]
-            t, src = _traffic(pmc, pmc_src, f"k_unproject_rows<{step}>", f"k_unproject_fast<{step}>")
+            t, src = _traffic(pmc, pmc_src, f"k_unproject_rows<{step}>", f"k_unproject_fast<{step}>",
+                              calls_per_step=1)
             rooflines["unproject_kernel"].update(traffic=t, traffic_source=src)
         net_t = sum(v["t"] for v in per.values())
         net_f = sum(v["flops"] for v in per.values())
@@ -360,10 +415,13 @@ def main():
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": a.dtype, "data": f"synthetic (uint8 RGB uniform, PCG64 seeds 1000+i; seeded random {spec.name} weights)",
             "config": {"workload": f"{spec.name} {a.dtype} depth + unproject, batch {B} x {S}x{S} per GPU, density {a.density}"
-                                   + (", RCCL all-gather of every rank's points overlapped with the next step"
+                                   + ((", RCCL all-gather of every rank's points overlapped with the next step"
+                                       if a.backend == "nccl" else
+                                       ", gloo all-gather of every rank's points (host-staged, synchronous)")
                                       if gather else ""),
                        "model": spec.name, "network_input": [pipe.pre.out_h, pipe.pre.out_w], "global_batch": B * world,
                        "image": [S, S], "points_per_image": pipe.points_per_image, "parallelism": f"dp{world}",
+                       "backend": a.backend if world > 1 else None,
                        "hip_graph": not a.no_graph},
             "network_tflops": round(flops_img * B * world / (elapsed / a.steps) / 1e12, 1),
             "roofline": roofline,

@@ -433,9 +433,9 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
 using namespace i2pc;
 
 // lazy rescale on by default (I2PC_ATTN_LAZY / i2pc_set_tuning "attn_lazy")
-static int g_lazy = [] { const char* e = getenv("I2PC_ATTN_LAZY"); return e ? atoi(e) : 1; }();
+static thread_local int g_lazy = [] { const char* e = getenv("I2PC_ATTN_LAZY"); return e ? atoi(e) : 1; }();
 // scalar exponent FMAs (I2PC_ATTN_SCALAR / "attn_scalar")
-static int g_scalar = [] { const char* e = getenv("I2PC_ATTN_SCALAR"); return e ? atoi(e) : 1; }();
+static thread_local int g_scalar = [] { const char* e = getenv("I2PC_ATTN_SCALAR"); return e ? atoi(e) : 1; }();
 bool i2pc_attention_tune(const char* name, int value) {
   if (std::strcmp(name, "attn_lazy") == 0) { g_lazy = value; return true; }
   if (std::strcmp(name, "attn_scalar") == 0) { g_scalar = value; return true; }

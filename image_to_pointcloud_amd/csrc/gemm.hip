@@ -1630,25 +1630,25 @@ struct Plan {
 // initial value from I2PC_GEMM_P (0 -> 1, 2 -> 2)
 // 3 = automatic with the ping-pong engine where the persistent engine would run, 4 = ping-pong
 // engine wherever it applies (else the persistent engine wherever its epilogue applies)
-static int g_engine = [] {
+static thread_local int g_engine = [] {
   const char* e = getenv("I2PC_GEMM_P");
   if (!e) return 0;
   const int v = atoi(e);
   return v == 0 ? 1 : (v >= 2 && v <= 4) ? v : 0;
 }();
 
-static int g_tail = [] { const char* e = getenv("I2PC_GEMM_TAIL"); return e ? atoi(e) : 1; }();
+static thread_local int g_tail = [] { const char* e = getenv("I2PC_GEMM_TAIL"); return e ? atoi(e) : 1; }();
 // the persistent engine for N % 256 != 0, N % 128 == 0 (256 x 128 tiles; I2PC_GEMM_BN128 / "gemm_bn128")
-static int g_bn128 = [] { const char* e = getenv("I2PC_GEMM_BN128"); return e ? atoi(e) : 1; }();
+static thread_local int g_bn128 = [] { const char* e = getenv("I2PC_GEMM_BN128"); return e ? atoi(e) : 1; }();
 
 // split-K for calls the tile kernel would run with few tiles and a long K (I2PC_GEMM_SPLITK /
 // "gemm_splitk"; needs the caller's workspace, i2pc_gemm_ws)
-static int g_splitk = [] { const char* e = getenv("I2PC_GEMM_SPLITK"); return e ? atoi(e) : 1; }();
+static thread_local int g_splitk = [] { const char* e = getenv("I2PC_GEMM_SPLITK"); return e ? atoi(e) : 1; }();
 // split-K tile: 0 = 256 x 256 x 64 (one block per CU), 1 = 128 x 128 x 32 (32 KB of LDS: ~4 blocks
 // per CU cover each other's load latency)
 // 384 x 192 tiles for N % 192 == 0 calls that fit one round (I2PC_GEMM_TILE192 / "gemm_tile192")
-static int g_tile192 = [] { const char* e = getenv("I2PC_GEMM_TILE192"); return e ? atoi(e) : 1; }();
-static int g_split_tile = [] { const char* e = getenv("I2PC_GEMM_SPLIT_TILE"); return e ? atoi(e) : 0; }();
+static thread_local int g_tile192 = [] { const char* e = getenv("I2PC_GEMM_TILE192"); return e ? atoi(e) : 1; }();
+static thread_local int g_split_tile = [] { const char* e = getenv("I2PC_GEMM_SPLIT_TILE"); return e ? atoi(e) : 0; }();
 
 static int64_t max_row(const Args& p) {
   const int64_t m = p.M - 1;

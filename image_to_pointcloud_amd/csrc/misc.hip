@@ -235,7 +235,7 @@ static int grid_for(int64_t work, int per_block = 256) {
 using namespace i2pc;
 using namespace i2pc::misc;
 
-static int g_ln2 = 1;   // "ln_f2": the float2 row kernel for dim 384
+static thread_local int g_ln2 = 1;   // "ln_f2": the float2 row kernel for dim 384
 
 bool i2pc_misc_tune(const char* name, int value) {
   if (std::strcmp(name, "ln_f2") == 0) { g_ln2 = value; return true; }

@@ -93,6 +93,14 @@ struct alignas(16) SelState {
   uint32_t pad3[2];
   double rden64;           // RN(1 / den64): quotient seed for div_rn
   double pad4;
+  // window-only selection (k_sweep_w / k_resolve_w): per level-0 window w the finite keys below it,
+  // and for its end bins when k_window flagged them as spikes (wspike bit 0: first bin, bit 1:
+  // last bin; such a bin is counted with its min / max key instead of compacted)
+  uint32_t wspike[3];
+  uint32_t wbelow[3];
+  uint32_t wcntF[3], wminF[3], wmaxF[3];
+  uint32_t wcntL[3], wminL[3], wmaxL[3];
+  uint32_t pad5[3];
 };
 
 // Correctly rounded a / b from r = RN(1 / b) (Markstein's correction: q0 = RN(a r),
@@ -332,6 +340,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
     s.rlo = 0xffffffffu;
     s.rhi = 0u;
     for (int i = 0; i < 6; i += 2) { s.bbox_key[i] = 0xffffffffu; s.bbox_key[i + 1] = 0u; }
+    for (int w = 0; w < 3; ++w) { s.wminF[w] = s.wminL[w] = 0xffffffffu; }
     s.med = __uint_as_float(0x7fc00000u);
     st[gtid] = s;
   }
@@ -729,6 +738,208 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
   }
 }
 
+// Window-only selection sweep (the batch path's only full-resolution pass before the
+// unprojection): no histogram at all.  Per k_window window w (level-0 bins [wlo, whi]) it counts
+// the finite keys below the window (one wave-reduced atomic per workgroup), compacts the keys
+// inside it into w's candidate list, and -- for an end bin k_window flagged as a spike -- counts
+// that bin's keys with their min / max key instead of compacting them.  Plus the level-0
+// counters (non-finite counts, finite key range).  k_resolve_w turns this into exact keys; a
+// target outside every window (or in an unresolvable part) falls to k_sel_slow.
+template <bool SAME>
+__global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_t* cand, uint32_t cap, int B,
+                                                    Sweep sw) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
+  uint32_t* sh = smem_u;                                                  // [3][kSlotWords] staged keys
+  float* hrow = reinterpret_cast<float*>(smem_u + 3 * kSlotWords);        // [rows][kTileW]
+  __shared__ uint32_t red[kBlock / 64][24];
+  __shared__ uint32_t lcnt[3], gbase[3];
+  int b, chunk;
+  map_block(blockIdx.x, B, sw.nrb * sw.ntiles, b, chunk);
+  const int rb = chunk / sw.ntiles, c0 = (chunk - rb * sw.ntiles) * kTileW;
+  const int cw = min(kTileW, g.W - c0);
+  SelState* S = st + b;
+  if (S->phase != PH_INIT) return;
+  const VBins vb0 = level0_vbins(S->rlo, S->rhi);
+  const int nwin = (int)S->nwin;
+  int wlo[3] = {kBins, kBins, kBins}, whi[3] = {-1, -1, -1};
+  uint32_t spk[3] = {0, 0, 0};
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+    if (w < nwin) { wlo[w] = (int)S->wbin[2 * w]; whi[w] = (int)S->wbin[2 * w + 1]; spk[w] = S->wspike[w]; }
+  const bool any_spike = (spk[0] | spk[1] | spk[2]) != 0;
+  const int v0 = sw.row0 + rb * sw.R;
+  const int v1 = min(sw.row_end, v0 + sw.R);
+  if (threadIdx.x < 3) lcnt[threadIdx.x] = 0;
+  int lo = 0;
+  if (!SAME) {
+    lo = g.yt[v0].i0;
+    const int nr = g.yt[v1 - 1].i1 - lo + 1;
+    const float* D = g.depth + ((size_t)b * g.dh + lo) * g.dw;
+    float* raw = hrow + (size_t)sw.lds_rows * kTileW;
+    Tap tx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tx[j] = g.xt[c0 + min(j * kBlock + (int)threadIdx.x, cw - 1)];
+    if (sw.raw) {
+      stage_floats(raw, D, nr * g.dw);
+      __syncthreads();
+    }
+    const float* src = sw.raw ? raw : D;
+    for (int k = 0; k < nr; ++k) {
+      const float* r = src + (size_t)k * g.dw;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = j * kBlock + (int)threadIdx.x;
+        if (u < cw) hrow[k * kTileW + u] = r[tx[j].i0] * tx[j].w0 + r[tx[j].i1 < 0 ? tx[j].i0 : tx[j].i1] * tx[j].w1;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float* Dimg = g.depth + (size_t)b * g.dh * g.dw;
+  uint32_t nf = 0, nnan = 0, nneg = 0, npos = 0, kmin = 0xffffffffu, kmax = 0u;
+  uint32_t below[3] = {0, 0, 0};
+  uint32_t cF[3] = {0, 0, 0}, mnF[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mxF[3] = {0, 0, 0};
+  uint32_t cL[3] = {0, 0, 0}, mnL[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mxL[3] = {0, 0, 0};
+  Tap ty_next = SAME ? Tap{0, 0, 1.f, 0.f} : g.yt[v0];
+  for (int v = v0; v < v1; ++v) {
+    float ha[4], hc[4];
+    const Tap ty = ty_next;
+    if (!SAME) ty_next = g.yt[min(v + 1, v1 - 1)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int uc = min(j * kBlock + (int)threadIdx.x, cw - 1);
+      if (SAME) {
+        ha[j] = Dimg[(size_t)v * g.dw + c0 + uc];
+      } else {
+        ha[j] = hrow[(ty.i0 - lo) * kTileW + uc];
+        hc[j] = hrow[(ty.i1 - lo) * kTileW + uc];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool active = j * kBlock + (int)threadIdx.x < cw;
+      const float val = SAME ? ha[j] : ha[j] * ty.w0 + hc[j] * ty.w1;
+      const uint32_t key = f2key(val);
+      const bool fin = active && !key_nonfinite(key);
+      if (active && !fin) {
+        ++nf;
+        nnan += (key != kKeyPosInf && key != kKeyNegInf) ? 1u : 0u;
+        nneg += key == kKeyNegInf ? 1u : 0u;
+        npos += key == kKeyPosInf ? 1u : 0u;
+      }
+      kmin = min(kmin, fin ? key : 0xffffffffu);
+      kmax = max(kmax, fin ? key : 0u);
+      const int hb = fin ? (int)vbin(val, vb0) : kBins;      // non-finite: in no window, below none
+      int cq = -1;
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        below[w] += hb < wlo[w] ? 1u : 0u;
+        cq = (hb >= wlo[w] && hb <= whi[w]) ? w : cq;
+      }
+      if (any_spike && cq >= 0) {
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+          const bool inF = cq == w && (spk[w] & 1u) && hb == wlo[w];
+          const bool inL = cq == w && (spk[w] & 2u) && hb == whi[w] && !inF;
+          cF[w] += inF ? 1u : 0u;
+          mnF[w] = inF ? min(mnF[w], key) : mnF[w];
+          mxF[w] = inF ? max(mxF[w], key) : mxF[w];
+          cL[w] += inL ? 1u : 0u;
+          mnL[w] = inL ? min(mnL[w], key) : mnL[w];
+          mxL[w] = inL ? max(mxL[w], key) : mxL[w];
+          cq = (inF || inL) ? -1 : cq;
+        }
+      }
+      if (__ballot(cq >= 0)) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const uint64_t m = __ballot(cq == q);
+          if (!m) continue;
+          const int leader = __ffsll((unsigned long long)m) - 1;
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(&lcnt[q], (uint32_t)__popcll(m));
+          base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+          if (cq == q) {
+            const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (pos < (uint32_t)kSlotWords) {
+              sh[q * kSlotWords + pos] = key;
+            } else {
+              const uint32_t gpos = atomicAdd(&S->ccount[q], 1u);
+              if (gpos < cap) cand[((size_t)b * kSlots + q) * cap + gpos] = key;
+            }
+          }
+        }
+      }
+    }
+  }
+  // workgroup totals: one atomic per counter and workgroup
+  nf = wave_sum_u32(nf);
+  kmin = wave_min_u32(kmin);
+  kmax = wave_max_u32(kmax);
+  if (lane == 0) { red[wid][0] = nf; red[wid][1] = kmin; red[wid][2] = kmax; }
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    if (w < nwin) {
+      const uint32_t bw = wave_sum_u32(below[w]);
+      if (lane == 0) red[wid][3 + w] = bw;
+    }
+  }
+  if (any_spike) {
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const uint32_t a = wave_sum_u32(cF[w]), c = wave_min_u32(mnF[w]), d = wave_max_u32(mxF[w]);
+      const uint32_t e = wave_sum_u32(cL[w]), f = wave_min_u32(mnL[w]), h = wave_max_u32(mxL[w]);
+      if (lane == 0) {
+        red[wid][6 + 6 * w] = a; red[wid][7 + 6 * w] = c; red[wid][8 + 6 * w] = d;
+        red[wid][9 + 6 * w] = e; red[wid][10 + 6 * w] = f; red[wid][11 + 6 * w] = h;
+      }
+    }
+  }
+  if (__builtin_amdgcn_readfirstlane(nf)) {       // rare: split the non-finite count
+    nnan = wave_sum_u32(nnan);
+    nneg = wave_sum_u32(nneg);
+    npos = wave_sum_u32(npos);
+    if (lane == 0) {
+      if (nnan) atomicAdd(&S->nan_count, nnan);
+      if (nneg) atomicAdd(&S->ninf_neg, nneg);
+      if (npos) atomicAdd(&S->ninf_pos, npos);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0, mn = 0xffffffffu, mx = 0;
+    for (int w = 0; w < kBlock / 64; ++w) { c += red[w][0]; mn = min(mn, red[w][1]); mx = max(mx, red[w][2]); }
+    if (c) atomicAdd(&S->nonfinite_count, c);
+    if (mn != 0xffffffffu) atomicMin(&S->kmin, mn);
+    if (mx) atomicMax(&S->kmax, mx);
+    for (int q = 0; q < nwin; ++q) {
+      uint32_t bw = 0;
+      for (int w = 0; w < kBlock / 64; ++w) bw += red[w][3 + q];
+      if (bw) atomicAdd(&S->wbelow[q], bw);
+      const uint32_t nq = min(lcnt[q], (uint32_t)kSlotWords);
+      gbase[q] = nq ? atomicAdd(&S->ccount[q], nq) : 0u;
+      if (spk[q]) {
+        uint32_t a = 0, cmn = 0xffffffffu, dmx = 0, e = 0, fmn = 0xffffffffu, hmx = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+          a += red[w][6 + 6 * q]; cmn = min(cmn, red[w][7 + 6 * q]); dmx = max(dmx, red[w][8 + 6 * q]);
+          e += red[w][9 + 6 * q]; fmn = min(fmn, red[w][10 + 6 * q]); hmx = max(hmx, red[w][11 + 6 * q]);
+        }
+        if (a) { atomicAdd(&S->wcntF[q], a); atomicMin(&S->wminF[q], cmn); atomicMax(&S->wmaxF[q], dmx); }
+        if (e) { atomicAdd(&S->wcntL[q], e); atomicMin(&S->wminL[q], fmn); atomicMax(&S->wmaxL[q], hmx); }
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = 0; q < nwin; ++q) {
+    const uint32_t nq = min(lcnt[q], (uint32_t)kSlotWords);
+    const uint32_t* src = sh + q * kSlotWords;
+    uint32_t* dst = cand + ((size_t)b * kSlots + q) * cap;
+    for (uint32_t i = threadIdx.x; i < nq; i += kBlock)
+      if (gbase[q] + i < cap) dst[gbase[q] + i] = src[i];
+  }
+}
+
 // For one histogram of `nb` bins, the bins holding the 0-based ranks[0..nt) and the ranks
 // inside them (all NT threads call; results in out_bin / out_rem after the closing barrier).
 // Each thread owns nb / NT consecutive bins; the segment sums are scanned per wave with
@@ -958,13 +1169,14 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist,
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    // ascending windows; overlapping / touching neighbours merge
+    // ascending windows; overlapping neighbours merge (touching ones stay apart, so a spike
+    // bin stays at a window's end)
     uint32_t w[6];
     int nw = 0;
     for (int k = 0; k < nq; ++k) {
       const uint32_t lo = wb[2 * k], hi = wb[2 * k + 1];
       if (lo > hi) continue;
-      if (nw > 0 && lo <= w[2 * nw - 1] + 1) {
+      if (nw > 0 && lo <= w[2 * nw - 1]) {
         w[2 * nw - 1] = max(w[2 * nw - 1], hi);
       } else {
         w[2 * nw] = lo;
@@ -973,6 +1185,17 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist,
       }
     }
     for (int i = 0; i < 2 * nw; ++i) S->wbin[i] = w[i];
+    // end bins expected to outgrow the window budget (the zero floor of a ReLU head, a saturated
+    // maximum): counted with their min / max key by k_sweep_w instead of compacted; a window
+    // holds such a bin only at an end (a bin larger than the window cannot have neighbours on
+    // both sides within the rank budget)
+    for (int k = 0; k < nw; ++k) {
+      const uint32_t lo = w[2 * k], hi = w[2 * k + 1];
+      uint32_t f = 0;
+      if ((double)mh[lo] * scale > (double)kWinKeys) f |= 1u;
+      if (hi > lo && (double)mh[hi] * scale > (double)kWinKeys) f |= 2u;
+      S->wspike[k] = f;
+    }
     S->nwin = (uint32_t)nw;
   }
 }
@@ -1229,6 +1452,117 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
   }
 }
 
+// Window-only resolve (after k_sweep_w): workgroup = (image b, window w).  Every workgroup of an
+// image derives the same targets (the four percentile ranks, or with NaN / Inf the ten fill
+// targets -- fill_targets); the workgroup of window w resolves the targets whose rank among the
+// finite keys falls inside w:
+//   rank r' = rank - (finite keys below w), the window's keys ordered [first bin | compacted | last bin]
+//   (bins are key intervals, ascending): a spike end bin resolves when it holds one key (min ==
+//   max), the compacted part by exact selection among its candidates (cand_select).
+// Anything else (a rank outside every window, a multi-key spike, an overflowed candidate list)
+// sets the image's err flag: k_sel_slow then selects it from scratch.  Window 0's workgroup
+// also stores the target bookkeeping k_sel_slow's finish needs.
+__global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32_t* cand, uint32_t cap, int B) {
+  __shared__ uint32_t lh[kBins];
+  __shared__ uint32_t ck[kLdsCand];
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t rbin[kMaxTgt], rrem[kMaxTgt], qr[kMaxTgt], qk[kMaxTgt], tl[kMaxTgt], tz[kMaxTgt], tr[kMaxTgt];
+  __shared__ int tq[kMaxTgt], nc;
+  __shared__ uint32_t clo, chi, fail;
+  __shared__ SelState s;
+  const int b = blockIdx.x / 3, w = blockIdx.x % 3;
+  if (b >= B) return;
+  if (threadIdx.x == 0) s = st[b];
+  __syncthreads();
+  if (s.phase != PH_INIT) return;
+  if (w > 0 && w >= (int)s.nwin) return;
+  SelState* S = st + b;
+  if (threadIdx.x == 0) {
+    fail = 0;
+    nc = 0;
+    bool done = false;
+    if (s.nonfinite_count == 0) {
+      pct_ranks(s.n, s.rank);
+      s.ntgt = 4;
+      for (int t = 0; t < 4; ++t) { s.tlo[t] = 0; s.thi[t] = 0xffffffffu; }
+    } else if (s.nan_count == s.n) {   // all-NaN: nanmedian is NaN, every value stays NaN
+      if (w == 0) {
+        S->has_med = 1;
+        S->mode = 2;
+        S->p2 = S->p98 = (double)__uint_as_float(0x7fc00000u);
+        S->phase = PH_DONE;
+      }
+      done = true;
+    } else {
+      fill_targets(s);      // (+-inf sentinel targets come back resolved: tlo == thi)
+    }
+    if (!done) {
+      const uint32_t nwin = s.nwin;
+      if (w == 0) {         // bookkeeping for k_sel_slow's finish
+        S->ntgt = s.ntgt;
+        S->fill = s.fill;
+        S->med_ranks = s.med_ranks;
+        for (int t = 0; t < (int)s.ntgt; ++t) {
+          S->rank[t] = s.rank[t];
+          if (s.tlo[t] == s.thi[t]) { S->tlo[t] = s.tlo[t]; S->thi[t] = s.thi[t]; }
+        }
+      }
+      const uint32_t cF = (s.wspike[w] & 1u) ? s.wcntF[w] : 0u, cL = (s.wspike[w] & 2u) ? s.wcntL[w] : 0u;
+      const uint32_t cC = s.ccount[w];
+      const uint64_t bw = s.wbelow[w];
+      for (int t = 0; t < (int)s.ntgt; ++t) {
+        if (s.tlo[t] == s.thi[t]) continue;
+        const uint64_t r = s.rank[t];
+        int in = -1;
+        for (uint32_t k = 0; k < nwin; ++k) {
+          const uint64_t lo = s.wbelow[k];
+          const uint64_t cnt = (uint64_t)((s.wspike[k] & 1u) ? s.wcntF[k] : 0u) + s.ccount[k] +
+                               ((s.wspike[k] & 2u) ? s.wcntL[k] : 0u);
+          if (r >= lo && r < lo + cnt) in = (int)k;
+        }
+        if (in < 0) { if (w == 0) fail = 1; continue; }
+        if (in != w) continue;
+        const uint64_t rp = r - bw;
+        if (rp < cF) {
+          if (s.wminF[w] == s.wmaxF[w]) { S->tlo[t] = S->thi[t] = s.wminF[w]; } else fail = 1;
+        } else if (rp < (uint64_t)cF + cC) {
+          if (cC > cap) { fail = 1; continue; }
+          qr[nc] = (uint32_t)(rp - cF);
+          tq[nc++] = t;
+        } else {
+          if (s.wminL[w] == s.wmaxL[w]) { S->tlo[t] = S->thi[t] = s.wminL[w]; } else fail = 1;
+        }
+      }
+      if (nc > 0) {          // key interval of the compacted bins
+        const VBins vb = level0_vbins(s.rlo, s.rhi);
+        const uint32_t b0 = s.wbin[2 * w] + ((s.wspike[w] & 1u) ? 1u : 0u);
+        const uint32_t b1 = s.wbin[2 * w + 1] - ((s.wspike[w] & 2u) ? 1u : 0u);
+        uint32_t a, z;
+        vbin_interval(b0, vb, s.kmin, s.kmax, clo, z);
+        vbin_interval(b1, vb, s.kmin, s.kmax, a, chi);
+        if (chi < clo) chi = clo;
+      }
+    } else {
+      nc = 0;
+    }
+  }
+  __syncthreads();
+  if (fail) atomicOr(&S->err, 1u);     // (every thread: the same word, same value)
+  if (nc == 0 || fail) return;
+  const uint32_t c = s.ccount[w];
+  const uint32_t* keys = cand + ((size_t)b * kSlots + w) * cap;
+  if (c <= (uint32_t)kLdsCand) {
+    dma_words(ck, keys, c);
+    keys = ck;
+  }
+  __syncthreads();
+  cand_select(keys, c, clo, chi, qr, nc, qk, lh, wsum, rbin, rrem, tl, tz, tr);
+  if (threadIdx.x < nc) {
+    const int t = tq[threadIdx.x];
+    S->tlo[t] = S->thi[t] = qk[threadIdx.x];
+  }
+}
+
 // Non-finite maps (app.py:194-196: NaN / +-Inf filled with np.nanmedian, then the
 // percentiles of the filled map) and any image the fast levels did not finish: the whole
 // selection of one image in one workgroup, 3-level radix select on the key bits (11 + 11 +
@@ -1309,7 +1643,18 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
   if (b >= B) return;
   if (threadIdx.x == 0) s = st[b];
   __syncthreads();
-  if (s.phase != PH_SLOW) return;
+  if (s.phase == PH_INIT) {
+    // window path (k_sweep_w / k_resolve_w): every target resolved unless err
+    if (s.err == 0) {
+      if (threadIdx.x == 0) {
+        finish_targets(s);
+        st[b] = s;
+      }
+      return;
+    }
+  } else if (s.phase != PH_SLOW) {
+    return;
+  }
   const int n = g.H * g.W;
   uint32_t nan_c = 0, nf_c = 0;
   for (int p = threadIdx.x; p < n; p += kSlowBlock) {
@@ -2158,9 +2503,9 @@ static size_t sweep_lds(const Sweep& sw, int dw) { return sw.lds_rows ? (size_t)
 
 // k_unproject_rows knobs (I2PC_UNP_ROWS / _NT / _RPT, or i2pc_set_tuning "unp_rows" / "unp_nt" / "unp_rpt")
 static int env_int(const char* name, int dflt) { const char* e = getenv(name); return e ? atoi(e) : dflt; }
-static int g_unp_rows = env_int("I2PC_UNP_ROWS", 1);
-static int g_unp_nt = env_int("I2PC_UNP_NT", 1);
-static int g_unp_rpt = env_int("I2PC_UNP_RPT", kRowsPT);
+static thread_local int g_unp_rows = env_int("I2PC_UNP_ROWS", 1);
+static thread_local int g_unp_nt = env_int("I2PC_UNP_NT", 1);
+static thread_local int g_unp_rpt = env_int("I2PC_UNP_RPT", kRowsPT);
 
 // k_unproject_rows geometry: column tiles of 4 * tpr points (tpr a multiple of 64, <= kBlock),
 // 8192 points per workgroup where the rows allow, LDS = staged model rows + one 16-B slot per
@@ -2266,6 +2611,10 @@ static int select_level(const Geo& g, SelState* st, uint32_t* hist, uint32_t* ca
   return I2PC_OK;
 }
 
+// "sel_windows" (I2PC_SEL_WIN): 1 = the window-only batch selection (k_sweep_w / k_resolve_w),
+// 0 = the histogram levels (the band path's); both exact.
+static thread_local int g_sel_windows = [] { const char* e = getenv("I2PC_SEL_WIN"); return e ? atoi(e) : 1; }();
+
 static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, const uint32_t* rpart,
                          uint32_t cap, int B, const Sweep& sw, hipStream_t s, const Exchange* x = nullptr) {
   // full-resolution sample of ~64 K points per image for the level-0 estimate
@@ -2273,6 +2622,20 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
   const int ns = ((g.H + stride - 1) / stride) * ((g.W + stride - 1) / stride);
   hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g, B, st, hist, rpart, stride);
   hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, hist, cap, B, x ? 0 : 1, ns);
+  if (!x && g_sel_windows) {
+    // batch path: one window-only sweep + resolve; k_sel_slow finishes (or, for the rare image
+    // a window missed, selects from scratch)
+    const size_t lds = sizeof(uint32_t) * 3 * kSlotWords +
+                       (size_t)sw.lds_rows * (kTileW + (sw.raw ? g.dw : 0)) * sizeof(float);
+    const dim3 grid(B * sw.nrb * sw.ntiles), block(kBlock);
+    if (g.same)
+      hipLaunchKernelGGL((k_sweep_w<true>), grid, block, lds, s, g, st, cand, cap, B, sw);
+    else
+      hipLaunchKernelGGL((k_sweep_w<false>), grid, block, lds, s, g, st, cand, cap, B, sw);
+    hipLaunchKernelGGL(k_resolve_w, dim3(B * 3), dim3(kBlock), 0, s, st, cand, cap, B);
+    hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
+    return check_launch("select");
+  }
   int rc;
   if ((rc = select_level<0>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   if ((rc = select_level<1>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
@@ -2518,5 +2881,6 @@ bool i2pc_unproject_tune(const char* name, int value) {
   if (std::strcmp(name, "unp_rows") == 0) { i2pc::unproj::g_unp_rows = value; return true; }
   if (std::strcmp(name, "unp_nt") == 0) { i2pc::unproj::g_unp_nt = value; return true; }
   if (std::strcmp(name, "unp_rpt") == 0) { i2pc::unproj::g_unp_rpt = value; return true; }
+  if (std::strcmp(name, "sel_windows") == 0) { i2pc::unproj::g_sel_windows = value; return true; }
   return false;
 }

@@ -54,15 +54,21 @@ class OverlappedGather:
     PointBatch.  step() computes into slot k % 2 on the current stream, then launches the two
     RCCL all-gathers of that slot asynchronously (torch.distributed async_op: the collective
     waits for the compute on its own stream, the current stream goes on with step k + 1).
-    Before a slot is overwritten, the current stream waits for the gather that read it."""
+    Before a slot is overwritten, the current stream waits for the gather that read it.
+
+    With a gloo process group and device buffers (ranks sharing one GPU, the 1-GPU rehearsal
+    of the multi-rank path) the gather is staged through host memory and runs synchronously:
+    gloo moves host tensors; the results are the same bytes."""
 
     def __init__(self, runs, world: int, batch: int, points: int, device, group=None):
         import torch
+        import torch.distributed as dist
         if len(runs) != 2:
             raise ValueError("OverlappedGather needs two step callables (double-buffered point sets)")
         self.runs, self.group = runs, group
         self.gx = [torch.empty((world * batch, points, 3), dtype=torch.float32, device=device) for _ in range(2)]
         self.gr = [torch.empty((world * batch, points, 3), dtype=torch.uint8, device=device) for _ in range(2)]
+        self.host_staged = self.gx[0].is_cuda and dist.get_backend(group) == "gloo"
         self.works = [None, None]
         self.k = 0
 
@@ -71,8 +77,15 @@ class OverlappedGather:
         slot = self.k & 1
         self._wait(slot)                      # the gather that read this slot's buffers is done
         out = self.runs[slot]()
-        self.works[slot] = (dist.all_gather_into_tensor(self.gx[slot], out.xyz, group=self.group, async_op=True),
-                            dist.all_gather_into_tensor(self.gr[slot], out.rgb, group=self.group, async_op=True))
+        if self.host_staged:
+            for dst, src in ((self.gx[slot], out.xyz), (self.gr[slot], out.rgb)):
+                host = dst.new_empty(dst.shape, device="cpu")
+                dist.all_gather_into_tensor(host, src.cpu(), group=self.group)
+                dst.copy_(host)
+        else:
+            self.works[slot] = (
+                dist.all_gather_into_tensor(self.gx[slot], out.xyz, group=self.group, async_op=True),
+                dist.all_gather_into_tensor(self.gr[slot], out.rgb, group=self.group, async_op=True))
         self.k += 1
         return slot
 
@@ -89,6 +102,9 @@ class OverlappedGather:
         self._wait(1)
 
     def gathered(self, slot):
+        """The gathered (xyz, rgb) of the last step that wrote `slot`, [world*B, N, 3] image-major;
+        the current stream first waits for that slot's gather."""
+        self._wait(slot)
         return self.gx[slot], self.gr[slot]
 
 
@@ -98,6 +114,8 @@ def max_over_ranks(seconds: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return seconds
+    if dist.get_backend() == "gloo":
+        device = None                           # gloo reduces host tensors
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -151,7 +169,9 @@ class RcclComm:
             nranks, rank = dist.get_world_size(group), dist.get_rank(group)
             if unique_id is None:
                 obj = [self.unique_id() if rank == 0 else None]
-                dist.broadcast_object_list(obj, src=0, group=group)
+                # src is a GLOBAL rank: the group's rank 0 (not global rank 0 for a subgroup)
+                src = dist.get_global_rank(group, 0) if group is not None else 0
+                dist.broadcast_object_list(obj, src=src, group=group)
                 unique_id = obj[0]
         elif unique_id is None:
             if nranks != 1:
@@ -171,8 +191,15 @@ class RcclComm:
         return buf.raw
 
     def close(self):
+        """Destroy the communicator (explicitly, or by leaving a `with` block: never from a
+        finaliser, which may run after HIP has shut down)."""
         if getattr(self, "handle", None) is not None and self.handle.value:
             self._lib.i2pc_comm_destroy(self.handle)
             self.handle = None
 
-    __del__ = close
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

@@ -298,6 +298,14 @@ def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: i
     dev = depth.device
     if out is not None:
         xyz, rgb, bbox, stats = out
+        # the kernels write nb points: a buffer sized for another band or density would overrun
+        for name, t, dt, need in (("xyz", xyz, torch.float32, nb * 3), ("rgb", rgb, torch.uint8, nb * 3),
+                                  ("bbox", bbox, torch.float64, 6), ("stats", stats, torch.float64, 4)):
+            if (t.dtype != dt or t.device != dev or not t.is_contiguous() or t.numel() < need
+                    or (name in ("xyz", "rgb") and (t.dim() != 2 or t.shape[1] != 3))):
+                raise ValueError(f"out {name}: need a contiguous {dt} tensor on {dev} with >= {need} elements"
+                                 + (" shaped [>= nb, 3]" if name in ("xyz", "rgb") else "")
+                                 + f", got {t.dtype} {tuple(t.shape)} on {t.device}")
     else:
         xyz = torch.empty((nb, 3), dtype=torch.float32, device=dev)
         rgb = torch.empty((nb, 3), dtype=torch.uint8, device=dev)

@@ -120,8 +120,9 @@ def gemm_kernel_label(desc: GemmDesc) -> str:
 
 
 def set_tuning(name: str, value: int) -> None:
-    """Kernel-selection knob (i2pc_set_tuning): gemm_tail, gemm_bn128, gemm_splitk, unp_rows, unp_nt,
-    unp_rpt, attn_lazy, attn_scalar."""
+    """Kernel-selection knob (i2pc_set_tuning) for calls made from THIS host thread (thread-local
+    in libi2pc.so): gemm_tail, gemm_bn128, gemm_splitk, unp_rows, unp_nt, unp_rpt, sel_windows,
+    attn_lazy, attn_scalar, ln_f2."""
     _lib.call("i2pc_set_tuning", name.encode(), int(value))
 
 

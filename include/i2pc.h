@@ -19,7 +19,8 @@
  *     can be captured into a hipGraph;
  *   - return 0 on success, a negative I2PC_E* code otherwise; the message of
  *     the last error on the calling thread is in i2pc_last_error();
- *   - re-entrant; one call may run per stream concurrently.
+ *   - re-entrant; one call may run per stream concurrently (kernel-selection knobs are
+ *     per host thread, see i2pc_set_tuning).
  * No torch, no C++ types cross this boundary.
  */
 #ifndef I2PC_H_
@@ -282,17 +283,23 @@ int i2pc_maxpool3s2(const void* x, int batch, int h, int w, int c, int out_h, in
  * no device work).  Returns "invalid" for a descriptor i2pc_gemm would reject. */
 const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* desc);
 
-/* GEMM engine selection (process-wide): 0 = automatic (the persistent 256-column
- * engine for calls with >= 3 tiles per CU whose epilogue it implements, else the
- * tile kernel), 1 = tile kernel only, 2 = persistent engine wherever its epilogue
- * applies, 3 = automatic with the ping-pong persistent engine (k_gemm_8p: dense A,
- * plain / fp32-residual epilogues, K >= 128) where the persistent engine would run,
- * 4 = ping-pong engine wherever it applies (else as 2).  All produce bit-identical
- * results; tests use this to cross-check them. */
+/* GEMM engine selection for calls made from the CALLING THREAD (thread-local: a setting on one
+ * host thread never changes the kernels another thread's calls launch): 0 = automatic (the
+ * persistent 256-column engine for calls with >= 3 tiles per CU whose epilogue it implements,
+ * else the tile kernel), 1 = tile kernel only, 2 = persistent engine wherever its epilogue
+ * applies, 3 = automatic with the ping-pong persistent engine (k_gemm_8p: dense A, plain /
+ * fp32-residual epilogues, K >= 128) where the persistent engine would run, 4 = ping-pong engine
+ * wherever it applies.  All modes give bit-identical results for the same split-K choice;
+ * split-K (i2pc_gemm_ws with a workspace, knob "gemm_splitk") runs in modes 0 and 3 only and adds
+ * the fp32 partial sums in another order, so a few-tile K >= 4096 call may differ in the last
+ * bits between modes 0/3 and 1/2/4, and between i2pc_gemm (never splits) and i2pc_gemm_ws. */
 int i2pc_gemm_set_engine(int mode);
 
-/* Process-wide kernel-selection knobs for A/B measurement (not part of the drop-in surface;
- * every setting but gemm_splitk computes the same results bit for bit):
+/* Kernel-selection knobs for A/B measurement (not part of the drop-in surface).  Like the engine
+ * mode they are THREAD-LOCAL: each host thread starts from the defaults below and a change
+ * affects only the calls that thread makes, so concurrent callers on other threads / streams keep
+ * their kernels (the re-entrancy promise above).  Every setting but gemm_splitk computes the same
+ * results bit for bit:
  *   "gemm_tail"   1 = split the last round of a persistent GEMM into 256 x 128 tiles where that
  *                 saves a round
  *   "gemm_bn128"  1 = the persistent engine with 256 x 128 tiles for N % 256 != 0, N % 128 == 0
@@ -302,11 +309,13 @@ int i2pc_gemm_set_engine(int mode);
  *   "unp_rows"    1 = the row-sweep unprojection kernel
  *   "unp_nt"      1 = non-temporal point stores
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
+ *   "sel_windows" 1 = the window-only p2 / p98 selection of i2pc_unproject (one sweep), 0 = the
+ *                 histogram levels (the band path's)
  *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _UNP_ROWS / _UNP_NT / _UNP_RPT /
- * _ATTN_LAZY / _ATTN_SCALAR environment variables, else 1, 1, 1, 1, 1, 8, 1, 1.  A HIP graph keeps the kernels
- * it captured: re-capture after changing a knob. */
+ * _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR environment variables, else 1, 1, 1, 1, 1, 8, 1, 1, 1.  A
+ * HIP graph keeps the kernels it captured: re-capture after changing a knob. */
 int i2pc_set_tuning(const char* name, int value);
 
 /* LayerNorm over the last dim: x fp32 [rows][dim] (row stride ldx) -> y bf16 [rows][dim]

@@ -39,3 +39,38 @@ def test_missing_device_fails_loudly():
     import numpy as np
     with pytest.raises(_lib.I2PCError):
         geometry.depth_to_point_cloud(np.zeros((4, 4, 3), np.uint8), np.zeros((4, 4), np.float32))
+
+
+def test_kernel_selection_knobs_are_per_thread():
+    """i2pc_gemm_set_engine / i2pc_set_tuning change the kernels of the CALLING thread only
+    (include/i2pc.h: re-entrant across threads), checked through i2pc_gemm_kernel_name (no
+    device work)."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libi2pc.so not built")
+    import threading
+    from image_to_pointcloud_amd import ops
+    d = ops.GemmDesc()
+    d.m, d.n, d.k, d.lda, d.ldw, d.ldc = 18464, 3072, 1024, 1024, 1024, 3072
+    d.a = d.w = d.c = 16
+    default = ops.gemm_kernel_label(d)
+    seen = {}
+    ready, done = threading.Event(), threading.Event()
+
+    def other():
+        ready.wait(10)
+        seen["other"] = ops.gemm_kernel_label(d)      # while the main thread has engine 1 set
+        done.set()
+
+    t = threading.Thread(target=other)
+    t.start()
+    try:
+        ops.set_gemm_engine(1)                          # tile kernel only, this thread
+        seen["mine"] = ops.gemm_kernel_label(d)
+        ready.set()
+        done.wait(10)
+    finally:
+        ops.set_gemm_engine(0)
+        t.join(10)
+    assert seen["other"] == default
+    assert seen["mine"] != default and seen["mine"].startswith("k_gemm<")
+    assert ops.gemm_kernel_label(d) == default

@@ -134,8 +134,7 @@ def _overlap_worker(rank, ws, port, q):
         seen = []
         for k in range(5):
             slot = og.step()
-            if k >= 1:                              # step k-1's gather (other slot) may be read now
-                og._wait(slot ^ 1)
+            if k >= 1:                              # step k-1's gather (other slot); gathered() waits for it
                 gx, gr = og.gathered(slot ^ 1)
                 seen.append((k - 1, gx[:, 0, 0].tolist(), gr[:, 0, 0].tolist()))
         og.finish()

@@ -1,0 +1,102 @@
+"""The multi-rank device path on ONE GPU (C3 layout rehearsal): two ranks share the card over a
+gloo process group, each runs its graph-captured pipelines on its own images, and the
+OverlappedGather all-gathers every rank's point buffers (per-image independence,
+backend/app.py:197-223).  The 8-GPU RCCL run is the driver's; this checks the same code path
+end to end on the device, and that `bench.py --gpus N` really starts N ranks."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        import bench
+        from image_to_pointcloud_amd import distributed as D, geometry
+        from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL
+        from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        B, S = 2, 256
+        pipe = PointCloudPipeline(B, S, S, spec=DA_V2_SMALL, density="medium", device=dev, seed=0)
+        pipe2 = PointCloudPipeline(B, S, S, spec=DA_V2_SMALL, density="medium", device=dev, model=pipe.model)
+        images = bench._images(B, S, rank, dev)
+        pipe.capture(images)
+        pipe2.capture(images)
+        og = D.OverlappedGather([pipe.replay, pipe2.replay], ws, B, pipe.points_per_image, dev)
+        for _ in range(3):
+            slot = og.step()
+        og.finish()
+        gx, gr = og.gathered(slot)
+        # this rank's own images, unprojected by a separate eager call on the same depth
+        pipe.infer_depth(images)
+        mine = geometry.unproject_batch(pipe.depth, images, density="medium")
+        torch.cuda.synchronize()
+        q.put((rank, gx.cpu().numpy(), gr.cpu().numpy(), mine.xyz.cpu().numpy(), mine.rgb.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_gather_two_ranks_on_device_bit_identical():
+    import torch.multiprocessing as mp
+    ws, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted((q.get(timeout=240) for _ in range(ws)), key=lambda t: t[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0
+    B = out[0][3].shape[0]
+    for rank, gx, gr, _, _ in out:
+        assert gx.shape[0] == ws * B
+        for src, _, _, mx, mr in out:         # rank src's images sit at [src*B, (src+1)*B)
+            assert gx[src * B:(src + 1) * B].tobytes() == mx.tobytes(), (rank, src)
+            assert gr[src * B:(src + 1) * B].tobytes() == mr.tobytes(), (rank, src)
+    assert out[0][3].tobytes() != out[1][3].tobytes()     # the ranks really had different images
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """`python bench.py --gpus 2` (no launcher env) starts torch.distributed.run with two ranks as a
+    child process and prints rank 0's line with n_gpus 2 and the all-gather in the workload."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--batch", "2",
+           "--size", "512", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-kernel-profile"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 4
+    assert "all-gather" in rec["config"]["workload"]
+    assert rec["value"] > 0
+    # a launcher world that disagrees with --gpus is an error, not a silent 1-GPU number
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

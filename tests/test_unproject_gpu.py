@@ -422,3 +422,59 @@ def test_row_kernel_equirect_matches_fast_kernel():
     finally:
         ops.set_tuning("unp_rows", 1)
     assert _same_bits(outs[0], outs[1]), _first_diff(outs[0], outs[1])
+
+
+def _sel_cases():
+    """Maps that stress the window-only selection (k_sweep_w / k_resolve_w): spikes of equal
+    values at either percentile (zero floor / saturated maximum, just inside and just outside the
+    rank), quantised values, NaN / Inf, constant and tiny maps."""
+    rng = np.random.Generator(np.random.PCG64(7))
+    base = _smooth_depth(96, 128, 61)
+    out = {"smooth": base}
+    for frac in (0.015, 0.0199, 0.0201, 0.025, 0.3):          # zero floor around the p2 rank
+        d = base.copy()
+        d.ravel()[rng.permutation(d.size)[:int(frac * d.size)]] = 0.0
+        out[f"zero_{frac}"] = d
+    for frac in (0.019, 0.0205, 0.05):                          # saturated maximum around p98
+        d = base.copy()
+        d.ravel()[rng.permutation(d.size)[:int(frac * d.size)]] = np.float32(base.max())
+        out[f"sat_{frac}"] = d
+    out["quantised"] = (np.round(base * 16) / 16).astype(np.float32)
+    out["two_valued"] = np.where(rng.random(base.shape) < 0.5, 1.0, 2.0).astype(np.float32)
+    d = base.copy(); d[3, 4] = np.nan; d[10, 11] = np.inf; d[20, 0] = -np.inf
+    out["nan_inf"] = d
+    d = base.copy(); d.ravel()[rng.permutation(d.size)[:d.size * 2 // 5]] = np.nan
+    out["nan_40pct"] = d
+    out["constant"] = np.full_like(base, 2.5)
+    out["all_nan"] = np.full_like(base, np.nan)
+    return out
+
+
+@pytest.mark.parametrize("size", [(300, 400), (96, 128)])
+def test_window_selection_matches_histogram_levels_and_oracle(size):
+    """The batch path's window-only selection against the histogram levels (i2pc_set_tuning
+    'sel_windows' 0) and the oracle, bit for bit, on maps built to make windows miss."""
+    from image_to_pointcloud_amd import ops
+    g = _geom()
+    dev = torch.device("cuda")
+    H, W = size
+    cases = _sel_cases()
+    names = list(cases)
+    deps = np.stack([cases[k] for k in names])
+    imgs = np.stack([_rgb(H, W, 70 + i) for i in range(len(names))])
+    outs = []
+    try:
+        for win in (1, 0):
+            ops.set_tuning("sel_windows", win)
+            pb = g.unproject_batch(torch.from_numpy(deps).to(dev), torch.from_numpy(imgs).to(dev), density="high",
+                                   invert=True, depth_scale=10.0)
+            outs.append((pb.xyz.cpu().numpy(), pb.stats.cpu().numpy()))
+    finally:
+        ops.set_tuning("sel_windows", 1)
+    for i, k in enumerate(names):
+        assert _same_bits(outs[0][1][i], outs[1][1][i]), (k, outs[0][1][i], outs[1][1][i])
+        assert _same_bits(outs[0][0][i], outs[1][0][i]), (k, _first_diff(outs[0][0][i], outs[1][0][i]))
+        with np.errstate(all="ignore"):
+            ep, _ = ref.depth_to_point_cloud(imgs[i], deps[i], density="high", invert=True, depth_scale=10.0,
+                                             loop=False)
+        assert _same_bits(outs[0][0][i], ep), (k, _first_diff(outs[0][0][i], ep))

@@ -16,7 +16,7 @@
 #   trace-unp [B] [density]    kernel durations of the unprojection microbench (kernel trace only)
 #   pmc-unp                    SQ counters of the unprojection microbench
 set -o pipefail
-R=${ROUND:-r02}
+R=${ROUND:-r03}
 TASK=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out profiles

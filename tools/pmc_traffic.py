@@ -32,7 +32,9 @@ def label(name: str) -> str:
     return n
 
 
-def main(d, out):
+def main(d, out, steps=2):
+    """steps: eager bench steps per pass (tools/gpu.sh profile runs `--steps 1 --no-graph`, which
+    steps once before the timed step: 2), so per-step totals are the pass sums / steps."""
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
@@ -45,14 +47,18 @@ def main(d, out):
         write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
         res[k] = {"fetch_size_kb": round(fetch, 1), "write_size_kb": round(write, 1),
                   "dispatches": len(cs["FETCH_SIZE"]),
-                  "hbm_bytes_per_launch": round((2 * fetch + write) * 1024)}
+                  "hbm_bytes_per_launch": round((2 * fetch + write) * 1024),
+                  # every dispatch of the label in one step (e.g. a GEMM call's main + tail launch)
+                  "hbm_bytes_per_step": round((2 * sum(cs["FETCH_SIZE"]) + sum(cs["WRITE_SIZE"])) * 1024 / steps)}
     with open(out, "w") as fh:
         json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace), "
-                             "one eager bench step; hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
+                             "eager bench steps; hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024; "
+                             "hbm_bytes_per_launch averages the label's dispatches, hbm_bytes_per_step sums "
+                             f"them per step ({steps} steps per pass)",
                    "kernels": res}, fh, indent=1, sort_keys=True)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:12]:
         print(f"{k:60s} {v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch  ({v['dispatches']} dispatches)")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 2)
