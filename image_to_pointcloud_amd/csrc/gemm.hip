@@ -85,6 +85,10 @@ struct Args {
   uint32_t* Cs; int64_t ldcs;          // fp8 output scales (EPI_Q8), dwords per row
   uint32_t as_bytes, ws_bytes;
   int kspan;   // split-K (tile kernel): K-steps per blockIdx.y slice, 0 = the whole K
+  // LayerNorm fold (i2pc.h): consumer row scales float2 [M] + column sums [N]; producer chunk
+  // partials float2 [M][N / 64] + the bf16 copy of the fp32 output
+  const float* lnr; const float* csum;
+  float* lnp; bf16_t* cbf; int64_t ldcb;
 };
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
@@ -261,6 +265,30 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       float* c = static_cast<float*>(p.C) + off;
       *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      if constexpr (LPR % 8 == 0) {
+        if (p.lnp) {
+          // LayerNorm producer: the bf16 copy, and (mean, M2) of each 64-column chunk = 8 lanes
+          uint4 o;
+          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+          o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          *reinterpret_cast<uint4*>(p.cbf + (int64_t)m * p.ldcb + n) = o;
+          float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+          sm += __shfl_xor(sm, 1);
+          sm += __shfl_xor(sm, 2);
+          sm += __shfl_xor(sm, 4);
+          const float mean = sm * (1.0f / 64.0f);
+          float q = 0.f;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) q = __builtin_fmaf(v[t] - mean, v[t] - mean, q);
+          q += __shfl_xor(q, 1);
+          q += __shfl_xor(q, 2);
+          q += __shfl_xor(q, 4);
+          if ((c8 & 7) == 0)
+            *reinterpret_cast<float2*>(p.lnp + ((int64_t)m * (p.N / 64) + n / 64) * 2) = make_float2(mean, q);
+        }
+      }
     } else {
       uint4 o;
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -554,7 +582,7 @@ namespace pers {
 
 using namespace ::i2pc::mx;
 
-enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4, EPI_Q8 = 5 };
+enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4, EPI_Q8 = 5, EPI_LNF = 6 };
 constexpr int OOB = 0x7FFFFFF0;   // buffer range; offsets >= OOB are dropped / read as 0
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -634,16 +662,23 @@ template <int EPI> struct EpiCount {
 // columns ncol + j*16 + (lane >> 4)*4 (the swapped 16x16 MFMA layout), j < RN.  Issues exactly
 // RM * (loads + stores) vector-memory instructions (EpiCount), all unconditional -- plus, only in
 // the fp8 engine, plain row-bias / table loads the counted waits tolerate (extra, older-first).
+// EPI_LNF (LayerNorm fold, i2pc.h): t = rs.x * acc + rs.y * col_sum + bias with the wave's row
+// scales rs (float2, from LDS at rows_lds[local row]) and column sums (LDS, like the bias).
 template <int RM, int RN, int EPI, bool F8>
 __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], int mw0, int ncol, const float* bias_lds,
-                                           rsrc_t c_rs, rsrc_t r_rs, rsrc_t r2_rs, rsrc_t cs_rs) {
+                                           rsrc_t c_rs, rsrc_t r_rs, rsrc_t r2_rs, rsrc_t cs_rs,
+                                           const float* csum_lds = nullptr, const float* rows_lds = nullptr) {
     constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
     static_assert(RN == 2 || RN == 4, "RN");
     const int lane = threadIdx.x & 63;
     const int frow = lane & 15, fq = lane >> 4;
-    float4 bias4[RN];
+    float4 bias4[RN], csum4[RN];
 #pragma unroll
     for (int j = 0; j < RN; ++j) bias4[j] = *reinterpret_cast<const float4*>(bias_lds + fq * 4 + j * 16);
+    if constexpr (EPI == EPI_LNF) {
+#pragma unroll
+      for (int j = 0; j < RN; ++j) csum4[j] = *reinterpret_cast<const float4*>(csum_lds + fq * 4 + j * 16);
+    }
     const int mrow = mw0 + frow;       // + i * 16
     const int act = p.act;
     constexpr bool CT = EPI == EPI_CT;
@@ -707,10 +742,20 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
       const bool ok = m < p.M;
       const int mc = ok ? m : p.M - 1;
       float v[RN][4];
+      float2 rs = make_float2(1.f, 0.f);
+      if constexpr (EPI == EPI_LNF) rs = *reinterpret_cast<const float2*>(rows_lds + (i * 16 + frow) * 2);
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        float t[4] = {acc[i][j][0] + bias4[j].x, acc[i][j][1] + bias4[j].y, acc[i][j][2] + bias4[j].z,
-                      acc[i][j][3] + bias4[j].w};
+        float t[4];
+        if constexpr (EPI == EPI_LNF) {
+          t[0] = __builtin_fmaf(acc[i][j][0], rs.x, __builtin_fmaf(csum4[j].x, rs.y, bias4[j].x));
+          t[1] = __builtin_fmaf(acc[i][j][1], rs.x, __builtin_fmaf(csum4[j].y, rs.y, bias4[j].y));
+          t[2] = __builtin_fmaf(acc[i][j][2], rs.x, __builtin_fmaf(csum4[j].z, rs.y, bias4[j].z));
+          t[3] = __builtin_fmaf(acc[i][j][3], rs.x, __builtin_fmaf(csum4[j].w, rs.y, bias4[j].w));
+        } else {
+          t[0] = acc[i][j][0] + bias4[j].x; t[1] = acc[i][j][1] + bias4[j].y;
+          t[2] = acc[i][j][2] + bias4[j].z; t[3] = acc[i][j][3] + bias4[j].w;
+        }
         if constexpr (F8 && (EPI == EPI_PLAIN || EPI == EPI_Q8)) {   // per-image row bias (DPT readout CLS half), position table
           const int n = ncol + j * 16 + fq * 4;
           if (p.rbias) {
@@ -821,9 +866,12 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   constexpr int SC_BYTES = F8 ? (BM + BN) * 4 : 0;
   constexpr int STAGE = A_BYTES + W_BYTES + SC_BYTES;
   constexpr int BIAS_OFF = 2 * STAGE;
+  constexpr int CSUM_OFF = BIAS_OFF + 2048;          // EPI_LNF: column sums [2][1 KB], row scales [2][BM * 8]
+  constexpr int ROWS_OFF = CSUM_OFF + 2048;
   constexpr int NRL = EpiCount<EPI>::loads * RN / 4, NS = EpiCount<EPI>::stores;
   constexpr int E_ALL = RM * (NRL + NS);
   static_assert(BM == 256 || BM == 320, "BM");
+  static_assert(EPI != EPI_LNF || (BM == 256 && !F8 && !CONV), "EPI_LNF: dense bf16 A, BM 256");
   static_assert(BN == 256 || BN == 128, "BN");
   static_assert(!F8 || BM == 256, "fp8 engine: BM 256 (scale loads: one wave per 64 rows)");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -896,12 +944,26 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   // one K-stage (A BM x KSTEP, W BN x KSTEP [+ their scale dwords]) into LDS buffer `buf`;
   // with `bias_par` >= 0 wave 0 first stages the tile's BN bias values into bias slot bias_par
+  const rsrc_t cs_rs_ln = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.csum), 0, EPI == EPI_LNF ? p.N * 4 : 0,
+                                                            0x00020000);
+  const rsrc_t lr_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.lnr), 0, EPI == EPI_LNF ? p.M * 8 : 0,
+                                                         0x00020000);
   auto stage = [&](int buf, int k0, int bias_par) {
     uint8_t* sA = smem + buf * STAGE;
     uint8_t* sW = sA + A_BYTES;
     if (bias_par >= 0 && wid == 0 && lane < BN / 4)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rs, (lds_ptr_t)(smem + BIAS_OFF + bias_par * 1024), 16,
                                                 (nn0 + lane * 4) * 4, 0, 0, 0);
+    if constexpr (EPI == EPI_LNF) {
+      // the tile's column sums (wave 1) and its BM rows' (rstd, -rstd * mean) (waves 2, 3; rows past
+      // M read as zero), landing with the stage
+      if (bias_par >= 0 && wid == 1 && lane < BN / 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(cs_rs_ln, (lds_ptr_t)(smem + CSUM_OFF + bias_par * 1024), 16,
+                                                  (nn0 + lane * 4) * 4, 0, 0, 0);
+      if (bias_par >= 0 && (wid == 2 || wid == 3))
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lr_rs, (lds_ptr_t)(smem + ROWS_OFF + bias_par * BM * 8 + (wid - 2) * 1024),
+                                                  16, (nm0 + (wid - 2) * 128 + lane * 2) * 8, 0, 0, 0);
+    }
     int kk = 0, ky = 0, kx = 0, ci0 = 0;
     if constexpr (CONV) {
       kk = k0 / p.cc;
@@ -1062,7 +1124,8 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     // ---- epilogue of tile (m0, n0): register-direct, counted
     epilogue_p<RM, RN, EPI, F8>(p, acc, m0 + wm * TM, n0 + wn * (BN / 4),
                                 reinterpret_cast<const float*>(smem + BIAS_OFF + tpar * 1024) + wn * (BN / 4), c_rs, r_rs,
-                                r2_rs, cs_rs);
+                                r2_rs, cs_rs, reinterpret_cast<const float*>(smem + CSUM_OFF + tpar * 1024) + wn * (BN / 4),
+                                reinterpret_cast<const float*>(smem + ROWS_OFF + tpar * BM * 8) + wm * TM * 2);
     PSTAMP(tord, 3);
     ++tord;
     if (!has_next) break;
@@ -1563,7 +1626,7 @@ static void launch_p(const Args& p, hipStream_t s) {
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = p.N / BN;
   q.group_m = group_m_for(q.tiles_m);
-  const int smem = 2 * ((BM + BN) * 128 + (F8 ? (BM + BN) * 4 : 0)) + 2048;
+  const int smem = 2 * ((BM + BN) * 128 + (F8 ? (BM + BN) * 4 : 0)) + 2048 + (EPI == pers::EPI_LNF ? 2048 + 2 * BM * 8 : 0);
   auto kern = pers::k_gemm_p<BM, CONV, RELU_A, EPI, BN, F8>;
   static bool attr = false;
   if (!attr) {
@@ -1663,7 +1726,14 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   int epi = -1;
   // N a multiple of 128 only (e.g. the DPT head's first conv, 256 -> 128): 256 x 128 tiles
   const int pbn = p.N % 256 == 0 ? 256 : (p.N % 128 == 0 && g_bn128) ? 128 : 0;
-  if (pbn && !p.rbias && !p.tbl && force == 0 && pforce != 1) {
+  if (p.lnr) {
+    // LayerNorm-fold consumer: the persistent engine's EPI_LNF only (dense A, bf16 out, no extras)
+    const bool ok = pbn && !conv && !relu && !p.rbias && !p.tbl && !p.res && !p.res2 && !p.c_f32 && p.ct_s == 0 &&
+                    p.a_g == 0 && (int64_t)(p.M + 320) * p.lda * 2 < pers::OOB && (int64_t)p.N * p.ldw * 2 < pers::OOB &&
+                    (max_row(p) * p.ldc + p.N) * 2 < pers::OOB;
+    return ok ? Plan{1, 256, pbn, pers::EPI_LNF} : Plan{-2, 0, 0, 0};
+  }
+  if (pbn && !p.rbias && !p.tbl && !p.lnp && force == 0 && pforce != 1) {
     const bool ct = p.ct_s > 0;
     if (ct) epi = (!p.res && !p.res2 && !p.c_f32 && p.ct_c % 8 == 0) ? pers::EPI_CT : -1;
     else if (!p.res && !p.res2 && !p.c_f32) epi = pers::EPI_PLAIN;
@@ -1744,6 +1814,12 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   else if (p.N % 64 == 0) pl = Plan{0, 128, 64, 64};
   else if (p.N % 32 == 0) pl = Plan{0, 128, 32, 64};
   else pl = Plan{-1, 0, 0, 0};
+  if (p.lnp && pl.kind == 0) {
+    // LayerNorm-fold producer: the tile epilogue's row layout must give whole 64-column chunks
+    // to 8-lane groups (wave tile a multiple of 64 columns)
+    const int wn = pl.bn == 256 ? 4 : pl.bn == 32 || pl.bn == 192 ? (pl.bn == 192 ? 2 : 1) : 2;
+    if ((pl.bn / wn) % 64 != 0) pl = p.N % 128 == 0 ? Plan{0, 128, 128, 64} : Plan{-2, 0, 0, 0};
+  }
   return pl;
 }
 
@@ -1759,7 +1835,7 @@ struct SplitPlan {
 
 static SplitPlan split_for(const Args& p, const Plan& pl) {
   SplitPlan sp;
-  if (!g_splitk || pl.kind != 0 || (g_engine != 0 && g_engine != 3)) return sp;   // automatic modes only
+  if (!g_splitk || pl.kind != 0 || (g_engine != 0 && g_engine != 3) || p.lnp) return sp;   // automatic modes only
   int bm, bn, kb = 64, slots = 1;
   if (g_split_tile == 1 && p.N % 128 == 0) { bm = bn = 128; kb = 32; slots = 4; }
   else if (p.N % 256 == 0) bm = bn = 256;
@@ -1814,7 +1890,7 @@ static const int g_quarter = [] { const char* e = getenv("I2PC_GEMM_Q"); return 
 template <bool CONV, bool RELU_A>
 static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
   using namespace pers;
-  if (g_quarter && p.K >= 128) {
+  if (g_quarter && p.K >= 128 && pl.epi != EPI_LNF) {
     if constexpr (!CONV && !RELU_A) {
       if (pl.epi == EPI_PLAIN) { launch_q<false, false, EPI_PLAIN>(p, s); return check_launch("gemm_q"); }
       if (pl.epi == EPI_RESF32) { launch_q<false, false, EPI_RESF32>(p, s); return check_launch("gemm_q"); }
@@ -1827,15 +1903,19 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
       return check_launch("gemm_q");
     }
   }
-  if (pl.bn == 128) {   // plan: EPI_PLAIN, no ReLU on A
+  if (pl.bn == 128) {   // plan: EPI_PLAIN (or EPI_LNF), no ReLU on A
     if constexpr (!RELU_A) {
+      if constexpr (!CONV) {
+        if (pl.epi == EPI_LNF) { launch_p<256, false, false, EPI_LNF, 128>(p, s); return check_launch("gemm"); }
+      }
       launch_p<256, CONV, false, EPI_PLAIN, 128>(p, s);
       return check_launch("gemm");
     }
     return set_error(I2PC_EUNSUPPORTED, "gemm: no persistent BN=128 variant with ReLU on A");
   }
   if constexpr (!CONV && !RELU_A) {
-    if (pl.epi == EPI_PLAIN) launch_p<256, false, false, EPI_PLAIN>(p, s);
+    if (pl.epi == EPI_LNF) launch_p<256, false, false, EPI_LNF>(p, s);
+    else if (pl.epi == EPI_PLAIN) launch_p<256, false, false, EPI_PLAIN>(p, s);
     else if (pl.epi == EPI_RESF32) launch_p<256, false, false, EPI_RESF32>(p, s);
     else launch_p<256, false, false, EPI_CT>(p, s);
   } else if constexpr (CONV && !RELU_A) {
@@ -1877,13 +1957,21 @@ template <bool CONV, bool RELU_A>
 static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
   if constexpr (!CONV && !RELU_A) {
     int ma = 0;
-    const int ts = (pl.kind == 1 || pl.kind == 2) && pl.epi == pers::EPI_PLAIN && !g_quarter ? tail_split(p, ma) : 0;
+    const bool lnf = pl.epi == pers::EPI_LNF;
+    const int ts = (pl.kind == 1 || pl.kind == 2) && (pl.epi == pers::EPI_PLAIN || lnf) && pl.bn == 256 && !g_quarter
+                       ? tail_split(p, ma) : 0;
     if (ts) {
       Args pa = p, pb = p;
       pa.M = ma;
       pb.M = p.M - ma;
       pb.a_o = p.a_o + ma;
       pb.o_o = p.o_o + ma;
+      if (lnf) {
+        pb.lnr = p.lnr + (int64_t)ma * 2;      // row scales follow the rows
+        launch_p<256, false, false, pers::EPI_LNF>(pa, s);
+        launch_p<256, false, false, pers::EPI_LNF, 128>(pb, s);
+        return check_launch("gemm (tail split)");
+      }
       if (pl.kind == 2) launch_8p<pers::EPI_PLAIN>(pa, s);
       else launch_p<256, false, false, pers::EPI_PLAIN>(pa, s);
       launch_p<256, false, false, pers::EPI_PLAIN, 128>(pb, s);
@@ -1899,6 +1987,7 @@ static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
     return set_error(I2PC_EUNSUPPORTED, "gemm: no ping-pong variant");
   }
   if (pl.kind == 1) return run_persistent<CONV, RELU_A>(pl, p, s);
+  if (pl.kind == -2) return set_error(I2PC_EUNSUPPORTED, "gemm: LayerNorm fold not available for this call");
   if (pl.kind < 0) return set_error(I2PC_EUNSUPPORTED, "gemm: N=%d must be a multiple of 32", p.N);
   if (pl.bm == 256 && pl.epi == 64) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
   else if (pl.bm == 256) launch<256, 256, 2, 4, 32, CONV, RELU_A>(p, s);
@@ -1925,13 +2014,15 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu, const SplitPl
   if (pl.kind == 2) {
     snprintf(buf, sizeof buf, "k_gemm_8p<%s>", pl.epi == pers::EPI_PLAIN ? "plain" : "res_f32");
   } else if (pl.kind == 1) {
-    static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT"};
+    static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8", "ln_fold"};
     if (g_quarter && pl.epi != pers::EPI_CT) snprintf(buf, sizeof buf, "k_gemm_q<%s, %s, %s>", c, r, epis[pl.epi]);
     else if (pl.bn == 128) snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s, 128>", pl.bm, c, r, epis[pl.epi]);
     else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
   } else if (pl.kind == 0) {
     const int wm = pl.bn == 32 || pl.bn == 192 ? 4 : 2, wn = pl.bn == 256 ? 4 : pl.bn == 32 ? 1 : 2;
     snprintf(buf, sizeof buf, "k_gemm<%d, %d, %d, %d, %d, %s, %s>", pl.bm, pl.bn, wm, wn, pl.epi, c, r);
+  } else if (pl.kind == -2) {
+    snprintf(buf, sizeof buf, "invalid");
   } else {
     snprintf(buf, sizeof buf, "unsupported");
   }
@@ -2036,6 +2127,15 @@ static int make_args(const i2pc_gemm_desc* d, gemm::Args& p) {
   p.C = d->c; p.c_f32 = d->c_f32; p.ldc = d->ldc;
   p.o_g = d->out_group; p.o_gs = d->out_group_stride; p.o_o = d->out_offset;
   p.ct_s = d->convt_s; p.ct_h = d->convt_h; p.ct_w = d->convt_w; p.ct_c = d->convt_c;
+  p.lnr = d->ln_rows; p.csum = d->col_sum;
+  p.lnp = d->ln_part; p.cbf = static_cast<gemm::bf16_t*>(d->c_bf16); p.ldcb = d->ldc_bf16;
+  if (d->ln_rows) I2PC_REQUIRE(d->col_sum, "gemm: ln_rows needs col_sum");
+  if (d->ln_part) {
+    I2PC_REQUIRE(d->c_bf16 && d->c_f32 && d->n % 64 == 0 && d->ldc_bf16 % 8 == 0 && d->ldc_bf16 >= d->n,
+                 "gemm: ln_part needs c_bf16 (ldc_bf16 %% 8, >= n), an fp32 output and n %% 64 == 0");
+    I2PC_REQUIRE(d->out_group == 0 && d->out_offset == 0 && d->convt_s == 0, "gemm: ln_part needs a linear output row map");
+    I2PC_REQUIRE(!d->ln_rows, "gemm: ln_part and ln_rows in one call");
+  }
   if (d->conv) {
     I2PC_REQUIRE(d->conv_c % 64 == 0, "conv: Cin=%d must be a multiple of 64", d->conv_c);
     I2PC_REQUIRE(d->k == d->conv_k * d->conv_k * d->conv_c, "conv: K != k*k*Cin");

@@ -225,6 +225,33 @@ __global__ __launch_bounds__(256) void k_head_out(const bf16_t* __restrict__ x, 
   }
 }
 
+// LayerNorm row statistics from the 64-column chunk partials an i2pc_gemm producer epilogue
+// wrote ((mean, M2) per chunk): Chan's pairwise-free combination for equal chunk counts,
+// mean = avg(mean_c), M2 = sum M2_c + 64 sum (mean_c - mean)^2, var = M2 / (64 P) (biased, as
+// nn.LayerNorm), out = (rstd, -rstd * mean).  One thread per row, all its partials in flight.
+__global__ __launch_bounds__(256) void k_ln_rowstats(const float4* __restrict__ part, int rows, int P, float eps,
+                                                     float2* __restrict__ out) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  const float4* q = part + (int64_t)r * (P / 2);
+  float mu[64], m2[64];
+#pragma unroll 8
+  for (int i = 0; i < P / 2; ++i) {
+    const float4 v = q[i];
+    mu[2 * i] = v.x; m2[2 * i] = v.y; mu[2 * i + 1] = v.z; m2[2 * i + 1] = v.w;
+  }
+  float sm = 0.f;
+  for (int i = 0; i < P; ++i) sm += mu[i];
+  const float mean = sm / (float)P;
+  float M2 = 0.f;
+  for (int i = 0; i < P; ++i) {
+    const float d = mu[i] - mean;
+    M2 += m2[i] + 64.0f * d * d;
+  }
+  const float rstd = 1.0f / sqrtf(M2 / (float)(64 * P) + eps);
+  out[r] = make_float2(rstd, -rstd * mean);
+}
+
 static int grid_for(int64_t work, int per_block = 256) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((work + per_block - 1) / per_block, 256 * 16));
 }
@@ -240,6 +267,16 @@ static thread_local int g_ln2 = 1;   // "ln_f2": the float2 row kernel for dim 3
 bool i2pc_misc_tune(const char* name, int value) {
   if (std::strcmp(name, "ln_f2") == 0) { g_ln2 = value; return true; }
   return false;
+}
+
+extern "C" int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(part && rows_out, "NULL pointer");
+  I2PC_REQUIRE(rows > 0 && parts >= 2 && parts <= 64 && parts % 2 == 0, "ln_rowstats: parts=%d must be even, 2..64",
+               parts);
+  hipLaunchKernelGGL(k_ln_rowstats, dim3((rows + 255) / 256), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(part), rows, parts, eps, reinterpret_cast<float2*>(rows_out));
+  return check_launch("ln_rowstats");
 }
 
 extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,

@@ -52,6 +52,8 @@ constexpr int kWinKeys = 6144;   // expected full-resolution keys per level-0 wi
 constexpr int kTileW = 1024;     // selection sweep column tile (4 columns per thread)
 constexpr int kSlotWords = kBins / 2;   // sweep LDS per slot: 2048 packed 16-bit counts or 1024 staged keys
 constexpr int kHrowBudget = 40 * 1024;   // LDS bytes of staged + horizontally interpolated model rows
+constexpr int kStageW = 256;             // k_sweep_w: window keys a workgroup stages in LDS per window
+constexpr int kMaxSelRows = 64;          // k_sweep_w: output rows per workgroup at most
 
 // PH_INIT: level-0 sweep pending; PH_SEL: targets being narrowed; PH_SLOW: handed to
 // k_sel_slow (non-finite map); PH_DONE: p2 / p98 / mode final.
@@ -126,7 +128,7 @@ struct Geo {
 inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
-  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, field, tmp, total;
+  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, mhist, field, tmp, total;
   uint32_t cap;   // candidate keys per slot and image (compaction sweeps)
 };
 
@@ -148,6 +150,7 @@ static Layout layout(int B, int H, int W, int smooth) {
   L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
   L.trig = off;  off = align_up(off + sizeof(double) * 2 * ((size_t)W + H), 256);
   L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)B, 256);
+  L.mhist = off; off = align_up(off + sizeof(uint32_t) * kRangeChunks * kBins * (size_t)B, 256);
   L.field = off;
   if (smooth) {
     off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
@@ -400,11 +403,13 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
   }
 }
 
-// Level-0 histogram of a sample of each full-resolution map (finite values, the level-0 binning), into
-// histogram slot 3 (unused at level 0): the estimate k_window predicts the target bins from.
-__global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* hist,
+// Level-0 histogram of a sample of each full-resolution map (finite values, the level-0 binning):
+// one partial histogram per (image, chunk) in `mhist` [B][kRangeChunks][kBins], summed by k_window
+// (no global atomics: every chunk's workgroup sees most bins of its image).  The estimate k_window
+// predicts the target bins from.
+__global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* mhist,
                                                        const uint32_t* rpart, int stride) {
-  __shared__ uint32_t lh[kBins];
+  __shared__ __attribute__((aligned(16))) uint32_t lh[kBins];
   __shared__ uint32_t rr[2];
   const int b = blockIdx.x % B, c = blockIdx.x / B;
   SelState* S = st + b;
@@ -429,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   // column, values recomputed with the cv2 taps): its quantiles are the full map's up to
   // sampling noise, unlike the model pixels' (a zero floor of isolated model pixels all but
   // vanishes in the resize).  Each thread bins a contiguous run of samples (neighbours share
-  // bins: one LDS atomic per run).
+  // bins: one LDS atomic per run), 8 samples' loads in flight at a time.
   const int nsx = (g.W + stride - 1) / stride, nsy = (g.H + stride - 1) / stride, ns = nsx * nsy;
   const int per = (ns + kRangeChunks - 1) / kRangeChunks;
   const int i0 = c * per, i1 = min(ns, i0 + per);
@@ -437,18 +442,46 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   const int t0 = i0 + threadIdx.x * tper, t1 = min(i1, t0 + tper);
   int run = -1;
   uint32_t cnt = 0;
-  for (int i = t0; i < t1; i += 4) {
-    float v[4];
+  for (int i = t0; i < t1; i += 8) {
+    float v[8];
+    if (g.same) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < 8; ++k) {
+        const int si = min(i + k, t1 - 1), sy = si / nsx, sx = si - sy * nsx;
+        const int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
+        v[k] = sample(g, b, min(sy * stride + jy, g.H - 1), min(sx * stride + jx, g.W - 1));
+      }
+    } else {
       // jittered lattice: the offset inside each stride x stride cell cycles with the cell, so
       // every residue of the cv2 tap pattern (single-tap columns/rows included) is sampled
-      const int si = min(i + k, t1 - 1), sy = si / nsx, sx = si - sy * nsx;
-      const int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
-      v[k] = sample(g, b, min(sy * stride + jy, g.H - 1), min(sx * stride + jx, g.W - 1));
+      Tap ty[8], tx[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int si = min(i + k, t1 - 1), sy = si / nsx, sx = si - sy * nsx;
+        const int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
+        ty[k] = g.yt[min(sy * stride + jy, g.H - 1)];
+        tx[k] = g.xt[min(sx * stride + jx, g.W - 1)];
+      }
+      const float* D = g.depth + (size_t)b * g.dh * g.dw;
+      float a0[8], a1[8], c0[8], c1[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float* r0 = D + (size_t)ty[k].i0 * g.dw;
+        const float* r1 = D + (size_t)ty[k].i1 * g.dw;
+        const int x1 = tx[k].i1 < 0 ? tx[k].i0 : tx[k].i1;
+        a0[k] = r0[tx[k].i0]; a1[k] = r0[x1];
+        c0[k] = r1[tx[k].i0]; c1[k] = r1[x1];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {     // sample()'s arithmetic (single-tap columns: the raw value)
+        float h0, h1;
+        if (tx[k].i1 < 0) { h0 = a0[k]; h1 = c0[k]; }
+        else { h0 = a0[k] * tx[k].w0 + a1[k] * tx[k].w1; h1 = c0[k] * tx[k].w0 + c1[k] * tx[k].w1; }
+        v[k] = h0 * ty[k].w0 + h1 * ty[k].w1;
+      }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const int bn = (i + k < t1 && isfinite(v[k])) ? (int)vbin(v[k], vb) : -1;
       if (bn != run && run >= 0) atomicAdd(&lh[run], cnt);
       cnt = (bn == run ? cnt : 0u) + 1u;
@@ -457,9 +490,9 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   }
   if (run >= 0) atomicAdd(&lh[run], cnt);
   __syncthreads();
-  uint32_t* gh = hist + ((size_t)b * kSlots + 3) * kBins;
-  for (int i = threadIdx.x; i < kBins; i += kBlock)
-    if (lh[i]) atomicAdd(&gh[i], lh[i]);
+  uint4* gh = reinterpret_cast<uint4*>(mhist + ((size_t)b * kRangeChunks + c) * kBins);
+  const uint4* l4 = reinterpret_cast<const uint4*>(lh);
+  for (int i = threadIdx.x; i < kBins / 4; i += kBlock) gh[i] = l4[i];
 }
 
 // Block histogram in LDS as packed 16-bit counts (bin pairs share a word; a sweep workgroup
@@ -748,11 +781,14 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
 template <bool SAME>
 __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_t* cand, uint32_t cap, int B,
                                                     Sweep sw) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem_u[];
-  uint32_t* sh = smem_u;                                                  // [3][kSlotWords] staged keys
-  float* hrow = reinterpret_cast<float*>(smem_u + 3 * kSlotWords);        // [rows][kTileW]
+  // thread = 4 columns c0 + j * kBlock + tid of a kTileW-column tile, walking down the block's
+  // R output rows.  The horizontal cv2 pass of a model row is a thread's own business (its 4
+  // columns), so it stays in registers: rows ra (hA) and ra + 1 (hB) interpolated, the raw
+  // taps of row ra + 2 already loaded (pre) -- a model row advance costs no wait and no LDS.
+  __shared__ uint32_t sh[3][kStageW];               // staged window keys
   __shared__ uint32_t red[kBlock / 64][24];
   __shared__ uint32_t lcnt[3], gbase[3];
+  __shared__ Tap tys[kMaxSelRows];                  // the block's row taps (no global load in the row loop)
   int b, chunk;
   map_block(blockIdx.x, B, sw.nrb * sw.ntiles, b, chunk);
   const int rb = chunk / sw.ntiles, c0 = (chunk - rb * sw.ntiles) * kTileW;
@@ -770,57 +806,78 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
   const int v0 = sw.row0 + rb * sw.R;
   const int v1 = min(sw.row_end, v0 + sw.R);
   if (threadIdx.x < 3) lcnt[threadIdx.x] = 0;
-  int lo = 0;
-  if (!SAME) {
-    lo = g.yt[v0].i0;
-    const int nr = g.yt[v1 - 1].i1 - lo + 1;
-    const float* D = g.depth + ((size_t)b * g.dh + lo) * g.dw;
-    float* raw = hrow + (size_t)sw.lds_rows * kTileW;
-    Tap tx[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) tx[j] = g.xt[c0 + min(j * kBlock + (int)threadIdx.x, cw - 1)];
-    if (sw.raw) {
-      stage_floats(raw, D, nr * g.dw);
-      __syncthreads();
-    }
-    const float* src = sw.raw ? raw : D;
-    for (int k = 0; k < nr; ++k) {
-      const float* r = src + (size_t)k * g.dw;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int u = j * kBlock + (int)threadIdx.x;
-        if (u < cw) hrow[k * kTileW + u] = r[tx[j].i0] * tx[j].w0 + r[tx[j].i1 < 0 ? tx[j].i0 : tx[j].i1] * tx[j].w1;
-      }
-    }
-  }
+  if (!SAME && (int)threadIdx.x < v1 - v0) tys[threadIdx.x] = g.yt[v0 + threadIdx.x];
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float* Dimg = g.depth + (size_t)b * g.dh * g.dw;
+  int ucol[4];
+  bool act[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    act[j] = j * kBlock + (int)threadIdx.x < cw;
+    ucol[j] = c0 + min(j * kBlock + (int)threadIdx.x, cw - 1);
+  }
+  Tap tx[4];
+  float hA[4], hB[4], pre[8];
+  int ra = 0;
+  auto load_raw = [&](int r, float (&q)[8]) {
+    const float* R0 = Dimg + (size_t)min(r, g.dh - 1) * g.dw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      q[2 * j] = R0[tx[j].i0];
+      q[2 * j + 1] = R0[tx[j].i1 < 0 ? tx[j].i0 : tx[j].i1];
+    }
+  };
+  auto interp = [&](const float (&q)[8], float (&h)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[j] = q[2 * j] * tx[j].w0 + q[2 * j + 1] * tx[j].w1;   // cv2 HResizeLinear
+  };
+  float cur[4];
+  if (SAME) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = Dimg[(size_t)v0 * g.dw + ucol[j]];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tx[j] = g.xt[ucol[j]];
+    ra = tys[0].i0;
+    float q0[8], q1[8];
+    load_raw(ra, q0);
+    load_raw(ra + 1, q1);
+    load_raw(ra + 2, pre);
+    interp(q0, hA);
+    interp(q1, hB);
+  }
+
   uint32_t nf = 0, nnan = 0, nneg = 0, npos = 0, kmin = 0xffffffffu, kmax = 0u;
   uint32_t below[3] = {0, 0, 0};
   uint32_t cF[3] = {0, 0, 0}, mnF[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mxF[3] = {0, 0, 0};
   uint32_t cL[3] = {0, 0, 0}, mnL[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mxL[3] = {0, 0, 0};
-  Tap ty_next = SAME ? Tap{0, 0, 1.f, 0.f} : g.yt[v0];
   for (int v = v0; v < v1; ++v) {
-    float ha[4], hc[4];
-    const Tap ty = ty_next;
-    if (!SAME) ty_next = g.yt[min(v + 1, v1 - 1)];
+    float val[4];
+    if (SAME) {
+      // the next row's values in flight while this row is binned
+      const int vn = min(v + 1, v1 - 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int uc = min(j * kBlock + (int)threadIdx.x, cw - 1);
-      if (SAME) {
-        ha[j] = Dimg[(size_t)v * g.dw + c0 + uc];
-      } else {
-        ha[j] = hrow[(ty.i0 - lo) * kTileW + uc];
-        hc[j] = hrow[(ty.i1 - lo) * kTileW + uc];
+      for (int j = 0; j < 4; ++j) { val[j] = cur[j]; cur[j] = Dimg[(size_t)vn * g.dw + ucol[j]]; }
+    } else {
+      const Tap ty = tys[v - v0];
+      // advance the register rows to ty.i0 (wave-uniform; once per ~H / dh output rows)
+      while (ra < ty.i0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hA[j] = hB[j];
+        interp(pre, hB);
+        ++ra;
+        load_raw(ra + 2, pre);
       }
+      const bool second_is_a = ty.i1 == ra;     // (the bottom rows clamp i1 to i0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) val[j] = hA[j] * ty.w0 + (second_is_a ? hA[j] : hB[j]) * ty.w1;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool active = j * kBlock + (int)threadIdx.x < cw;
-      const float val = SAME ? ha[j] : ha[j] * ty.w0 + hc[j] * ty.w1;
-      const uint32_t key = f2key(val);
+      const bool active = act[j];
+      const uint32_t key = f2key(val[j]);
       const bool fin = active && !key_nonfinite(key);
       if (active && !fin) {
         ++nf;
@@ -830,7 +887,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
       }
       kmin = min(kmin, fin ? key : 0xffffffffu);
       kmax = max(kmax, fin ? key : 0u);
-      const int hb = fin ? (int)vbin(val, vb0) : kBins;      // non-finite: in no window, below none
+      const int hb = fin ? (int)vbin(val[j], vb0) : kBins;      // non-finite: in no window, below none
       int cq = -1;
 #pragma unroll
       for (int w = 0; w < 3; ++w) {
@@ -862,8 +919,8 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
           base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
           if (cq == q) {
             const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (pos < (uint32_t)kSlotWords) {
-              sh[q * kSlotWords + pos] = key;
+            if (pos < (uint32_t)kStageW) {
+              sh[q][pos] = key;
             } else {
               const uint32_t gpos = atomicAdd(&S->ccount[q], 1u);
               if (gpos < cap) cand[((size_t)b * kSlots + q) * cap + gpos] = key;
@@ -917,7 +974,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
       uint32_t bw = 0;
       for (int w = 0; w < kBlock / 64; ++w) bw += red[w][3 + q];
       if (bw) atomicAdd(&S->wbelow[q], bw);
-      const uint32_t nq = min(lcnt[q], (uint32_t)kSlotWords);
+      const uint32_t nq = min(lcnt[q], (uint32_t)kStageW);
       gbase[q] = nq ? atomicAdd(&S->ccount[q], nq) : 0u;
       if (spk[q]) {
         uint32_t a = 0, cmn = 0xffffffffu, dmx = 0, e = 0, fmn = 0xffffffffu, hmx = 0;
@@ -932,11 +989,10 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
   }
   __syncthreads();
   for (int q = 0; q < nwin; ++q) {
-    const uint32_t nq = min(lcnt[q], (uint32_t)kSlotWords);
-    const uint32_t* src = sh + q * kSlotWords;
+    const uint32_t nq = min(lcnt[q], (uint32_t)kStageW);
     uint32_t* dst = cand + ((size_t)b * kSlots + q) * cap;
     for (uint32_t i = threadIdx.x; i < nq; i += kBlock)
-      if (gbase[q] + i < cap) dst[gbase[q] + i] = src[i];
+      if (gbase[q] + i < cap) dst[gbase[q] + i] = sh[q][i];
   }
 }
 
@@ -1086,13 +1142,23 @@ __device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint3
     }
   }
   __syncthreads();
+  // narrow every unresolved target; targets sharing an interval (the adjacent ranks i0, i0 + 1 of
+  // one percentile, usually) share each round
+  uint32_t grank[kMaxTgt];
+  int gidx[kMaxTgt];
   for (int j = 0; j < nt; ++j) {
     for (int it = 0; it < 4 && tl[j] < tz[j]; ++it) {
-      cand_round(keys, c, tl[j], tz[j], &tr[j], 1, lh, wsum, rbin, rrem);
+      const uint32_t l = tl[j], z = tz[j];
+      int ng = 0;
+      for (int k = j; k < nt; ++k)
+        if (tl[k] == l && tz[k] == z) { gidx[ng] = k; grank[ng++] = tr[k]; }
+      cand_round(keys, c, l, z, grank, ng, lh, wsum, rbin, rrem);
       if (threadIdx.x == 0) {
-        const uint32_t l = tl[j], z = tz[j];
-        bin_interval(rbin[0], l, bin_mult(l, z), l, z, tl[j], tz[j]);
-        tr[j] = rrem[0];
+        const uint32_t mult = bin_mult(l, z);
+        for (int q = 0; q < ng; ++q) {
+          bin_interval(rbin[q], l, mult, l, z, tl[gidx[q]], tz[gidx[q]]);
+          tr[gidx[q]] = rrem[q];
+        }
       }
       __syncthreads();
     }
@@ -1107,19 +1173,28 @@ __device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint3
 // whose keys the level-0 sweep compacts.  When a target's bin lies inside a window (and the
 // window did not overflow), the level-0 resolve selects the exact key from those candidates
 // and the later levels are no-ops; otherwise they run as usual.  Consumes histogram slot 3.
-__global__ __launch_bounds__(kBlock) void k_window(SelState* st, uint32_t* hist, uint32_t cap, int B, int enable,
-                                                   int m) {
-  __shared__ uint32_t mh[kBins];
+__global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t* mhist, uint32_t cap, int B,
+                                                   int enable, int m) {
+  __shared__ __attribute__((aligned(16))) uint32_t mh[kBins];
   __shared__ uint32_t wsum[kBlock / 64], wb[6], tot;
   const int b = blockIdx.x;
   if (b >= B) return;
   SelState* S = st + b;
-  uint32_t* gh = hist + ((size_t)b * kSlots + 3) * kBins;
+  // the sample histogram: k_model_hist's per-chunk partials summed (8 bins per thread, all loads in flight)
   uint32_t local = 0;
-  for (int i = threadIdx.x; i < kBins; i += kBlock) {
-    mh[i] = gh[i];
-    local += gh[i];
-    gh[i] = 0;
+  {
+    static_assert(kBins == 8 * kBlock, "k_window: 8 bins per thread");
+    const uint4* src = reinterpret_cast<const uint4*>(mhist + (size_t)b * kRangeChunks * kBins) + 2 * threadIdx.x;
+    uint4 acc0 = make_uint4(0, 0, 0, 0), acc1 = make_uint4(0, 0, 0, 0);
+#pragma unroll 8
+    for (int c = 0; c < kRangeChunks; ++c) {
+      const uint4 x = src[c * (kBins / 4)], y = src[c * (kBins / 4) + 1];
+      acc0.x += x.x; acc0.y += x.y; acc0.z += x.z; acc0.w += x.w;
+      acc1.x += y.x; acc1.y += y.y; acc1.z += y.z; acc1.w += y.w;
+    }
+    reinterpret_cast<uint4*>(mh)[2 * threadIdx.x] = acc0;
+    reinterpret_cast<uint4*>(mh)[2 * threadIdx.x + 1] = acc1;
+    local = acc0.x + acc0.y + acc0.z + acc0.w + acc1.x + acc1.y + acc1.z + acc1.w;
   }
   if (threadIdx.x == 0) tot = 0;
   __syncthreads();
@@ -1533,15 +1608,6 @@ __global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32
           if (s.wminL[w] == s.wmaxL[w]) { S->tlo[t] = S->thi[t] = s.wminL[w]; } else fail = 1;
         }
       }
-      if (nc > 0) {          // key interval of the compacted bins
-        const VBins vb = level0_vbins(s.rlo, s.rhi);
-        const uint32_t b0 = s.wbin[2 * w] + ((s.wspike[w] & 1u) ? 1u : 0u);
-        const uint32_t b1 = s.wbin[2 * w + 1] - ((s.wspike[w] & 2u) ? 1u : 0u);
-        uint32_t a, z;
-        vbin_interval(b0, vb, s.kmin, s.kmax, clo, z);
-        vbin_interval(b1, vb, s.kmin, s.kmax, a, chi);
-        if (chi < clo) chi = clo;
-      }
     } else {
       nc = 0;
     }
@@ -1554,6 +1620,20 @@ __global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32
   if (c <= (uint32_t)kLdsCand) {
     dma_words(ck, keys, c);
     keys = ck;
+  }
+  // the candidates' key range (the interval cand_select narrows)
+  {
+    uint32_t mn = 0xffffffffu, mx = 0u;
+    for (uint32_t i = threadIdx.x; i < c; i += kBlock) { mn = min(mn, keys[i]); mx = max(mx, keys[i]); }
+    mn = wave_min_u32(mn);
+    mx = wave_max_u32(mx);
+    if ((threadIdx.x & 63) == 0) { rbin[threadIdx.x >> 6] = mn; rrem[threadIdx.x >> 6] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int k = 1; k < kBlock / 64; ++k) { mn = min(mn, rbin[k]); mx = max(mx, rrem[k]); }
+      clo = mn;
+      chi = mx < mn ? mn : mx;
+    }
   }
   __syncthreads();
   cand_select(keys, c, clo, chi, qr, nc, qk, lh, wsum, rbin, rrem, tl, tz, tr);
@@ -2614,24 +2694,36 @@ static int select_level(const Geo& g, SelState* st, uint32_t* hist, uint32_t* ca
 // "sel_windows" (I2PC_SEL_WIN): 1 = the window-only batch selection (k_sweep_w / k_resolve_w),
 // 0 = the histogram levels (the band path's); both exact.
 static thread_local int g_sel_windows = [] { const char* e = getenv("I2PC_SEL_WIN"); return e ? atoi(e) : 1; }();
+// output rows per k_sweep_w workgroup ("sel_rows", I2PC_SEL_ROWS)
+static thread_local int g_sel_rows = [] {
+  const char* e = getenv("I2PC_SEL_ROWS");
+  const int v = e ? atoi(e) : 16;
+  return v > 0 && v <= kMaxSelRows ? v : 16;
+}();
 
 static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, const uint32_t* rpart,
-                         uint32_t cap, int B, const Sweep& sw, hipStream_t s, const Exchange* x = nullptr) {
+                         uint32_t* mhist, uint32_t cap, int B, const Sweep& sw, hipStream_t s,
+                         const Exchange* x = nullptr) {
   // full-resolution sample of ~64 K points per image for the level-0 estimate
   const int stride = std::max(1, (int)std::sqrt((double)g.H * g.W / 65536.0));
   const int ns = ((g.H + stride - 1) / stride) * ((g.W + stride - 1) / stride);
-  hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g, B, st, hist, rpart, stride);
-  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, hist, cap, B, x ? 0 : 1, ns);
+  hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g, B, st, mhist, rpart, stride);
+  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, mhist, cap, B, x ? 0 : 1, ns);
   if (!x && g_sel_windows) {
     // batch path: one window-only sweep + resolve; k_sel_slow finishes (or, for the rare image
-    // a window missed, selects from scratch)
-    const size_t lds = sizeof(uint32_t) * 3 * kSlotWords +
-                       (size_t)sw.lds_rows * (kTileW + (sw.raw ? g.dw : 0)) * sizeof(float);
-    const dim3 grid(B * sw.nrb * sw.ntiles), block(kBlock);
+    // a window missed, selects from scratch).  Sweep workgroup = kSelRows output rows x a
+    // kTileW-column tile (register-streamed model rows, no LDS row window).
+    Sweep sww{};
+    sww.R = g_sel_rows;
+    sww.row0 = sw.row0;
+    sww.row_end = sw.row_end;
+    sww.nrb = std::max(1, (sw.row_end - sw.row0 + sww.R - 1) / sww.R);
+    sww.ntiles = (g.W + kTileW - 1) / kTileW;
+    const dim3 grid(B * sww.nrb * sww.ntiles), block(kBlock);
     if (g.same)
-      hipLaunchKernelGGL((k_sweep_w<true>), grid, block, lds, s, g, st, cand, cap, B, sw);
+      hipLaunchKernelGGL((k_sweep_w<true>), grid, block, 0, s, g, st, cand, cap, B, sww);
     else
-      hipLaunchKernelGGL((k_sweep_w<false>), grid, block, lds, s, g, st, cand, cap, B, sw);
+      hipLaunchKernelGGL((k_sweep_w<false>), grid, block, 0, s, g, st, cand, cap, B, sww);
     hipLaunchKernelGGL(k_resolve_w, dim3(B * 3), dim3(kBlock), 0, s, st, cand, cap, B);
     hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
     return check_launch("select");
@@ -2729,7 +2821,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   Exchange xb = xch ? *xch : Exchange{nullptr, nullptr, nullptr};
   xb.ex = reinterpret_cast<int64_t*>(ws + L.ex);
   uint32_t* cand = reinterpret_cast<uint32_t*>(ws + L.cand);
-  int rc = launch_select(g, st, hist, cand, rpart, L.cap, batch, ssel, s, xch ? &xb : nullptr);
+  int rc = launch_select(g, st, hist, cand, rpart, reinterpret_cast<uint32_t*>(ws + L.mhist), L.cap, batch, ssel, s,
+                         xch ? &xb : nullptr);
   if (rc) return rc;
 
   Cam cam;
@@ -2868,7 +2961,8 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
                      yt, h, w, h, w, 1.0, 1.0, nullptr);
   Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
   const Sweep ssel = plan_select(h, w, h, w, true, 0, h);
-  int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart, L.cap, batch, ssel, s);
+  int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart,
+                         reinterpret_cast<uint32_t*>(ws + L.mhist), L.cap, batch, ssel, s);
   if (rc) return rc;
   const int64_t total = (int64_t)batch * n;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
@@ -2882,5 +2976,9 @@ bool i2pc_unproject_tune(const char* name, int value) {
   if (std::strcmp(name, "unp_nt") == 0) { i2pc::unproj::g_unp_nt = value; return true; }
   if (std::strcmp(name, "unp_rpt") == 0) { i2pc::unproj::g_unp_rpt = value; return true; }
   if (std::strcmp(name, "sel_windows") == 0) { i2pc::unproj::g_sel_windows = value; return true; }
+  if (std::strcmp(name, "sel_rows") == 0) {
+    i2pc::unproj::g_sel_rows = value > 0 && value <= i2pc::unproj::kMaxSelRows ? value : 16;
+    return true;
+  }
   return false;
 }

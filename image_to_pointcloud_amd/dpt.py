@@ -31,6 +31,12 @@ from dataclasses import dataclass, field
 # The head's tail runs as one kernel (ops.head_upconv); False selects the unfused
 # resize -> conv -> head_out sequence (kept for parity tests).
 FUSED_HEAD = True
+# LayerNorm folded through the GEMMs (i2pc.h "LayerNorm fold"): the attention-out / FC2
+# residual epilogues also write the bf16 residual and per-64-column (mean, M2) partials,
+# ln_rowstats turns them into per-row (rstd, -rstd*mean), and QKV / FC1 run on gamma-scaled
+# weights with the normalisation applied in their epilogue -- no separate LayerNorm pass
+# (47 of the 48 in DPT-Large; layer 0's LN1 follows the embeddings).  False: LN kernels.
+LN_FOLD = True
 
 from . import ops
 
@@ -228,14 +234,22 @@ class DPTDepthModel:
             p = f"dpt.encoder.layer.{i}."
             q = [sd[p + f"attention.attention.{n}.weight"] for n in ("query", "key", "value")]
             qb = [sd[p + f"attention.attention.{n}.bias"] for n in ("query", "key", "value")]
-            self.layers.append(dict(
+            L = dict(
                 ln1_g=f32(sd[p + "layernorm_before.weight"]), ln1_b=f32(sd[p + "layernorm_before.bias"]),
                 w_qkv=bf(torch.cat(q, 0)), b_qkv=f32(torch.cat(qb, 0)),
                 w_o=bf(sd[p + "attention.output.dense.weight"]), b_o=f32(sd[p + "attention.output.dense.bias"]),
                 ln2_g=f32(sd[p + "layernorm_after.weight"]), ln2_b=f32(sd[p + "layernorm_after.bias"]),
                 w_1=bf(sd[p + "intermediate.dense.weight"]), b_1=f32(sd[p + "intermediate.dense.bias"]),
                 w_2=bf(sd[p + "output.dense.weight"]), b_2=f32(sd[p + "output.dense.bias"]),
-            ))
+            )
+            # the LN-folded forms: W' = bf16(W * gamma), col_sum = sum_k W', bias' = b + W beta
+            wf, cs, bfold = ops.ln_fold_weights(torch.cat(q, 0), torch.cat(qb, 0), sd[p + "layernorm_before.weight"],
+                                                sd[p + "layernorm_before.bias"])
+            L.update(w_qkv_f=wf.to(dev), s_qkv=cs.to(dev), b_qkv_f=bfold.to(dev))
+            wf, cs, bfold = ops.ln_fold_weights(sd[p + "intermediate.dense.weight"], sd[p + "intermediate.dense.bias"],
+                                                sd[p + "layernorm_after.weight"], sd[p + "layernorm_after.bias"])
+            L.update(w_1_f=wf.to(dev), s_1=cs.to(dev), b_1_f=bfold.to(dev))
+            self.layers.append(L)
         self.stages = []
         for i, (c, fac) in enumerate(zip(spec.neck, spec.factors)):
             p = f"neck.reassemble_stage."
@@ -300,9 +314,34 @@ class DPTDepthModel:
         M = B * T
         e = lambda shape, dt=torch.bfloat16: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
         b = dict(x=e((M, D), torch.float32), ln=e((M, D)), qkv=e((M, 3 * D)), att=e((M, D)), mlp=e((M, s.mlp)),
-                 hs=[e((M, D)) for _ in s.out_indices], rb=e((B, D), torch.float32), tok=e((B * gh * gw, D)))
+                 hs=[e((M, D)) for _ in s.out_indices], rb=e((B, D), torch.float32), tok=e((B * gh * gw, D)),
+                 part=e((M, D // 64, 2), torch.float32), rs=e((M, 2), torch.float32))
+        b["ln_fold"] = LN_FOLD and D % 64 == 0 and self._ln_fold_ok(b, M)
         self._bufs[(B, gh, gw)] = b
         return b
+
+    def _ln_fold_ok(self, b, M) -> bool:
+        """Whether libi2pc.so runs the LN-folded calls at this batch (asked of the C side:
+        i2pc_gemm_kernel_name is "invalid" for a descriptor i2pc_gemm would reject)."""
+        s, L = self.spec, self.layers[0]
+        D = s.hidden
+
+        def name(x, w, out, **kw):
+            d = ops.GemmDesc()
+            d.a, d.lda, d.m, d.n, d.k = x.data_ptr(), x.stride(0), M, w.shape[0], w.shape[1]
+            d.w, d.ldw, d.c, d.ldc = w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0)
+            d.c_f32 = int(out.dtype.is_floating_point and out.element_size() == 4)
+            for k, v in kw.items():
+                setattr(d, k, v)
+            return ops.gemm_kernel_label(d)
+        consumer = dict(ln_rows=b["rs"].data_ptr(), col_sum=L["s_qkv"].data_ptr(), bias=L["b_qkv_f"].data_ptr())
+        producer = dict(res=b["x"].data_ptr(), res_f32=1, ldr=D, ln_part=b["part"].data_ptr(),
+                        c_bf16=b["ln"].data_ptr(), ldc_bf16=D)
+        names = [name(b["ln"], L["w_qkv_f"], b["qkv"], **consumer),
+                 name(b["ln"], L["w_1_f"], b["mlp"], **dict(consumer, col_sum=L["s_1"].data_ptr(), act=1)),
+                 name(b["att"], L["w_o"], b["x"], **producer),
+                 name(b["mlp"], L["w_2"], b["x"], **producer)]
+        return "invalid" not in names
 
     # ------------------------------------------------------------------ forward
     def forward(self, patches, B: int, gh: int = None, gw: int = None):
@@ -322,17 +361,42 @@ class DPTDepthModel:
         ops.cls_pos(self.cls, self.pos0, x, B, T, D)
         scale = 1.0 / math.sqrt(D // s.heads)
         hs_i = 0
+        fold = buf["ln_fold"]
+        a_in = None          # LN fold: the bf16 residual rows the previous FC2 wrote (rows scaled by buf["rs"])
+        nl = len(self.layers)
         for i, L in enumerate(self.layers):
-            ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
-            qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
+            if not fold:
+                ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
+                qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
+                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+                ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
+                ln = ops.layernorm(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])
+                h = ops.linear(ln, L["w_1"], bias=L["b_1"], act="gelu", out=buf["mlp"])
+                ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x)
+                if i in s.out_indices:
+                    ops.f32_to_bf16(x, out=buf["hs"][hs_i])
+                    hs_i += 1
+                continue
+            if a_in is None:      # layer 0: LN1 of the embeddings
+                ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
+                qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
+            else:
+                qkv = ops.linear(a_in, L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
+                                 out=buf["qkv"])
             att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
-            ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
-            ln = ops.layernorm(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])
-            h = ops.linear(ln, L["w_1"], bias=L["b_1"], act="gelu", out=buf["mlp"])
-            ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x)
+            ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x, ln_part=buf["part"], out_bf16=buf["ln"])
+            ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"])
+            h = ops.linear(buf["ln"], L["w_1_f"], bias=L["b_1_f"], act="gelu", ln_rows=buf["rs"], col_sum=L["s_1"],
+                           out=buf["mlp"])
+            # FC2 + residual; its bf16 copy is the next QKV's A, or a kept hidden state (neck input)
+            dst = buf["ln"]
             if i in s.out_indices:
-                ops.f32_to_bf16(x, out=buf["hs"][hs_i])
+                dst = buf["hs"][hs_i]
                 hs_i += 1
+            ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x, ln_part=buf["part"], out_bf16=dst)
+            if i + 1 < nl:
+                ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"])
+            a_in = dst
         feats = [self._reassemble(j, buf["hs"][j], B, buf) for j in range(len(self.stages))]
         hidden = None
         for j, feat in enumerate(reversed(feats)):

@@ -34,6 +34,8 @@ class GemmDesc(ctypes.Structure):
         ("c", c_void_p), ("c_f32", c_int32), ("ldc", c_int64),
         ("out_group", c_int32), ("out_group_stride", c_int32), ("out_offset", c_int32),
         ("convt_s", c_int32), ("convt_h", c_int32), ("convt_w", c_int32), ("convt_c", c_int32),
+        ("ln_rows", c_void_p), ("col_sum", c_void_p), ("ln_part", c_void_p), ("c_bf16", c_void_p),
+        ("ldc_bf16", c_int64),
     ]
 
 
@@ -43,6 +45,8 @@ _lib.register("i2pc_gemm_workspace_bytes", ctypes.c_size_t, [ctypes.POINTER(Gemm
 _lib.register("i2pc_gemm_kernel_name", ctypes.c_char_p, [ctypes.POINTER(GemmDesc)])
 _lib.register("i2pc_gemm_set_engine", ctypes.c_int, [ctypes.c_int])
 _lib.register("i2pc_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
+_lib.register("i2pc_ln_rowstats", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, c_void_p,
+                                                 c_void_p])
 _lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
                                                ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_attention", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -144,6 +148,10 @@ def gemm_bytes(d: GemmDesc, esz: float = 2.0, c_esz: float = None) -> float:
         b += M * N * (4.0 if d.res_f32 else 2.0)
     if d.res2:
         b += M * N * 2.0
+    if d.ln_part:          # LN-fold producer: the bf16 copy + chunk partials
+        b += M * N * 2.0 + M * (N // 64) * 8.0
+    if d.ln_rows:          # LN-fold consumer: row scales + column sums
+        b += M * 8.0 + N * 4.0
     return b
 
 
@@ -161,11 +169,14 @@ def gemm(desc: GemmDesc) -> None:
 
 def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=False,
            a_map=(0, 0, 0), out_map=(0, 0, 0), rows=None, row_bias=None, row_bias_group=1,
-           table=None, table_rows=1, ldc=None):
+           table=None, table_rows=1, ldc=None, ln_rows=None, col_sum=None, ln_part=None, out_bf16=None):
     """out = act(x @ w.T + bias + row_bias + table) + res + res2.
 
     x: bf16 [*, K] (row stride x.stride(0)); w: bf16 [N, K]; rows = M (defaults to x rows).
     a_map / out_map = (group, group_stride, offset) row remaps (see i2pc.h).
+    LayerNorm fold (i2pc.h): ln_rows fp32 [M, 2] (ln_rowstats) + col_sum fp32 [N] make this the
+    consumer (out = act(rs.x * acc + rs.y * col_sum + bias)); ln_part fp32 [M, N / 64, 2] +
+    out_bf16 bf16 [M, N] make an fp32-output call the producer.
     """
     torch = _torch()
     _check(x, torch.bfloat16, "x")
@@ -189,8 +200,42 @@ def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=Fal
     d.c, d.c_f32 = _p(out), int(out.dtype == torch.float32)
     d.ldc = ldc if ldc is not None else out.stride(0)
     d.out_group, d.out_group_stride, d.out_offset = out_map
+    if ln_rows is not None:
+        _check(ln_rows, torch.float32, "ln_rows")
+        _check(col_sum, torch.float32, "col_sum")
+        d.ln_rows, d.col_sum = _p(ln_rows), _p(col_sum)
+    if ln_part is not None:
+        _check(ln_part, torch.float32, "ln_part")
+        _check(out_bf16, torch.bfloat16, "out_bf16")
+        if ln_part.numel() < 2 * M * (N // 64) or out_bf16.shape[0] < M or out_bf16.shape[-1] < N:
+            raise ValueError("ln_part / out_bf16 too small for the call")
+        d.ln_part, d.c_bf16, d.ldc_bf16 = _p(ln_part), _p(out_bf16), out_bf16.stride(0)
     gemm(d)
     return out
+
+
+def ln_rowstats(part, eps, out=None):
+    """LayerNorm row statistics from producer partials: part fp32 [M, P, 2] -> out fp32 [M, 2] =
+    (rstd, -rstd * mean) (i2pc_ln_rowstats)."""
+    torch = _torch()
+    _check(part, torch.float32, "part")
+    M, P = part.shape[0], part.shape[1]
+    if out is None:
+        out = torch.empty((M, 2), dtype=torch.float32, device=part.device)
+    with _Timed("k_ln_rowstats", 0.0, M * (P * 8.0 + 8.0)):
+        _lib.call("i2pc_ln_rowstats", _p(part), M, P, float(eps), _p(out), _stream())
+    return out
+
+
+def ln_fold_weights(w, b, gamma, beta):
+    """Weights of a LayerNorm-folded linear (i2pc.h): W' = bf16(W * gamma) [N, K], col_sum[n] =
+    sum_k W'[n][k] (fp32, of the bf16 values the GEMM multiplies), bias' = b + W beta (fp32)."""
+    torch = _torch()
+    w32 = w.to(torch.float32)
+    wg = (w32 * gamma.to(torch.float32)[None, :]).to(torch.bfloat16)
+    col = wg.to(torch.float64).sum(1).to(torch.float32)
+    bias = (b.to(torch.float64) + w32.to(torch.float64) @ beta.to(torch.float64)).to(torch.float32)
+    return wg.contiguous(), col.contiguous(), bias.contiguous()
 
 
 def conv2d(x, w, bias=None, k=3, stride=1, pad=1, relu_in=False, act=None, res=None, res2=None, out=None,

@@ -209,7 +209,26 @@ typedef struct i2pc_gemm_desc {
   void* c; int32_t c_f32; int64_t ldc;
   int32_t out_group, out_group_stride, out_offset;
   int32_t convt_s, convt_h, convt_w, convt_c;
+  /* LayerNorm folded through the GEMM (nn.LayerNorm before a linear layer, modeling_dpt.py:233-234,
+   * 376-381; NULL = off).
+   * Producer (fp32 output rows, e.g. the residual-add epilogue of attention-out / FC2): with
+   *   ln_part set it also writes c_bf16 [m][ldc_bf16] = bf16(out) and, per output row and 64-column
+   *   chunk, ln_part float2 [m][n / 64] = (mean, sum of squared deviations from it) of that chunk of
+   *   out.  Needs n % 64 == 0, c_f32, no row remap / ConvTranspose store (EUNSUPPORTED where the
+   *   chosen kernel cannot: i2pc_gemm_kernel_name says "invalid").
+   * Consumer (A = the producer's c_bf16, W = W * gamma[k] in bf16): with ln_rows set the epilogue
+   *   computes act(rs.x * acc + rs.y * col_sum[n] + bias[n]) with rs = ln_rows float2 [m] =
+   *   (rstd, -rstd * mean) (i2pc_ln_rowstats), col_sum fp32 [n] = sum_k of W's bf16 row, bias =
+   *   b + W beta: the LayerNorm of A's rows applied after the product.  Dense A, bf16 output, no
+   *   residuals / row bias / table (the persistent engine runs it). */
+  const float* ln_rows; const float* col_sum;
+  float* ln_part; void* c_bf16; int64_t ldc_bf16;
 } i2pc_gemm_desc;
+
+/* LayerNorm row statistics from i2pc_gemm's producer partials: rows_out float2 [rows] =
+ * (rstd, -rstd * mean) of each row's `parts` 64-column chunks (part float2 [rows][parts]), the
+ * chunks combined by Chan's formula; biased variance, rstd = 1 / sqrt(var + eps) (nn.LayerNorm). */
+int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out, void* stream);
 
 int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
 

@@ -58,16 +58,22 @@ def test_depth_anything_matches_transformers_fp32(which, B, hw):
     patches = prep(timgs, layout="patches")
     depth = ours(patches, B, gh, gw)
     torch.cuda.synchronize()
+    import copy
     with torch.no_grad():
         exp = ref(pixel_values=pix).predicted_depth.float()
+        # control: transformers' own bf16 forward of the same weights against its fp32 forward
+        ctl = copy.deepcopy(ref).to(torch.bfloat16)(pixel_values=pix.to(torch.bfloat16)).predicted_depth.float()
+    control = ((ctl - exp).norm() / exp.norm()).item()
     assert depth.shape == exp.shape, (depth.shape, exp.shape)
     err = depth - exp
     rel = (err.norm() / exp.norm()).item()
     mx = (err.abs().max() / exp.abs().max()).item()
     assert exp.abs().max() > 0 and exp.std() > 1e-3 * exp.abs().max(), "degenerate reference depth"
     from test_dpt_gpu import _report
-    _report(f"depth-anything-v2 {tuple(depth.shape)}", rel_l2=rel, max_rel=mx)
-    assert rel <= 1e-2 and mx <= 4e-2, f"rel L2 {rel:.3e} max {mx:.3e}"
+    _report(f"depth-anything-v2 {tuple(depth.shape)}", rel_l2=rel, max_rel=mx, torch_bf16_control=control)
+    # measured r02: 0.19-0.28 % -> half of SURVEY 8c's 1e-2, or 1.5x the torch bf16 control
+    bound = max(5e-3, 1.5 * control)
+    assert rel <= bound and mx <= 4e-2, f"rel L2 {rel:.3e} max {mx:.3e} (torch bf16 control {control:.3e})"
 
 
 @pytest.mark.parametrize("B,h,w,c,oh,ow,ac", [(2, 19, 19, 64, 37, 37, True), (1, 296, 296, 64, 518, 518, True),

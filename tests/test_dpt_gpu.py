@@ -2,9 +2,10 @@
 
 Same seeded weights (transformers key layout), same preprocessed input.
 Tolerance (bf16 operands / fp32 accumulation vs an fp32 network): relative L2
-error of the predicted depth <= 1e-2 (SURVEY §8c's bound) and max |err| <= 4e-2 * max |ref| for
-the tiny config; the 24-layer DPT-Large accumulates more bf16 rounding (measured r02: rel L2
-0.97e-2 at 384^2 and 1.12e-2 at 1024^2 input, max 1.6-1.8e-2), so its bound is rel L2 <= 1.5e-2.
+error of the predicted depth <= max(1e-2, 1.5 x control) and max |err| <= 4e-2 * max |ref|, where
+the control is transformers' OWN bf16 forward of the same weights against its fp32 forward (what
+plain bf16 arithmetic moves this network; measured r02 without it: rel L2 0.97e-2 at 384^2 and
+1.12e-2 at 1024^2 input).
 Every case prints the error it reached.  The preprocessing itself is checked bit-exact against
 DPTImageProcessorPil.
 
@@ -76,16 +77,22 @@ def test_dpt_forward_matches_transformers_fp32(which, B, hw):
     patches = prep(timgs, layout="patches")
     depth = ours(patches, B)
     torch.cuda.synchronize()
+    import copy
     with torch.no_grad():
         exp = ref(pixel_values=pix).predicted_depth.float()
+        # control: transformers' OWN forward in bf16 on the same weights -- how far plain bf16
+        # arithmetic moves this network from its fp32 forward
+        ctl = copy.deepcopy(ref).to(torch.bfloat16)(pixel_values=pix.to(torch.bfloat16)).predicted_depth.float()
+    control = ((ctl - exp).norm() / exp.norm()).item()
     assert depth.shape == exp.shape
     err = (depth - exp)
     rel = (err.norm() / exp.norm()).item()
     mx = (err.abs().max() / exp.abs().max()).item()
     assert exp.abs().max() > 0 and exp.std() > 1e-3 * exp.abs().max(), "degenerate reference depth"
-    _report(f"dpt-{which} B={B} {hw[0]}x{hw[1]}", rel_l2=rel, max_rel=mx)
-    bound = 1.5e-2 if which == "large" else 1e-2
-    assert rel <= bound and mx <= 4e-2, f"rel L2 {rel:.3e} max {mx:.3e}"
+    _report(f"dpt-{which} B={B} {hw[0]}x{hw[1]}", rel_l2=rel, max_rel=mx, torch_bf16_control=control)
+    # SURVEY 8c's 1e-2, or 1.5x what torch's own bf16 forward of these weights reaches
+    bound = max(1e-2, 1.5 * control)
+    assert rel <= bound and mx <= 4e-2, f"rel L2 {rel:.3e} max {mx:.3e} (torch bf16 control {control:.3e})"
 
 
 def _report(case, **vals):

@@ -1,0 +1,139 @@
+"""The LayerNorm fold of the DPT encoder (include/i2pc.h "LayerNorm fold"; nn.LayerNorm before
+the QKV and FC1 linears, transformers modeling_dpt.py:233-234 / 376-381):
+
+  producer  attention-out / FC2 with the fp32 residual: the fp32 output is unchanged bit for bit,
+            the bf16 copy is exactly bf16(out), the per-64-column (mean, M2) partials match fp64
+  rowstats  (rstd, -rstd * mean) per row == nn.LayerNorm's statistics (fp64 reference, 1e-5)
+  consumer  act(rstd * (x_bf16 @ (W gamma)^T) - rstd * mean * colsum + b + W beta) against the
+            fp64 LayerNorm + linear of the same fp32 rows: relative L2 within 1e-2 (bf16 output),
+            also for rows whose mean is 10x their spread (the cancellation case), and no worse
+            than 1.5x the unfused LN-kernel + GEMM path on the same data.
+"""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from image_to_pointcloud_amd import ops
+    return ops
+
+
+def _rand(shape, g, scale=1.0):
+    return ((torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1) * scale)
+
+
+@pytest.mark.parametrize("M,N,K", [(18464, 1024, 1024), (18464, 1024, 4096), (1000, 1024, 1024)])
+def test_producer_outputs(M, N, K):
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M + K)
+    a = _rand((M, K), g).to(torch.bfloat16).to(dev)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = _rand((N,), g, 0.1).to(torch.float32).to(dev)
+    x0 = (_rand((M, N), g) + 0.5).to(torch.float32).to(dev)
+    y_ref = x0.clone()
+    ops.linear(a, w, bias=b, res=y_ref, out=y_ref)
+    y = x0.clone()
+    part = torch.empty((M, N // 64, 2), dtype=torch.float32, device=dev)
+    yb = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    ops.linear(a, w, bias=b, res=y, out=y, ln_part=part, out_bf16=yb)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref), "fp32 output changed by the LN-fold producer"
+    assert torch.equal(yb, y.to(torch.bfloat16)), "bf16 copy is not bf16(out)"
+    yc = y.double().view(M, N // 64, 64)
+    mean = yc.mean(-1)
+    m2 = ((yc - mean[..., None]) ** 2).sum(-1)
+    p = part.double()
+    assert torch.allclose(p[..., 0], mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(p[..., 1], m2, rtol=1e-4, atol=1e-5)
+
+
+def test_rowstats_match_layernorm_statistics():
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(5)
+    M, N = 4096, 1024
+    x = (_rand((M, N), g) * torch.linspace(0.1, 3.0, M, dtype=torch.float64)[:, None]
+         + torch.linspace(-20, 20, M, dtype=torch.float64)[:, None])
+    xc = x.view(M, N // 64, 64)
+    mean_c = xc.mean(-1)
+    part = torch.stack([mean_c, ((xc - mean_c[..., None]) ** 2).sum(-1)], -1).to(torch.float32).to(dev)
+    rs = ops.ln_rowstats(part, 1e-12)
+    torch.cuda.synchronize()
+    mean = x.mean(1)
+    rstd = 1.0 / torch.sqrt(x.var(1, unbiased=False) + 1e-12)
+    got = rs.double().cpu()
+    assert torch.allclose(got[:, 0], rstd, rtol=1e-5)
+    assert torch.allclose(got[:, 1], -rstd * mean, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,act,offset", [(18464, 3072, None, 0.0), (18464, 4096, "gelu", 0.0),
+                                            (1000, 3072, None, 0.0), (2000, 1024, "gelu", 10.0)])
+def test_consumer_matches_layernorm_linear(M, N, act, offset):
+    ops = _ops()
+    dev = torch.device("cuda")
+    K = 1024
+    g = torch.Generator().manual_seed(N + M)
+    x = (_rand((M, K), g) + offset + _rand((M, 1), g)).to(torch.float32)
+    gamma = (1.0 + _rand((K,), g, 0.2)).to(torch.float32)
+    beta = _rand((K,), g, 0.1).to(torch.float32)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.float32)
+    b = _rand((N,), g, 0.1).to(torch.float32)
+    # fp64 reference: nn.LayerNorm then the linear (then GELU)
+    ln = torch.nn.functional.layer_norm(x.double(), (K,), gamma.double(), beta.double(), 1e-12)
+    ref = ln @ w.double().T + b.double()
+    if act == "gelu":
+        ref = torch.nn.functional.gelu(ref)
+    # fused: producer-style statistics from the fp32 rows, bf16 rows as A
+    xd = x.to(dev)
+    xc = xd.double().view(M, K // 64, 64)
+    mean_c = xc.mean(-1)
+    part = torch.stack([mean_c, ((xc - mean_c[..., None]) ** 2).sum(-1)], -1).to(torch.float32)
+    rs = ops.ln_rowstats(part, 1e-12)
+    wf, cs, bf = ops.ln_fold_weights(w, b, gamma, beta)
+    out = ops.linear(xd.to(torch.bfloat16), wf.to(dev), bias=bf.to(dev), act=act, ln_rows=rs, col_sum=cs.to(dev))
+    # unfused: the LayerNorm kernel, then the plain GEMM
+    lnk = ops.layernorm(xd, gamma.to(dev), beta.to(dev), 1e-12)
+    out_u = ops.linear(lnk, w.to(torch.bfloat16).to(dev), bias=b.to(dev), act=act)
+    torch.cuda.synchronize()
+    refd = ref.to(dev)
+    rel = ((out.double() - refd).norm() / refd.norm()).item()
+    rel_u = ((out_u.double() - refd).norm() / refd.norm()).item()
+    from test_dpt_gpu import _report
+    _report(f"ln-fold consumer M={M} N={N} act={act} offset={offset}", rel_l2=rel, unfused_rel_l2=rel_u)
+    assert rel <= 1e-2, rel
+    assert rel <= max(1.5 * rel_u, 5e-3), (rel, rel_u)
+
+
+def test_dpt_large_ln_fold_matches_unfused_forward():
+    """The whole DPT-Large encoder with and without the fold on the same input: depth within the
+    bf16 noise of each other (both are checked against transformers fp32 in test_dpt_gpu.py)."""
+    from image_to_pointcloud_amd import dpt
+    from image_to_pointcloud_amd.dpt import DPT_LARGE, DPTDepthModel, synthetic_state_dict
+    dev = torch.device("cuda")
+    model = DPTDepthModel(DPT_LARGE, synthetic_state_dict(DPT_LARGE, 0), dev)
+    B = 2
+    g = torch.Generator().manual_seed(3)
+    patches = torch.randn((B * 24 * 24, 768), generator=g).to(torch.bfloat16).to(dev)
+    old = dpt.LN_FOLD
+    try:
+        dpt.LN_FOLD = True
+        model._bufs.clear()
+        d1 = model(patches, B).clone()
+        assert model.buffers(B)["ln_fold"], "LN fold not taken at DPT-Large"
+        dpt.LN_FOLD = False
+        model._bufs.clear()
+        d0 = model(patches, B).clone()
+    finally:
+        dpt.LN_FOLD = old
+        model._bufs.clear()
+    torch.cuda.synchronize()
+    rel = ((d1 - d0).norm() / d0.norm()).item()
+    from test_dpt_gpu import _report
+    _report("dpt-large ln-fold vs LN kernels", rel_l2=rel)
+    assert rel <= 1e-2, rel

@@ -97,6 +97,14 @@ case "$TASK" in
   census)
     timeout -k 10 300 python -u tools/gemm_census.py "$@" > gpurun_out/census.txt 2>&1; rc=$?
     grep -v amdgpu.ids gpurun_out/census.txt; exit $rc ;;
+  gemmdiag)   # census of the C2 network + per-tile s_memtime stamps of the transformer GEMMs (stamps lib prebuilt)
+    timeout -k 10 300 python -u tools/gemm_census.py > gpurun_out/census.txt 2>&1 || { tail -5 gpurun_out/census.txt; exit 1; }
+    head -30 gpurun_out/census.txt
+    for shp in "18464 3072 1024" "18464 4096 1024 gelu" "18464 1024 1024" "18464 1024 4096"; do
+      I2PC_GEMM_P=2 I2PC_LIB=image_to_pointcloud_amd/libi2pc_stamps.so timeout -k 10 120 python -u tools/stamps_p.py $shp \
+        >> gpurun_out/stamps.txt 2>&1 || { tail -5 gpurun_out/stamps.txt; exit 1; }
+    done
+    cat gpurun_out/stamps.txt ;;
   ab-gemm)
     timeout -k 10 300 python -u -m pytest tests/test_gemm_engines_gpu.py -x -q --timeout 120 --timeout-method thread \
       > gpurun_out/eng.log 2>&1 || { tail -15 gpurun_out/eng.log; exit 1; }
