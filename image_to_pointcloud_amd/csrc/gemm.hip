@@ -89,6 +89,7 @@ struct Args {
   // partials float2 [M][N / 64] + the bf16 copy of the fp32 output
   const float* lnr; const float* csum;
   float* lnp; bf16_t* cbf; int64_t ldcb;
+  const float* lnsh;
 };
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
@@ -267,21 +268,26 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
       if constexpr (LPR % 8 == 0) {
         if (p.lnp) {
-          // LayerNorm producer: the bf16 copy, and (mean, M2) of each 64-column chunk = 8 lanes
+          // LayerNorm producer: the bf16 copy of out - shift[m], and (mean, M2) of each 64-column
+          // chunk (= 8 lanes) of it
+          const float shf = p.lnsh ? p.lnsh[m] : 0.f;
+          float u[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) u[t] = v[t] - shf;
           uint4 o;
-          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-          o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          o.x = (uint32_t)f2bf(u[0]) | ((uint32_t)f2bf(u[1]) << 16);
+          o.y = (uint32_t)f2bf(u[2]) | ((uint32_t)f2bf(u[3]) << 16);
+          o.z = (uint32_t)f2bf(u[4]) | ((uint32_t)f2bf(u[5]) << 16);
+          o.w = (uint32_t)f2bf(u[6]) | ((uint32_t)f2bf(u[7]) << 16);
           *reinterpret_cast<uint4*>(p.cbf + (int64_t)m * p.ldcb + n) = o;
-          float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+          float sm = ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
           sm += __shfl_xor(sm, 1);
           sm += __shfl_xor(sm, 2);
           sm += __shfl_xor(sm, 4);
           const float mean = sm * (1.0f / 64.0f);
           float q = 0.f;
 #pragma unroll
-          for (int t = 0; t < 8; ++t) q = __builtin_fmaf(v[t] - mean, v[t] - mean, q);
+          for (int t = 0; t < 8; ++t) q = __builtin_fmaf(u[t] - mean, u[t] - mean, q);
           q += __shfl_xor(q, 1);
           q += __shfl_xor(q, 2);
           q += __shfl_xor(q, 4);
@@ -2129,6 +2135,7 @@ static int make_args(const i2pc_gemm_desc* d, gemm::Args& p) {
   p.ct_s = d->convt_s; p.ct_h = d->convt_h; p.ct_w = d->convt_w; p.ct_c = d->convt_c;
   p.lnr = d->ln_rows; p.csum = d->col_sum;
   p.lnp = d->ln_part; p.cbf = static_cast<gemm::bf16_t*>(d->c_bf16); p.ldcb = d->ldc_bf16;
+  p.lnsh = d->ln_part ? d->ln_shift : nullptr;
   if (d->ln_rows) I2PC_REQUIRE(d->col_sum, "gemm: ln_rows needs col_sum");
   if (d->ln_part) {
     I2PC_REQUIRE(d->c_bf16 && d->c_f32 && d->n % 64 == 0 && d->ldc_bf16 % 8 == 0 && d->ldc_bf16 >= d->n,

@@ -28,7 +28,8 @@ __device__ __forceinline__ float wave_sum(float x) {
 template <int V>
 __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, int64_t ldx,
                                                    const float* __restrict__ g, const float* __restrict__ b,
-                                                   float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy) {
+                                                   float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy,
+                                                   float* __restrict__ mean_out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -41,6 +42,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
     s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
   }
   const float mean = wave_sum(s) / (float)dim;
+  if (mean_out && lane == 0) mean_out[row] = mean;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < V; ++i) {
@@ -68,7 +70,8 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
 template <int V>
 __global__ __launch_bounds__(256) void k_layernorm2(const float* __restrict__ x, int64_t ldx,
                                                     const float* __restrict__ g, const float* __restrict__ b,
-                                                    float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy) {
+                                                    float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy,
+                                                   float* __restrict__ mean_out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -80,6 +83,7 @@ __global__ __launch_bounds__(256) void k_layernorm2(const float* __restrict__ x,
 #pragma unroll
   for (int i = 0; i < V; ++i) s += v[i].x + v[i].y;
   const float mean = wave_sum(s) / (float)dim;
+  if (mean_out && lane == 0) mean_out[row] = mean;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < V; ++i) {
@@ -100,7 +104,8 @@ __global__ __launch_bounds__(256) void k_layernorm2(const float* __restrict__ x,
 // generic row width (dim % 64 == 0, dim <= 2048): E scalars per lane, stride 64 (coalesced)
 __global__ __launch_bounds__(256) void k_layernorm_any(const float* __restrict__ x, int64_t ldx,
                                                        const float* __restrict__ g, const float* __restrict__ b,
-                                                       float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy) {
+                                                       float eps, int rows, int dim, bf16_t* __restrict__ y, int64_t ldy,
+                                                   float* __restrict__ mean_out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -114,6 +119,7 @@ __global__ __launch_bounds__(256) void k_layernorm_any(const float* __restrict__
     s += v[i];
   }
   const float mean = wave_sum(s) / (float)dim;
+  if (mean_out && lane == 0) mean_out[row] = mean;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < 32; ++i)
@@ -226,30 +232,44 @@ __global__ __launch_bounds__(256) void k_head_out(const bf16_t* __restrict__ x, 
 }
 
 // LayerNorm row statistics from the 64-column chunk partials an i2pc_gemm producer epilogue
-// wrote ((mean, M2) per chunk): Chan's pairwise-free combination for equal chunk counts,
+// wrote ((mean, M2) per chunk of out - shift): Chan's combination for equal chunk counts,
 // mean = avg(mean_c), M2 = sum M2_c + 64 sum (mean_c - mean)^2, var = M2 / (64 P) (biased, as
-// nn.LayerNorm), out = (rstd, -rstd * mean).  One thread per row, all its partials in flight.
-__global__ __launch_bounds__(256) void k_ln_rowstats(const float4* __restrict__ part, int rows, int P, float eps,
-                                                     float2* __restrict__ out) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  const float4* q = part + (int64_t)r * (P / 2);
-  float mu[64], m2[64];
-#pragma unroll 8
-  for (int i = 0; i < P / 2; ++i) {
-    const float4 v = q[i];
-    mu[2 * i] = v.x; m2[2 * i] = v.y; mu[2 * i + 1] = v.z; m2[2 * i + 1] = v.w;
-  }
+// nn.LayerNorm), out = (rstd, -rstd * mean), shift_out = shift_in + mean.  16 lanes per row (coalesced 8-byte
+// partials, partial c on lane c % 16), 16 rows per 256-thread block.
+__global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ part, int rows, int P, float eps,
+                                                     float2* __restrict__ out, const float* shift_in,
+                                                     float* shift_out) {
+  const int r = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int l = threadIdx.x & 15;
+  const bool ok = r < rows;
+  const float2* q = part + (int64_t)(ok ? r : 0) * P;
+  float2 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (l + 16 * j < P) ? q[l + 16 * j] : make_float2(0.f, 0.f);
   float sm = 0.f;
-  for (int i = 0; i < P; ++i) sm += mu[i];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sm += v[j].x;
+  sm += __shfl_xor(sm, 1);
+  sm += __shfl_xor(sm, 2);
+  sm += __shfl_xor(sm, 4);
+  sm += __shfl_xor(sm, 8);
   const float mean = sm / (float)P;
-  float M2 = 0.f;
-  for (int i = 0; i < P; ++i) {
-    const float d = mu[i] - mean;
-    M2 += m2[i] + 64.0f * d * d;
+  float m2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (l + 16 * j < P) {
+      const float d = v[j].x - mean;
+      m2 += v[j].y + 64.0f * d * d;
+    }
+  m2 += __shfl_xor(m2, 1);
+  m2 += __shfl_xor(m2, 2);
+  m2 += __shfl_xor(m2, 4);
+  m2 += __shfl_xor(m2, 8);
+  if (ok && l == 0) {
+    const float rstd = 1.0f / sqrtf(m2 / (float)(64 * P) + eps);
+    out[r] = make_float2(rstd, -rstd * mean);
+    if (shift_out) shift_out[r] = (shift_in ? shift_in[r] : 0.f) + mean;
   }
-  const float rstd = 1.0f / sqrtf(M2 / (float)(64 * P) + eps);
-  out[r] = make_float2(rstd, -rstd * mean);
 }
 
 static int grid_for(int64_t work, int per_block = 256) {
@@ -269,19 +289,35 @@ bool i2pc_misc_tune(const char* name, int value) {
   return false;
 }
 
-extern "C" int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out, void* stream) {
+extern "C" int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out,
+                                const float* shift_in, float* shift_out, void* stream) {
   clear_error();
   I2PC_REQUIRE(part && rows_out, "NULL pointer");
-  I2PC_REQUIRE(rows > 0 && parts >= 2 && parts <= 64 && parts % 2 == 0, "ln_rowstats: parts=%d must be even, 2..64",
-               parts);
-  hipLaunchKernelGGL(k_ln_rowstats, dim3((rows + 255) / 256), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<const float4*>(part), rows, parts, eps, reinterpret_cast<float2*>(rows_out));
+  I2PC_REQUIRE(rows > 0 && parts >= 1 && parts <= 64, "ln_rowstats: parts=%d must be 1..64", parts);
+  hipLaunchKernelGGL(k_ln_rowstats, dim3((rows + 15) / 16), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float2*>(part), rows, parts, eps, reinterpret_cast<float2*>(rows_out), shift_in,
+                     shift_out);
   return check_launch("ln_rowstats");
 }
+
+static int layernorm_impl(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps, int rows,
+                          int dim, void* y, int64_t ldy, float* mean_out, void* stream);
 
 extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
                               int rows, int dim, void* y, int64_t ldy, void* stream) {
   clear_error();
+  return layernorm_impl(x, ldx, gamma, beta, eps, rows, dim, y, ldy, nullptr, stream);
+}
+
+extern "C" int i2pc_layernorm_stats(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
+                                    int rows, int dim, void* y, int64_t ldy, float* row_mean, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(row_mean, "layernorm_stats: NULL row_mean");
+  return layernorm_impl(x, ldx, gamma, beta, eps, rows, dim, y, ldy, row_mean, stream);
+}
+
+static int layernorm_impl(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps, int rows,
+                          int dim, void* y, int64_t ldy, float* mean_out, void* stream) {
   I2PC_REQUIRE(x && gamma && beta && y, "NULL pointer");
   I2PC_REQUIRE(rows > 0 && dim > 0 && dim % 64 == 0 && dim <= 2048, "layernorm: dim=%d must be a multiple of 64 <= 2048", dim);
   I2PC_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "layernorm: row strides must be multiples of 4");
@@ -289,22 +325,22 @@ extern "C" int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, c
   const dim3 grid((rows + 3) / 4), block(256);
   bf16_t* yy = static_cast<bf16_t*>(y);
   if (dim == 384 && g_ln2) {
-    hipLaunchKernelGGL(k_layernorm2<3>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy);
+    hipLaunchKernelGGL(k_layernorm2<3>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out);
     return check_launch("layernorm");
   }
   if (dim % 256 != 0) {
-    hipLaunchKernelGGL(k_layernorm_any, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy);
+    hipLaunchKernelGGL(k_layernorm_any, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out);
     return check_launch("layernorm");
   }
   switch (dim / 256) {
-    case 1: hipLaunchKernelGGL(k_layernorm<1>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
-    case 2: hipLaunchKernelGGL(k_layernorm<2>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
-    case 3: hipLaunchKernelGGL(k_layernorm<3>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
-    case 4: hipLaunchKernelGGL(k_layernorm<4>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
-    case 5: hipLaunchKernelGGL(k_layernorm<5>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
-    case 6: hipLaunchKernelGGL(k_layernorm<6>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
-    case 7: hipLaunchKernelGGL(k_layernorm<7>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
-    case 8: hipLaunchKernelGGL(k_layernorm<8>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy); break;
+    case 1: hipLaunchKernelGGL(k_layernorm<1>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
+    case 2: hipLaunchKernelGGL(k_layernorm<2>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
+    case 3: hipLaunchKernelGGL(k_layernorm<3>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
+    case 4: hipLaunchKernelGGL(k_layernorm<4>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
+    case 5: hipLaunchKernelGGL(k_layernorm<5>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
+    case 6: hipLaunchKernelGGL(k_layernorm<6>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
+    case 7: hipLaunchKernelGGL(k_layernorm<7>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
+    case 8: hipLaunchKernelGGL(k_layernorm<8>, grid, block, 0, s, x, ldx, gamma, beta, eps, rows, dim, yy, ldy, mean_out); break;
   }
   return check_launch("layernorm");
 }

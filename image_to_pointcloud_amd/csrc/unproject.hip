@@ -44,6 +44,7 @@ constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
 constexpr int kSlowBlock = 1024;
 constexpr int kRangeChunks = 32;
+constexpr int kSampleChunks = 8;    // k_model_hist workgroups (partial sample histograms) per image
 // Level 0 bins values (one bin ~ up to 2^31 keys near 0); levels 1-3 bin keys 2048 ways each:
 // 2^31 -> 2^20 -> 2^9 -> 1 key, so the last level always resolves.
 constexpr int kLastLevel = 3;
@@ -52,7 +53,7 @@ constexpr int kWinKeys = 6144;   // expected full-resolution keys per level-0 wi
 constexpr int kTileW = 1024;     // selection sweep column tile (4 columns per thread)
 constexpr int kSlotWords = kBins / 2;   // sweep LDS per slot: 2048 packed 16-bit counts or 1024 staged keys
 constexpr int kHrowBudget = 40 * 1024;   // LDS bytes of staged + horizontally interpolated model rows
-constexpr int kStageW = 256;             // k_sweep_w: window keys a workgroup stages in LDS per window
+constexpr int kStageW = 1024;            // k_sweep_w: window keys a workgroup stages in LDS per window
 constexpr int kMaxSelRows = 64;          // k_sweep_w: output rows per workgroup at most
 
 // PH_INIT: level-0 sweep pending; PH_SEL: targets being narrowed; PH_SLOW: handed to
@@ -150,7 +151,7 @@ static Layout layout(int B, int H, int W, int smooth) {
   L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
   L.trig = off;  off = align_up(off + sizeof(double) * 2 * ((size_t)W + H), 256);
   L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)B, 256);
-  L.mhist = off; off = align_up(off + sizeof(uint32_t) * kRangeChunks * kBins * (size_t)B, 256);
+  L.mhist = off; off = align_up(off + sizeof(uint32_t) * kSampleChunks * kBins * (size_t)B, 256);
   L.field = off;
   if (smooth) {
     off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
 }
 
 // Level-0 histogram of a sample of each full-resolution map (finite values, the level-0 binning):
-// one partial histogram per (image, chunk) in `mhist` [B][kRangeChunks][kBins], summed by k_window
+// one partial histogram per (image, chunk) in `mhist` [B][kSampleChunks][kBins], summed by k_window
 // (no global atomics: every chunk's workgroup sees most bins of its image).  The estimate k_window
 // predicts the target bins from.
 __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* mhist,
@@ -436,7 +437,7 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   // vanishes in the resize).  Each thread bins a contiguous run of samples (neighbours share
   // bins: one LDS atomic per run), 8 samples' loads in flight at a time.
   const int nsx = (g.W + stride - 1) / stride, nsy = (g.H + stride - 1) / stride, ns = nsx * nsy;
-  const int per = (ns + kRangeChunks - 1) / kRangeChunks;
+  const int per = (ns + kSampleChunks - 1) / kSampleChunks;
   const int i0 = c * per, i1 = min(ns, i0 + per);
   const int tper = (per + kBlock - 1) / kBlock;
   const int t0 = i0 + threadIdx.x * tper, t1 = min(i1, t0 + tper);
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   }
   if (run >= 0) atomicAdd(&lh[run], cnt);
   __syncthreads();
-  uint4* gh = reinterpret_cast<uint4*>(mhist + ((size_t)b * kRangeChunks + c) * kBins);
+  uint4* gh = reinterpret_cast<uint4*>(mhist + ((size_t)b * kSampleChunks + c) * kBins);
   const uint4* l4 = reinterpret_cast<const uint4*>(lh);
   for (int i = threadIdx.x; i < kBins / 4; i += kBlock) gh[i] = l4[i];
 }
@@ -914,15 +915,24 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
           const uint64_t m = __ballot(cq == q);
           if (!m) continue;
           const int leader = __ffsll((unsigned long long)m) - 1;
+          const uint32_t cnt = (uint32_t)__popcll(m);
           uint32_t base = 0;
-          if (lane == leader) base = atomicAdd(&lcnt[q], (uint32_t)__popcll(m));
+          if (lane == leader) base = atomicAdd(&lcnt[q], cnt);
           base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+          // ranks below `room` fill the LDS stage; the rest of the wave's keys (a spatially dense
+          // window: a smooth map puts a quantile's pixels in a few blocks) go straight to the
+          // candidate list with ONE global reservation per wave
+          const uint32_t room = base < (uint32_t)kStageW ? (uint32_t)kStageW - base : 0u;
+          const uint32_t over = cnt > room ? cnt - room : 0u;
+          uint32_t gb = 0;
+          if (over && lane == leader) gb = atomicAdd(&S->ccount[q], over);
+          gb = (uint32_t)__builtin_amdgcn_readlane((int)gb, leader);
           if (cq == q) {
-            const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (pos < (uint32_t)kStageW) {
-              sh[q][pos] = key;
+            const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (r < room) {
+              sh[q][base + r] = key;
             } else {
-              const uint32_t gpos = atomicAdd(&S->ccount[q], 1u);
+              const uint32_t gpos = gb + (r - room);
               if (gpos < cap) cand[((size_t)b * kSlots + q) * cap + gpos] = key;
             }
           }
@@ -1184,10 +1194,10 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
   uint32_t local = 0;
   {
     static_assert(kBins == 8 * kBlock, "k_window: 8 bins per thread");
-    const uint4* src = reinterpret_cast<const uint4*>(mhist + (size_t)b * kRangeChunks * kBins) + 2 * threadIdx.x;
+    const uint4* src = reinterpret_cast<const uint4*>(mhist + (size_t)b * kSampleChunks * kBins) + 2 * threadIdx.x;
     uint4 acc0 = make_uint4(0, 0, 0, 0), acc1 = make_uint4(0, 0, 0, 0);
 #pragma unroll 8
-    for (int c = 0; c < kRangeChunks; ++c) {
+    for (int c = 0; c < kSampleChunks; ++c) {
       const uint4 x = src[c * (kBins / 4)], y = src[c * (kBins / 4) + 1];
       acc0.x += x.x; acc0.y += x.y; acc0.z += x.z; acc0.w += x.w;
       acc1.x += y.x; acc1.y += y.y; acc1.z += y.z; acc1.w += y.w;
@@ -2707,7 +2717,7 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
   // full-resolution sample of ~64 K points per image for the level-0 estimate
   const int stride = std::max(1, (int)std::sqrt((double)g.H * g.W / 65536.0));
   const int ns = ((g.H + stride - 1) / stride) * ((g.W + stride - 1) / stride);
-  hipLaunchKernelGGL(k_model_hist, dim3(B * kRangeChunks), dim3(kBlock), 0, s, g, B, st, mhist, rpart, stride);
+  hipLaunchKernelGGL(k_model_hist, dim3(B * kSampleChunks), dim3(kBlock), 0, s, g, B, st, mhist, rpart, stride);
   hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, mhist, cap, B, x ? 0 : 1, ns);
   if (!x && g_sel_windows) {
     // batch path: one window-only sweep + resolve; k_sel_slow finishes (or, for the rare image

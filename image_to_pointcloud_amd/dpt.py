@@ -315,7 +315,7 @@ class DPTDepthModel:
         e = lambda shape, dt=torch.bfloat16: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
         b = dict(x=e((M, D), torch.float32), ln=e((M, D)), qkv=e((M, 3 * D)), att=e((M, D)), mlp=e((M, s.mlp)),
                  hs=[e((M, D)) for _ in s.out_indices], rb=e((B, D), torch.float32), tok=e((B * gh * gw, D)),
-                 part=e((M, D // 64, 2), torch.float32), rs=e((M, 2), torch.float32))
+                 part=e((M, D // 64, 2), torch.float32), rs=e((M, 2), torch.float32), shift=e((M,), torch.float32))
         b["ln_fold"] = LN_FOLD and D % 64 == 0 and self._ln_fold_ok(b, M)
         self._bufs[(B, gh, gw)] = b
         return b
@@ -336,7 +336,7 @@ class DPTDepthModel:
             return ops.gemm_kernel_label(d)
         consumer = dict(ln_rows=b["rs"].data_ptr(), col_sum=L["s_qkv"].data_ptr(), bias=L["b_qkv_f"].data_ptr())
         producer = dict(res=b["x"].data_ptr(), res_f32=1, ldr=D, ln_part=b["part"].data_ptr(),
-                        c_bf16=b["ln"].data_ptr(), ldc_bf16=D)
+                        c_bf16=b["ln"].data_ptr(), ldc_bf16=D, ln_shift=b["shift"].data_ptr())
         names = [name(b["ln"], L["w_qkv_f"], b["qkv"], **consumer),
                  name(b["ln"], L["w_1_f"], b["mlp"], **dict(consumer, col_sum=L["s_1"].data_ptr(), act=1)),
                  name(b["att"], L["w_o"], b["x"], **producer),
@@ -377,25 +377,30 @@ class DPTDepthModel:
                     ops.f32_to_bf16(x, out=buf["hs"][hs_i])
                     hs_i += 1
                 continue
-            if a_in is None:      # layer 0: LN1 of the embeddings
-                ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
+            if a_in is None:      # layer 0: LN1 of the embeddings (its row means: the first shift)
+                ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"], mean_out=buf["shift"])
                 qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
             else:
                 qkv = ops.linear(a_in, L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
                                  out=buf["qkv"])
             att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
-            ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x, ln_part=buf["part"], out_bf16=buf["ln"])
-            ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"])
+            # the residual's bf16 copy is stored minus the previous LayerNorm's row mean (shift),
+            # so rows whose mean is large against their spread keep their precision
+            ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x, ln_part=buf["part"], out_bf16=buf["ln"],
+                       ln_shift=buf["shift"])
+            ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=buf["shift"], shift_out=buf["shift"])
             h = ops.linear(buf["ln"], L["w_1_f"], bias=L["b_1_f"], act="gelu", ln_rows=buf["rs"], col_sum=L["s_1"],
                            out=buf["mlp"])
-            # FC2 + residual; its bf16 copy is the next QKV's A, or a kept hidden state (neck input)
-            dst = buf["ln"]
+            # FC2 + residual; its bf16 copy is the next QKV's A -- shifted like the one above, except
+            # for a kept hidden state, which the neck reads as it is (unshifted)
             if i in s.out_indices:
-                dst = buf["hs"][hs_i]
+                dst, shift = buf["hs"][hs_i], None
                 hs_i += 1
-            ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x, ln_part=buf["part"], out_bf16=dst)
+            else:
+                dst, shift = buf["ln"], buf["shift"]
+            ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x, ln_part=buf["part"], out_bf16=dst, ln_shift=shift)
             if i + 1 < nl:
-                ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"])
+                ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=shift, shift_out=buf["shift"])
             a_in = dst
         feats = [self._reassemble(j, buf["hs"][j], B, buf) for j in range(len(self.stages))]
         hidden = None

@@ -24,7 +24,10 @@ quantised once at load (ops.quantize_mx); activations are quantised by their pro
 (LayerNorm, the FC1 / conv1 / readout epilogues) or by one i2pc_quant_fp8 pass.  The BiT stem
 (~9 % of the FLOPs, GroupNorm-bound), the embedding projection, the attention core, the
 readout's CLS half, the fusion 1x1 projections and the fused head tail stay bf16.
-dtype="bf16": the DPT-Large kernels throughout.
+dtype="bf16": the DPT-Large kernels throughout.  `bf16_points` keeps named groups of an fp8
+model in bf16 (FP8_POINTS: "qkv", "o", "fc1", "fc2" of every encoder layer, "readout", "neck",
+"fusion", "head"): the per-point ablation of tests/test_dpt_hybrid_gpu.py, and the mixed default
+DEFAULT_BF16_POINTS chosen from it.
 """
 from __future__ import annotations
 
@@ -33,6 +36,12 @@ from dataclasses import dataclass
 
 from . import ops
 from .dpt import DPTDepthModel, DPTSpec, _pack_conv
+
+
+# quantisation points of the fp8 path (groups of GEMMs whose inputs and weights are MX fp8)
+FP8_POINTS = ("qkv", "o", "fc1", "fc2", "readout", "neck", "fusion", "head")
+# groups the fp8 model keeps in bf16 by default (chosen from the per-point ablation)
+DEFAULT_BF16_POINTS = ("qkv", "fc2")
 
 
 @dataclass(frozen=True)
@@ -215,21 +224,29 @@ class DPTHybridModel(DPTDepthModel):
 
     input_layout = "nchw"
 
-    def __init__(self, spec: HybridSpec, state_dict: dict, device, dtype: str = "fp8"):
+    def __init__(self, spec: HybridSpec, state_dict: dict, device, dtype: str = "fp8", bf16_points=None):
         import torch
         if dtype not in ("bf16", "fp8"):
             raise ValueError(f"dtype must be 'bf16' or 'fp8', got {dtype!r}")
         self.spec, self.dtype = spec, dtype
+        self.bf16_points = frozenset(DEFAULT_BF16_POINTS if bf16_points is None else bf16_points)
+        if not self.bf16_points <= set(FP8_POINTS):
+            raise ValueError(f"unknown bf16 points {sorted(self.bf16_points - set(FP8_POINTS))}; known: {FP8_POINTS}")
         self.device = torch.device(device)
         self._bufs = {}
         dev = self.device
         sd = {k: v.detach().to(torch.float32).cpu() for k, v in state_dict.items()}
-        f8 = dtype == "fp8"
+        f8 = self._f8
         bf = lambda t: t.to(torch.bfloat16).contiguous().to(dev)               # noqa: E731
         f32 = lambda t: t.to(torch.float32).contiguous().to(dev)               # noqa: E731
-        lin = lambda t: ops.quantize_mx(t.to(dev)) if f8 else bf(t)            # noqa: E731
-        cnv = lambda t: (ops.quantize_mx(t.permute(0, 2, 3, 1).reshape(t.shape[0], -1).contiguous().to(dev))   # noqa: E731
-                         if f8 else _pack_conv(t, torch).to(dev))
+
+        def lin(t, pt):
+            return ops.quantize_mx(t.to(dev)) if f8(pt) else bf(t)
+
+        def cnv(t, pt):
+            if f8(pt):
+                return ops.quantize_mx(t.permute(0, 2, 3, 1).reshape(t.shape[0], -1).contiguous().to(dev))
+            return _pack_conv(t, torch).to(dev)
         D, g = spec.hidden, spec.grid
         # ---- BiT stem (bf16)
         p = "dpt.embeddings.backbone.bit."
@@ -268,23 +285,24 @@ class DPTHybridModel(DPTDepthModel):
             bq = torch.cat([sd[q + f"attention.attention.{n}.bias"] for n in ("query", "key", "value")], 0)
             self.layers.append(dict(
                 ln1_g=f32(sd[q + "layernorm_before.weight"]), ln1_b=f32(sd[q + "layernorm_before.bias"]),
-                w_qkv=lin(wq), b_qkv=f32(bq),
-                w_o=lin(sd[q + "attention.output.dense.weight"]), b_o=f32(sd[q + "attention.output.dense.bias"]),
+                w_qkv=lin(wq, "qkv"), b_qkv=f32(bq),
+                w_o=lin(sd[q + "attention.output.dense.weight"], "o"), b_o=f32(sd[q + "attention.output.dense.bias"]),
                 ln2_g=f32(sd[q + "layernorm_after.weight"]), ln2_b=f32(sd[q + "layernorm_after.bias"]),
-                w_1=lin(sd[q + "intermediate.dense.weight"]), b_1=f32(sd[q + "intermediate.dense.bias"]),
-                w_2=lin(sd[q + "output.dense.weight"]), b_2=f32(sd[q + "output.dense.bias"])))
+                w_1=lin(sd[q + "intermediate.dense.weight"], "fc1"), b_1=f32(sd[q + "intermediate.dense.bias"]),
+                w_2=lin(sd[q + "output.dense.weight"], "fc2"), b_2=f32(sd[q + "output.dense.bias"])))
         # ---- neck
         self.stages = []
         for i, (c, fac) in enumerate(zip(spec.neck, spec.factors)):
-            st = dict(c=c, fac=fac, w_neck=cnv(sd[f"neck.convs.{i}.weight"]))
+            st = dict(c=c, fac=fac, w_neck=cnv(sd[f"neck.convs.{i}.weight"], "neck"))
             if i >= 2:
                 q = "neck.reassemble_stage."
                 wr = sd[q + f"readout_projects.{i}.0.weight"]
-                st.update(w_tok=lin(wr[:, :D]), w_cls=bf(wr[:, D:]), b_ro=f32(sd[q + f"readout_projects.{i}.0.bias"]),
-                          w_proj=lin(sd[q + f"layers.{i}.projection.weight"].reshape(c, D)),
+                st.update(w_tok=lin(wr[:, :D], "readout"), w_cls=bf(wr[:, D:]),
+                          b_ro=f32(sd[q + f"readout_projects.{i}.0.bias"]),
+                          w_proj=lin(sd[q + f"layers.{i}.projection.weight"].reshape(c, D), "readout"),
                           b_proj=f32(sd[q + f"layers.{i}.projection.bias"]))
                 if fac < 1:
-                    st["w_rs"] = cnv(sd[q + f"layers.{i}.resize.weight"])
+                    st["w_rs"] = cnv(sd[q + f"layers.{i}.resize.weight"], "readout")
                     st["b_rs"] = f32(sd[q + f"layers.{i}.resize.bias"])
             self.stages.append(st)
         F = spec.fusion
@@ -294,15 +312,19 @@ class DPTHybridModel(DPTDepthModel):
             fl = dict(w_proj=bf(sd[q + "projection.weight"].reshape(F, F)), b_proj=f32(sd[q + "projection.bias"]))
             for r in ("residual_layer1", "residual_layer2"):
                 for cv in ("convolution1", "convolution2"):
-                    fl[f"{r}.{cv}.w"] = cnv(sd[q + f"{r}.{cv}.weight"])
+                    fl[f"{r}.{cv}.w"] = cnv(sd[q + f"{r}.{cv}.weight"], "fusion")
                     fl[f"{r}.{cv}.b"] = f32(sd[q + f"{r}.{cv}.bias"])
             self.fusion.append(fl)
-        self.w_h0 = cnv(sd["head.head.0.weight"])
+        self.w_h0 = cnv(sd["head.head.0.weight"], "head")
         self.b_h0 = f32(sd["head.head.0.bias"])
         self.w_h2 = _pack_conv(sd["head.head.2.weight"], torch).to(dev)
         self.b_h2 = f32(sd["head.head.2.bias"])
         self.w_h4 = f32(sd["head.head.4.weight"].reshape(32))
         self.b_h4 = float(sd["head.head.4.bias"].reshape(()).item())
+
+    def _f8(self, point: str) -> bool:
+        """Whether quantisation point `point` (FP8_POINTS) runs on the MX fp8 engine."""
+        return self.dtype == "fp8" and point not in self.bf16_points
 
     # ------------------------------------------------------------------ buffers
     def buffers(self, B: int) -> dict:
@@ -315,12 +337,10 @@ class DPTHybridModel(DPTDepthModel):
         M = B * T
         e = lambda shape, dt=torch.bfloat16: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
         b = dict(x=e((M, D), torch.float32), qkv=e((M, 3 * D)), att=e((M, D)), rb=e((B, D), torch.float32),
-                 hs=[e((M, D)) for _ in range(2)])
+                 hs=[e((M, D)) for _ in range(2)], lnb=e((M, D)), mlpb=e((M, s.mlp)))
         if self.dtype == "fp8":
             b.update(ln=ops.empty_fp8((M, D), dev), att8=ops.empty_fp8((M, D), dev), mlp=ops.empty_fp8((M, s.mlp), dev),
                      tok8=[ops.empty_fp8((B * g * g, D), dev) for _ in range(2)])
-        else:
-            b.update(ln=e((M, D)), mlp=e((M, s.mlp)))
         self._bufs[B] = b
         return b
 
@@ -340,34 +360,43 @@ class DPTHybridModel(DPTDepthModel):
         ops.cls_pos(self.cls, self.pos0, x, B, T, D)
         scale = 1.0 / math.sqrt(D // s.heads)
         keep = list(s.out_indices[2:])
+        f8 = self._f8
         for i, L in enumerate(self.layers):
-            if self.dtype == "fp8":
+            if f8("qkv"):
                 ln = ops.layernorm_fp8(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
                 qkv = ops.linear_fp8(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
-                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            else:
+                ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["lnb"])
+                qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
+            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            if f8("o"):
                 ops.linear_fp8(ops.quant_fp8(att, out=buf["att8"]), L["w_o"], bias=L["b_o"], res=x, out=x)
+            else:
+                ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
+            if f8("fc1"):       # FC1's epilogue writes FC2's operand format
                 ln = ops.layernorm_fp8(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])
-                h = ops.linear_fp8(ln, L["w_1"], bias=L["b_1"], act="gelu", out=buf["mlp"], out_fp8=True)
+                h = ops.linear_fp8(ln, L["w_1"], bias=L["b_1"], act="gelu",
+                                   out=buf["mlp"] if f8("fc2") else buf["mlpb"], out_fp8=f8("fc2"))
+            else:
+                ln = ops.layernorm(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["lnb"])
+                h = ops.linear(ln, L["w_1"], bias=L["b_1"], act="gelu", out=buf["mlpb"])
+                if f8("fc2"):
+                    h = ops.quant_fp8(h, out=buf["mlp"])
+            if f8("fc2"):
                 ops.linear_fp8(h, L["w_2"], bias=L["b_2"], res=x, out=x)
             else:
-                ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
-                qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
-                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
-                ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
-                ln = ops.layernorm(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])
-                h = ops.linear(ln, L["w_1"], bias=L["b_1"], act="gelu", out=buf["mlp"])
                 ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x)
             if i in keep:
                 j = keep.index(i)
                 ops.f32_to_bf16(x, out=buf["hs"][j])
-                if self.dtype == "fp8":      # the readout's token rows (CLS skipped), quantised once
+                if f8("readout"):    # the readout's token rows (CLS skipped), quantised once
                     ops.quant_fp8(x, rows=B * np_, a_map=(np_, T, 1), out=buf["tok8"][j])
         feats = [self._neck_bit(0, feats_bit[0]), self._neck_bit(1, feats_bit[1])]
         feats += [self._reassemble_vit(j, buf, B) for j in (2, 3)]
         hidden = None
         for j, feat in enumerate(reversed(feats)):
             hidden = self._fuse(self.fusion[j], feat, hidden)
-        if self.dtype == "fp8":
+        if f8("head"):
             t = ops.conv2d_fp8(ops.quant_fp8(hidden), self.w_h0, bias=self.b_h0)
         else:
             t = ops.conv2d(hidden, self.w_h0, bias=self.b_h0)
@@ -406,7 +435,7 @@ class DPTHybridModel(DPTDepthModel):
 
     def _neck_bit(self, j, f):
         st = self.stages[j]
-        if self.dtype == "fp8":
+        if self._f8("neck"):
             return ops.conv2d_fp8(ops.quant_fp8(f), st["w_neck"])
         return ops.conv2d(f, st["w_neck"])
 
@@ -418,20 +447,27 @@ class DPTHybridModel(DPTDepthModel):
         hs = buf["hs"][k]
         rb = ops.linear(hs, st["w_cls"], bias=st["b_ro"], rows=B, a_map=(1, T, 0), out=buf["rb"])
         c = st["c"]
-        if self.dtype == "fp8":
+        f8n = self._f8("neck")
+        if self._f8("readout"):
+            # the last readout GEMM writes the neck conv's operand format
+            sub = st["fac"] < 1
             tok = ops.linear_fp8(buf["tok8"][k], st["w_tok"], row_bias=rb, row_bias_group=np_, act="gelu", out_fp8=True)
-            proj = ops.linear_fp8(tok, st["w_proj"], bias=st["b_proj"], out_fp8=True).view(B, g, g, c)
+            proj = ops.linear_fp8(tok, st["w_proj"], bias=st["b_proj"], out_fp8=f8n or sub)
+            proj = proj.view(B, g, g, c)
+            if sub:
+                proj = ops.conv2d_fp8(proj, st["w_rs"], bias=st["b_rs"], k=3, stride=2, pad=1, out_fp8=f8n)
+        else:
+            tok = ops.linear(hs, st["w_tok"], rows=B * np_, a_map=(np_, T, 1), row_bias=rb, row_bias_group=np_,
+                             act="gelu")
+            proj = ops.linear(tok, st["w_proj"], bias=st["b_proj"]).view(B, g, g, c)
             if st["fac"] < 1:
-                proj = ops.conv2d_fp8(proj, st["w_rs"], bias=st["b_rs"], k=3, stride=2, pad=1, out_fp8=True)
-            return ops.conv2d_fp8(proj, st["w_neck"])
-        tok = ops.linear(hs, st["w_tok"], rows=B * np_, a_map=(np_, T, 1), row_bias=rb, row_bias_group=np_, act="gelu")
-        proj = ops.linear(tok, st["w_proj"], bias=st["b_proj"]).view(B, g, g, c)
-        if st["fac"] < 1:
-            proj = ops.conv2d(proj, st["w_rs"], bias=st["b_rs"], k=3, stride=2, pad=1)
-        return ops.conv2d(proj, st["w_neck"])
+                proj = ops.conv2d(proj, st["w_rs"], bias=st["b_rs"], k=3, stride=2, pad=1)
+            if f8n:
+                proj = ops.quant_fp8(proj)
+        return ops.conv2d_fp8(proj, st["w_neck"]) if f8n else ops.conv2d(proj, st["w_neck"])
 
     def _fuse(self, fl, feat, hidden):
-        if self.dtype != "fp8":
+        if not self._f8("fusion"):
             return super()._fuse(fl, feat, hidden)
         if hidden is None:
             h = feat

@@ -214,8 +214,10 @@ typedef struct i2pc_gemm_desc {
    * Producer (fp32 output rows, e.g. the residual-add epilogue of attention-out / FC2): with
    *   ln_part set it also writes c_bf16 [m][ldc_bf16] = bf16(out) and, per output row and 64-column
    *   chunk, ln_part float2 [m][n / 64] = (mean, sum of squared deviations from it) of that chunk of
-   *   out.  Needs n % 64 == 0, c_f32, no row remap / ConvTranspose store (EUNSUPPORTED where the
-   *   chosen kernel cannot: i2pc_gemm_kernel_name says "invalid").
+   *   out.  With ln_shift (fp32 [m], e.g. the row means of the previous LayerNorm) both are taken
+   *   of out - ln_shift[row] instead (the bf16 copy then keeps its precision for rows whose mean is
+   *   large against their spread).  Needs n % 64 == 0, c_f32, no row remap / ConvTranspose store
+   *   (EUNSUPPORTED where the chosen kernel cannot: i2pc_gemm_kernel_name says "invalid").
    * Consumer (A = the producer's c_bf16, W = W * gamma[k] in bf16): with ln_rows set the epilogue
    *   computes act(rs.x * acc + rs.y * col_sum[n] + bias[n]) with rs = ln_rows float2 [m] =
    *   (rstd, -rstd * mean) (i2pc_ln_rowstats), col_sum fp32 [n] = sum_k of W's bf16 row, bias =
@@ -223,12 +225,17 @@ typedef struct i2pc_gemm_desc {
    *   residuals / row bias / table (the persistent engine runs it). */
   const float* ln_rows; const float* col_sum;
   float* ln_part; void* c_bf16; int64_t ldc_bf16;
+  const float* ln_shift;
 } i2pc_gemm_desc;
 
 /* LayerNorm row statistics from i2pc_gemm's producer partials: rows_out float2 [rows] =
  * (rstd, -rstd * mean) of each row's `parts` 64-column chunks (part float2 [rows][parts]), the
- * chunks combined by Chan's formula; biased variance, rstd = 1 / sqrt(var + eps) (nn.LayerNorm). */
-int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out, void* stream);
+ * chunks combined by Chan's formula; biased variance, rstd = 1 / sqrt(var + eps) (nn.LayerNorm).
+ * shift_in (fp32 [rows] or NULL = 0): the producer's ln_shift -- the partials were taken of
+ * out - shift_in, so `mean` above is the shifted mean; shift_out (or NULL) receives the rows' true
+ * means, shift_in + mean (the next producer's shift; may alias shift_in).  parts <= 64. */
+int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out, const float* shift_in,
+                     float* shift_out, void* stream);
 
 int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
 
@@ -342,6 +349,10 @@ int i2pc_set_tuning(const char* name, int value);
  * (nn.LayerNorm, modeling_dpt.py:233-234). dim % 64 == 0, dim <= 2048. */
 int i2pc_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
                    int rows, int dim, void* y, int64_t ldy, void* stream);
+/* i2pc_layernorm that also stores each row's mean (fp32 [rows]; e.g. the first ln_shift of a
+ * LayerNorm-folded encoder). */
+int i2pc_layernorm_stats(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps,
+                         int rows, int dim, void* y, int64_t ldy, float* row_mean, void* stream);
 
 /* Fused multi-head self-attention (softmax(Q K^T * scale) V, no mask), head_dim 64.
  * qkv: bf16 [batch*tokens][3*heads*64] (Q | K | V column blocks, the fused QKV GEMM output);

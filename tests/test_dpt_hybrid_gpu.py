@@ -126,3 +126,42 @@ def test_c5_pipeline_fp8_to_coloured_ply(tmp_path):
     head = data[: data.index(b"end_header\n") + len(b"end_header\n")].decode()
     assert "element vertex 1048576" in head and "property uchar red" in head
     assert len(data) - len(head) == 1048576 * (3 * 8 + 3)        # double xyz + uchar rgb (Open3D layout)
+
+
+def test_fp8_quantisation_point_ablation():
+    """Which MX fp8 quantisation point costs the accuracy: the fp8 network
+    with ONE group of GEMMs back in bf16 at a time (dpt_hybrid.FP8_POINTS), relative L2 of the depth
+    against transformers fp32 on 384^2 and 1024^2 inputs.  Prints the table and
+    checks the default mix (DEFAULT_BF16_POINTS) against the 5e-2 bound at both sizes."""
+    from image_to_pointcloud_amd.dpt_hybrid import (DEFAULT_BF16_POINTS, DPT_HYBRID, FP8_POINTS, DPTHybridModel,
+                                                    synthetic_state_dict)
+    from image_to_pointcloud_amd.preprocess import Preprocessor, ProcessorSpec
+    spec, B = DPT_HYBRID, 2
+    dev = torch.device("cuda")
+    sd = synthetic_state_dict(spec, 0)
+    ref = _hf(spec, sd, dev)
+    cases = []
+    for hw in ((384, 384), (1024, 1024)):
+        imgs = _images(B, hw[0], hw[1], 7)
+        prep = Preprocessor(hw[0], hw[1], ProcessorSpec(size=(spec.image, spec.image)))
+        pix = prep(torch.from_numpy(imgs).to(dev), layout="nchw")
+        with torch.no_grad():
+            exp = ref(pixel_values=pix).predicted_depth.float()
+        cases.append((hw, pix, exp))
+    del ref
+    configs = ([("all fp8", ()), ("default", tuple(DEFAULT_BF16_POINTS))] + [(f"{p} bf16", (p,)) for p in FP8_POINTS]
+               + [("qkv+fc2 bf16", ("qkv", "fc2")), ("qkv+fc1+fc2 bf16", ("qkv", "fc1", "fc2")),
+                  ("qkv+fc2+neck bf16", ("qkv", "fc2", "neck"))])
+    table = {}
+    for name, pts in configs:
+        model = DPTHybridModel(spec, sd, dev, dtype="fp8", bf16_points=pts)
+        errs = []
+        for hw, pix, exp in cases:
+            depth = model(pix, B)
+            torch.cuda.synchronize()
+            errs.append(((depth - exp).norm() / exp.norm()).item())
+        table[name] = errs
+        _report(f"dpt-hybrid fp8 ablation: {name}", rel_l2_384=errs[0], rel_l2_1024=errs[1])
+        del model
+        torch.cuda.empty_cache()
+    assert max(table["default"]) <= 5e-2, table["default"]
