@@ -103,7 +103,9 @@ struct alignas(16) SelState {
   uint32_t wbelow[3];
   uint32_t wcntF[3], wminF[3], wmaxF[3];
   uint32_t wcntL[3], wminL[3], wmaxL[3];
-  uint32_t pad5[3];
+  // window w as values (k_window): finite values < wvlo[w] lie below it, values in [wvlo, wvhi]
+  // inside; a spike first bin ends at wvF[w], a spike last bin starts at wvL[w]
+  float wvlo[3], wvhi[3], wvF[3], wvL[3];
 };
 
 // Correctly rounded a / b from r = RN(1 / b) (Markstein's correction: q0 = RN(a r),
@@ -443,25 +445,42 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   const int t0 = i0 + threadIdx.x * tper, t1 = min(i1, t0 + tper);
   int run = -1;
   uint32_t cnt = 0;
+  // lattice position of sample t0, then stepped (no division per sample): the jitter offsets
+  // jy = (7 sx + 3 sy) mod stride, jx = (5 sy + 3 sx) mod stride advance by 7 / 3 per column
+  int sy = t0 / nsx, sx = t0 - sy * nsx;
+  int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
+  const int d7 = 7 % stride, d3 = 3 % stride;
+  auto step = [&]() {
+    if (++sx == nsx) {
+      sx = 0;
+      ++sy;
+      jy = (sy * 3) % stride;
+      jx = (sy * 5) % stride;
+    } else {
+      jy += d7; jy -= jy >= stride ? stride : 0;
+      jx += d3; jx -= jx >= stride ? stride : 0;
+    }
+  };
   for (int i = t0; i < t1; i += 8) {
+    int py[8], px[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {       // (past t1: a repeat of the last sample, not counted)
+      py[k] = min(sy * stride + jy, g.H - 1);
+      px[k] = min(sx * stride + jx, g.W - 1);
+      if (i + k + 1 < t1) step();
+    }
     float v[8];
     if (g.same) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int si = min(i + k, t1 - 1), sy = si / nsx, sx = si - sy * nsx;
-        const int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
-        v[k] = sample(g, b, min(sy * stride + jy, g.H - 1), min(sx * stride + jx, g.W - 1));
-      }
+      for (int k = 0; k < 8; ++k) v[k] = sample(g, b, py[k], px[k]);
     } else {
       // jittered lattice: the offset inside each stride x stride cell cycles with the cell, so
       // every residue of the cv2 tap pattern (single-tap columns/rows included) is sampled
       Tap ty[8], tx[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const int si = min(i + k, t1 - 1), sy = si / nsx, sx = si - sy * nsx;
-        const int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
-        ty[k] = g.yt[min(sy * stride + jy, g.H - 1)];
-        tx[k] = g.xt[min(sx * stride + jx, g.W - 1)];
+        ty[k] = g.yt[py[k]];
+        tx[k] = g.xt[px[k]];
       }
       const float* D = g.depth + (size_t)b * g.dh * g.dw;
       float a0[8], a1[8], c0[8], c1[8];
@@ -773,43 +792,24 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
 }
 
 // Window-only selection sweep (the batch path's only full-resolution pass before the
-// unprojection): no histogram at all.  Per k_window window w (level-0 bins [wlo, whi]) it counts
-// the finite keys below the window (one wave-reduced atomic per workgroup), compacts the keys
-// inside it into w's candidate list, and -- for an end bin k_window flagged as a spike -- counts
-// that bin's keys with their min / max key instead of compacting them.  Plus the level-0
-// counters (non-finite counts, finite key range).  k_resolve_w turns this into exact keys; a
-// target outside every window (or in an unresolvable part) falls to k_sel_slow.
-template <bool SAME>
-__global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_t* cand, uint32_t cap, int B,
-                                                    Sweep sw) {
-  // thread = 4 columns c0 + j * kBlock + tid of a kTileW-column tile, walking down the block's
-  // R output rows.  The horizontal cv2 pass of a model row is a thread's own business (its 4
-  // columns), so it stays in registers: rows ra (hA) and ra + 1 (hB) interpolated, the raw
-  // taps of row ra + 2 already loaded (pre) -- a model row advance costs no wait and no LDS.
-  __shared__ uint32_t sh[3][kStageW];               // staged window keys
-  __shared__ uint32_t red[kBlock / 64][24];
-  __shared__ uint32_t lcnt[3], gbase[3];
-  __shared__ Tap tys[kMaxSelRows];                  // the block's row taps (no global load in the row loop)
-  int b, chunk;
-  map_block(blockIdx.x, B, sw.nrb * sw.ntiles, b, chunk);
-  const int rb = chunk / sw.ntiles, c0 = (chunk - rb * sw.ntiles) * kTileW;
-  const int cw = min(kTileW, g.W - c0);
-  SelState* S = st + b;
-  if (S->phase != PH_INIT) return;
-  const VBins vb0 = level0_vbins(S->rlo, S->rhi);
-  const int nwin = (int)S->nwin;
-  int wlo[3] = {kBins, kBins, kBins}, whi[3] = {-1, -1, -1};
-  uint32_t spk[3] = {0, 0, 0};
-#pragma unroll
-  for (int w = 0; w < 3; ++w)
-    if (w < nwin) { wlo[w] = (int)S->wbin[2 * w]; whi[w] = (int)S->wbin[2 * w + 1]; spk[w] = S->wspike[w]; }
-  const bool any_spike = (spk[0] | spk[1] | spk[2]) != 0;
-  const int v0 = sw.row0 + rb * sw.R;
-  const int v1 = min(sw.row_end, v0 + sw.R);
-  if (threadIdx.x < 3) lcnt[threadIdx.x] = 0;
-  if (!SAME && (int)threadIdx.x < v1 - v0) tys[threadIdx.x] = g.yt[v0 + threadIdx.x];
-  __syncthreads();
-
+// unprojection): no histogram at all.  Per k_window window w it counts the finite values below
+// the window, compacts the keys inside it into w's candidate list, and -- for an end bin
+// k_window flagged as a spike -- counts that bin's keys with their min / max key instead of
+// compacting them; plus the non-finite counts.  k_resolve_w turns this into exact keys; a target
+// outside every window (or in an unresolvable part) falls to k_sel_slow.
+//
+// The window bounds arrive as VALUES (k_window: the first / last key of the window's level-0
+// bins, as floats), so a pixel costs its cv2 interpolation, one class test and two float
+// compares per window (VALU) plus a few mask operations (SALU, balanced against the VALU: both
+// issue about once per CU cycle).  Lanes past the tile's edge carry NaN (below no window, in
+// none); keys are formed only in the rare waves that hold a window pixel.  Float order is key order on finite values
+// except -0 < +0, and a bin bound never separates the two zeros (vbin maps both to one bin).
+template <bool SAME, int NW>
+__device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t* cand, uint32_t cap, int b,
+                                             int v0, int v1, int cw, int c0, const Tap* tys,
+                                             uint32_t (*sh)[kStageW], uint32_t (*red)[24], uint32_t* lcnt,
+                                             const float* vlo, const float* vhi, const float* vF,
+                                             const float* vL, const uint32_t* spk) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float* Dimg = g.depth + (size_t)b * g.dh * g.dw;
   int ucol[4];
@@ -819,8 +819,13 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
     act[j] = j * kBlock + (int)threadIdx.x < cw;
     ucol[j] = c0 + min(j * kBlock + (int)threadIdx.x, cw - 1);
   }
+  bool any_spike = false;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) any_spike |= spk[w] != 0u;
   Tap tx[4];
-  float hA[4], hB[4], pre[8];
+  // rows ra (hA) and ra + 1 (hB) interpolated, the raw taps of rows ra + 2 (p2) and ra + 3 (p3)
+  // in flight: an advance waits on loads issued two advances earlier
+  float hA[4], hB[4], p2[8], p3[8];
   int ra = 0;
   auto load_raw = [&](int r, float (&q)[8]) {
     const float* R0 = Dimg + (size_t)min(r, g.dh - 1) * g.dw;
@@ -840,121 +845,136 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
     for (int j = 0; j < 4; ++j) cur[j] = Dimg[(size_t)v0 * g.dw + ucol[j]];
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) tx[j] = g.xt[ucol[j]];
+    for (int j = 0; j < 4; ++j) {
+      tx[j] = g.xt[ucol[j]];
+      if (!act[j]) tx[j].w0 = __builtin_nanf("");   // (interpolates to NaN)
+    }
     ra = tys[0].i0;
     float q0[8], q1[8];
     load_raw(ra, q0);
     load_raw(ra + 1, q1);
-    load_raw(ra + 2, pre);
+    load_raw(ra + 2, p2);
+    load_raw(ra + 3, p3);
     interp(q0, hA);
     interp(q1, hB);
   }
 
-  uint32_t nf = 0, nnan = 0, nneg = 0, npos = 0, kmin = 0xffffffffu, kmax = 0u;
-  uint32_t below[3] = {0, 0, 0};
-  uint32_t cF[3] = {0, 0, 0}, mnF[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mxF[3] = {0, 0, 0};
-  uint32_t cL[3] = {0, 0, 0}, mnL[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mxL[3] = {0, 0, 0};
+  // non-finite counts: wave-uniform (scalar registers); the rest per lane (wave-reduced at the end)
+  uint32_t nf = 0, nnan = 0, nneg = 0, npos = 0;
+  uint32_t below[NW], cF[NW], cL[NW];
+  uint32_t mnF[NW], mxF[NW], mnL[NW], mxL[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    below[w] = cF[w] = cL[w] = 0u;
+    mnF[w] = mnL[w] = 0xffffffffu;
+    mxF[w] = mxL[w] = 0u;
+  }
   for (int v = v0; v < v1; ++v) {
     float val[4];
     if (SAME) {
-      // the next row's values in flight while this row is binned
+      // the next row's values in flight while this row is counted
       const int vn = min(v + 1, v1 - 1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { val[j] = cur[j]; cur[j] = Dimg[(size_t)vn * g.dw + ucol[j]]; }
+      for (int j = 0; j < 4; ++j) {
+        val[j] = act[j] ? cur[j] : __builtin_nanf("");
+        cur[j] = Dimg[(size_t)vn * g.dw + ucol[j]];
+      }
     } else {
       const Tap ty = tys[v - v0];
       // advance the register rows to ty.i0 (wave-uniform; once per ~H / dh output rows)
       while (ra < ty.i0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) hA[j] = hB[j];
-        interp(pre, hB);
+        interp(p2, hB);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) p2[i] = p3[i];
         ++ra;
-        load_raw(ra + 2, pre);
+        load_raw(ra + 3, p3);
       }
       const bool second_is_a = ty.i1 == ra;     // (the bottom rows clamp i1 to i0)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) val[j] = hA[j] * ty.w0 + (second_is_a ? hA[j] : hB[j]) * ty.w1;
+      for (int j = 0; j < 4; ++j) val[j] = hA[j] * ty.w0 + (second_is_a ? hA[j] : hB[j]) * ty.w1;   // cv2 VResizeLinear
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool active = act[j];
-      const uint32_t key = f2key(val[j]);
-      const bool fin = active && !key_nonfinite(key);
-      if (active && !fin) {
-        ++nf;
-        nnan += (key != kKeyPosInf && key != kKeyNegInf) ? 1u : 0u;
-        nneg += key == kKeyNegInf ? 1u : 0u;
-        npos += key == kKeyPosInf ? 1u : 0u;
-      }
-      kmin = min(kmin, fin ? key : 0xffffffffu);
-      kmax = max(kmax, fin ? key : 0u);
-      const int hb = fin ? (int)vbin(val[j], vb0) : kBins;      // non-finite: in no window, below none
-      int cq = -1;
+      const float x = val[j];
+      if (__ballot(!__builtin_isfinite(x))) {     // rare: split the non-finite pixels (edge lanes' NaN aside)
+        const uint64_t am = __ballot(act[j]);
+        const bool ni = x == -INFINITY;
+        const uint64_t nfm = __ballot(!__builtin_isfinite(x)) & am;
+        const uint64_t negm = __ballot(ni) & am;
+        const uint64_t posm = __ballot(x == INFINITY) & am;
+        nf += (uint32_t)__popcll(nfm);
+        nneg += (uint32_t)__popcll(negm);
+        npos += (uint32_t)__popcll(posm);
+        nnan += (uint32_t)__popcll(nfm & ~(negm | posm));
 #pragma unroll
-      for (int w = 0; w < 3; ++w) {
-        below[w] += hb < wlo[w] ? 1u : 0u;
-        cq = (hb >= wlo[w] && hb <= whi[w]) ? w : cq;
+        for (int w = 0; w < NW; ++w) below[w] -= ni ? 1u : 0u;   // -inf compares below every window
       }
-      if (any_spike && cq >= 0) {
+      bool inw[NW], anyl = false;
 #pragma unroll
-        for (int w = 0; w < 3; ++w) {
-          const bool inF = cq == w && (spk[w] & 1u) && hb == wlo[w];
-          const bool inL = cq == w && (spk[w] & 2u) && hb == whi[w] && !inF;
+      for (int w = 0; w < NW; ++w) {
+        const bool bl = x < vlo[w];
+        below[w] += bl ? 1u : 0u;
+        inw[w] = !bl && x <= vhi[w];               // (NaN / +inf: neither)
+        anyl |= inw[w];
+      }
+      if (!__ballot(anyl)) continue;
+      const uint32_t key = f2key(x);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        uint64_t m = __ballot(inw[w]);
+        if (!m) continue;
+        if (any_spike && spk[w]) {
+          const uint64_t fm = (spk[w] & 1u) ? __ballot(x <= vF[w]) & m : 0ull;
+          const uint64_t lm = (spk[w] & 2u) ? __ballot(x >= vL[w]) & m & ~fm : 0ull;
+          const bool inF = (fm >> lane) & 1ull, inL = (lm >> lane) & 1ull;
           cF[w] += inF ? 1u : 0u;
+          cL[w] += inL ? 1u : 0u;
           mnF[w] = inF ? min(mnF[w], key) : mnF[w];
           mxF[w] = inF ? max(mxF[w], key) : mxF[w];
-          cL[w] += inL ? 1u : 0u;
           mnL[w] = inL ? min(mnL[w], key) : mnL[w];
           mxL[w] = inL ? max(mxL[w], key) : mxL[w];
-          cq = (inF || inL) ? -1 : cq;
-        }
-      }
-      if (__ballot(cq >= 0)) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const uint64_t m = __ballot(cq == q);
+          m &= ~(fm | lm);
           if (!m) continue;
-          const int leader = __ffsll((unsigned long long)m) - 1;
-          const uint32_t cnt = (uint32_t)__popcll(m);
-          uint32_t base = 0;
-          if (lane == leader) base = atomicAdd(&lcnt[q], cnt);
-          base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-          // ranks below `room` fill the LDS stage; the rest of the wave's keys (a spatially dense
-          // window: a smooth map puts a quantile's pixels in a few blocks) go straight to the
-          // candidate list with ONE global reservation per wave
-          const uint32_t room = base < (uint32_t)kStageW ? (uint32_t)kStageW - base : 0u;
-          const uint32_t over = cnt > room ? cnt - room : 0u;
-          uint32_t gb = 0;
-          if (over && lane == leader) gb = atomicAdd(&S->ccount[q], over);
-          gb = (uint32_t)__builtin_amdgcn_readlane((int)gb, leader);
-          if (cq == q) {
-            const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (r < room) {
-              sh[q][base + r] = key;
-            } else {
-              const uint32_t gpos = gb + (r - room);
-              if (gpos < cap) cand[((size_t)b * kSlots + q) * cap + gpos] = key;
-            }
+        }
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&lcnt[w], cnt);
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+        // ranks below `room` fill the LDS stage; the rest of the wave's keys (a spatially dense
+        // window: a smooth map puts a quantile's pixels in a few blocks) go straight to the
+        // candidate list with ONE global reservation per wave
+        const uint32_t room = base < (uint32_t)kStageW ? (uint32_t)kStageW - base : 0u;
+        const uint32_t over = cnt > room ? cnt - room : 0u;
+        uint32_t gb = 0;
+        if (over && lane == leader) gb = atomicAdd(&S->ccount[w], over);
+        gb = (uint32_t)__builtin_amdgcn_readlane((int)gb, leader);
+        if ((m >> lane) & 1ull) {
+          const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          if (r < room) {
+            sh[w][base + r] = key;
+          } else {
+            const uint32_t gpos = gb + (r - room);
+            if (gpos < cap) cand[((size_t)b * kSlots + w) * cap + gpos] = key;
           }
         }
       }
     }
   }
-  // workgroup totals: one atomic per counter and workgroup
-  nf = wave_sum_u32(nf);
-  kmin = wave_min_u32(kmin);
-  kmax = wave_max_u32(kmax);
-  if (lane == 0) { red[wid][0] = nf; red[wid][1] = kmin; red[wid][2] = kmax; }
+  // wave totals -> red[wave][...]: 0 nf, 1 nnan, 2 nneg, 3 npos, 4 + w below, then per window
+  // 6 + 6 w: F count / min / max, L count / min / max
 #pragma unroll
-  for (int w = 0; w < 3; ++w) {
-    if (w < nwin) {
-      const uint32_t bw = wave_sum_u32(below[w]);
-      if (lane == 0) red[wid][3 + w] = bw;
-    }
+  for (int w = 0; w < NW; ++w) below[w] = wave_sum_u32(below[w]);
+  if (lane == 0) {
+    red[wid][0] = nf; red[wid][1] = nnan; red[wid][2] = nneg; red[wid][3] = npos;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) red[wid][4 + w] = below[w];
   }
   if (any_spike) {
 #pragma unroll
-    for (int w = 0; w < 3; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const uint32_t a = wave_sum_u32(cF[w]), c = wave_min_u32(mnF[w]), d = wave_max_u32(mxF[w]);
       const uint32_t e = wave_sum_u32(cL[w]), f = wave_min_u32(mnL[w]), h = wave_max_u32(mxL[w]);
       if (lane == 0) {
@@ -963,26 +983,57 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
       }
     }
   }
-  if (__builtin_amdgcn_readfirstlane(nf)) {       // rare: split the non-finite count
-    nnan = wave_sum_u32(nnan);
-    nneg = wave_sum_u32(nneg);
-    npos = wave_sum_u32(npos);
-    if (lane == 0) {
-      if (nnan) atomicAdd(&S->nan_count, nnan);
-      if (nneg) atomicAdd(&S->ninf_neg, nneg);
-      if (npos) atomicAdd(&S->ninf_pos, npos);
-    }
+}
+
+template <bool SAME>
+__global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_t* cand, uint32_t cap, int B,
+                                                    Sweep sw) {
+  // thread = 4 columns c0 + j * kBlock + tid of a kTileW-column tile, walking down the block's
+  // R output rows.  The horizontal cv2 pass of a model row is a thread's own business (its 4
+  // columns), so it stays in registers.
+  __shared__ uint32_t sh[3][kStageW];               // staged window keys
+  __shared__ uint32_t red[kBlock / 64][24];
+  __shared__ uint32_t lcnt[3], gbase[3];
+  __shared__ Tap tys[kMaxSelRows];                  // the block's row taps (no global load in the row loop)
+  int b, chunk;
+  map_block(blockIdx.x, B, sw.nrb * sw.ntiles, b, chunk);
+  const int rb = chunk / sw.ntiles, c0 = (chunk - rb * sw.ntiles) * kTileW;
+  const int cw = min(kTileW, g.W - c0);
+  SelState* S = st + b;
+  if (S->phase != PH_INIT) return;
+  const int nwin = (int)S->nwin;
+  if (nwin == 0) return;                            // (no window: every target goes to k_sel_slow)
+  float vlo[3], vhi[3], vF[3], vL[3];
+  uint32_t spk[3];
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    vlo[w] = S->wvlo[w]; vhi[w] = S->wvhi[w]; vF[w] = S->wvF[w]; vL[w] = S->wvL[w];
+    spk[w] = w < nwin ? S->wspike[w] : 0u;
+  }
+  const int v0 = sw.row0 + rb * sw.R;
+  const int v1 = min(sw.row_end, v0 + sw.R);
+  if (threadIdx.x < 3) lcnt[threadIdx.x] = 0;
+  if (!SAME && (int)threadIdx.x < v1 - v0) tys[threadIdx.x] = g.yt[v0 + threadIdx.x];
+  __syncthreads();
+  switch (nwin) {
+    case 1: sweep_w_rows<SAME, 1>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, lcnt, vlo, vhi, vF, vL, spk); break;
+    case 2: sweep_w_rows<SAME, 2>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, lcnt, vlo, vhi, vF, vL, spk); break;
+    default: sweep_w_rows<SAME, 3>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, lcnt, vlo, vhi, vF, vL, spk); break;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t c = 0, mn = 0xffffffffu, mx = 0;
-    for (int w = 0; w < kBlock / 64; ++w) { c += red[w][0]; mn = min(mn, red[w][1]); mx = max(mx, red[w][2]); }
-    if (c) atomicAdd(&S->nonfinite_count, c);
-    if (mn != 0xffffffffu) atomicMin(&S->kmin, mn);
-    if (mx) atomicMax(&S->kmax, mx);
+    uint32_t c[4] = {0, 0, 0, 0};
+    for (int w = 0; w < kBlock / 64; ++w)
+      for (int i = 0; i < 4; ++i) c[i] += red[w][i];
+    if (c[0]) {
+      atomicAdd(&S->nonfinite_count, c[0]);
+      if (c[1]) atomicAdd(&S->nan_count, c[1]);
+      if (c[2]) atomicAdd(&S->ninf_neg, c[2]);
+      if (c[3]) atomicAdd(&S->ninf_pos, c[3]);
+    }
     for (int q = 0; q < nwin; ++q) {
       uint32_t bw = 0;
-      for (int w = 0; w < kBlock / 64; ++w) bw += red[w][3 + q];
+      for (int w = 0; w < kBlock / 64; ++w) bw += red[w][4 + q];
       if (bw) atomicAdd(&S->wbelow[q], bw);
       const uint32_t nq = min(lcnt[q], (uint32_t)kStageW);
       gbase[q] = nq ? atomicAdd(&S->ccount[q], nq) : 0u;
@@ -1056,8 +1107,9 @@ __device__ void pct_ranks(uint32_t n, uint32_t* rank) {
 }
 
 // np.percentile's linear interpolation between the keys of ranks i0 / i1 (keys[4]), then
-// app.py:198-206's branch choice.
-__device__ void finalize_pct(SelState& s, const uint32_t* keys) {
+// app.py:198-206's branch choice.  have_mm: s.kmin / s.kmax hold the map's finite key range (the
+// window path does not count it: it returns false, s unchanged, when the branch needs it).
+__device__ bool finalize_pct(SelState& s, const uint32_t* keys, bool have_mm = true) {
   const uint32_t n = s.n;
   const double qs[2] = {2.0 / 100.0, 98.0 / 100.0};
   double r[2];
@@ -1072,6 +1124,7 @@ __device__ void finalize_pct(SelState& s, const uint32_t* keys) {
   double p2 = r[0], p98 = r[1];
   int branch = 0;
   if (p98 <= p2) {                       // app.py:198-199
+    if (!have_mm) return false;
     p2 = (double)key2f(s.kmin);
     p98 = (double)key2f(s.kmax);
     branch = 1;
@@ -1089,6 +1142,7 @@ __device__ void finalize_pct(SelState& s, const uint32_t* keys) {
   s.p2 = p2;
   s.p98 = p98;
   s.phase = PH_DONE;
+  return true;
 }
 
 // n 32-bit words global -> LDS by global_load_lds (16 B per lane, 1 KiB per wave-instruction,
@@ -1137,25 +1191,60 @@ __device__ void cand_round(const uint32_t* keys, uint32_t c, uint32_t lo, uint32
 }
 
 // Exact keys of ranks[0..nt) among one slot's candidate keys, all inside [lo, hi]: one round
-// for every target of the slot, then per target on its bin (at most 1024 keys wide after
-// level 0, so one key per bin) until its interval is one key wide.  Block-wide; out, tl, tz,
-// tr are shared arrays of nt entries.
+// for every target of the slot; a target whose bin then holds at most kGatherMax keys is settled
+// by gathering them and counting ranks (one pass over the candidates), the rest narrow by further
+// rounds (at most 1024 keys wide after level 0, so one key per bin) until one key wide.
+// Block-wide; out, tl, tz, tr are shared arrays of nt entries.
+constexpr uint32_t kGatherMax = 256;
 __device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint32_t hi, const uint32_t* ranks, int nt,
                             uint32_t* out, uint32_t* lh, uint32_t* wsum, uint32_t* rbin, uint32_t* rrem,
                             uint32_t* tl, uint32_t* tz, uint32_t* tr) {
+  __shared__ uint32_t tn[kMaxTgt], gcnt;
   cand_round(keys, c, lo, hi, ranks, nt, lh, wsum, rbin, rrem);
   if (threadIdx.x == 0) {
     const uint32_t mult = bin_mult(lo, hi);
     for (int j = 0; j < nt; ++j) {
       bin_interval(rbin[j], lo, mult, lo, hi, tl[j], tz[j]);
       tr[j] = rrem[j];
+      tn[j] = lh[rbin[j]];
     }
   }
   __syncthreads();
-  // narrow every unresolved target; targets sharing an interval (the adjacent ranks i0, i0 + 1 of
-  // one percentile, usually) share each round
   uint32_t grank[kMaxTgt];
   int gidx[kMaxTgt];
+  // gather-and-count: the keys of a small bin into LDS (lh reused), then each key's rank range
+  for (int j = 0; j < nt; ++j) {
+    if (!(tl[j] < tz[j] && tn[j] <= kGatherMax)) continue;
+    const uint32_t l = tl[j], z = tz[j];
+    int ng = 0;
+    for (int k = j; k < nt; ++k)
+      if (tl[k] == l && tz[k] == z) { gidx[ng] = k; grank[ng++] = tr[k]; }
+    if (threadIdx.x == 0) gcnt = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < c; i += kBlock) {
+      const uint32_t k = keys[i];
+      if (k >= l && k <= z) {
+        const uint32_t pos = atomicAdd(&gcnt, 1u);
+        if (pos < kGatherMax) lh[pos] = k;
+      }
+    }
+    __syncthreads();
+    const uint32_t m = min(gcnt, kGatherMax);
+    for (uint32_t i = threadIdx.x; i < m; i += kBlock) {
+      const uint32_t k = lh[i];
+      uint32_t less = 0, leq = 0;
+      for (uint32_t q = 0; q < m; ++q) {
+        const uint32_t v = lh[q];
+        less += v < k ? 1u : 0u;
+        leq += v <= k ? 1u : 0u;
+      }
+      for (int q = 0; q < ng; ++q)
+        if (less <= grank[q] && grank[q] < leq) { tl[gidx[q]] = k; tz[gidx[q]] = k; }   // (equal keys: same value)
+    }
+    __syncthreads();
+  }
+  // narrow every unresolved target; targets sharing an interval (the adjacent ranks i0, i0 + 1 of
+  // one percentile, usually) share each round
   for (int j = 0; j < nt; ++j) {
     for (int it = 0; it < 4 && tl[j] < tz[j]; ++it) {
       const uint32_t l = tl[j], z = tz[j];
@@ -1282,6 +1371,45 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
       S->wspike[k] = f;
     }
     S->nwin = (uint32_t)nw;
+    for (int i = 0; i < 2 * nw; ++i) wb[i] = w[i];
+    tot = (uint32_t)nw;
+  }
+  __syncthreads();
+  // the windows as values for k_sweep_w: the first / last finite key of the window's bins, and of
+  // its first bin's end / last bin's start (spike split).  Each is the smallest finite key whose
+  // level-0 bin reaches a target (vbin is monotone in the key): a 64-way search per wave (each
+  // round every lane tests one key, the range shrinks 64x), searches spread over the waves.
+  const int nw = (int)tot;
+  const VBins vb = level0_vbins(S->rlo, S->rhi);
+  const uint64_t clo = kKeyNegInf + 1u, chi = kKeyPosInf - 1u;
+  for (int sidx = wv; sidx < 4 * nw; sidx += kBlock / 64) {
+    const int k = sidx >> 2, kind = sidx & 3;
+    const uint32_t lo = wb[2 * k], hi = wb[2 * k + 1];
+    const uint32_t target = kind == 0 ? lo : (kind == 1 ? hi + 1u : (kind == 2 ? lo + 1u : hi));
+    uint64_t a = clo, z = chi + 1;       // answer in [a, z]; z = chi + 1: no finite key reaches target
+    while (a < z) {
+      const uint64_t step = (z - a + 63) >> 6;
+      const uint64_t q = a + (uint64_t)lane * step;
+      const bool hit = q < z && vbin(key2f((uint32_t)q), vb) >= target;
+      const uint64_t m = __ballot(hit);
+      if (!m) {                          // every tested key short: past the last one tested
+        a += min<uint64_t>(63, (z - a - 1) / step) * step + 1;
+      } else {
+        const int f = __ffsll((unsigned long long)m) - 1;
+        const uint64_t qf = a + (uint64_t)f * step;
+        if (f == 0) z = a;               // (a itself reaches the target)
+        else { a = a + (uint64_t)(f - 1) * step + 1; z = qf; }
+      }
+    }
+    // a: smallest finite key with vbin >= target (chi + 1 if none)
+    const uint32_t key = (kind == 1 || kind == 2) ? (uint32_t)(a - 1) : (uint32_t)a;   // (kKeyPosInf: +inf)
+    if (lane == 0) {
+      const float v = key2f(key);
+      if (kind == 0) S->wvlo[k] = v;
+      if (kind == 1) S->wvhi[k] = v;
+      if (kind == 2) S->wvF[k] = v;
+      if (kind == 3) S->wvL[k] = v;
+    }
   }
 }
 
@@ -1321,12 +1449,10 @@ __device__ void fill_targets(SelState& s) {
   s.fill = 1;
 }
 
-// All targets resolved: p2 / p98 (and their branch) from the target keys.
-__device__ void finish_targets(SelState& s) {
-  if (!s.fill) {
-    finalize_pct(s, s.tlo);
-    return;
-  }
+// All targets resolved: p2 / p98 (and their branch) from the target keys (false: the
+// min / max branch without have_mm -- finalize_pct).
+__device__ bool finish_targets(SelState& s, bool have_mm = true) {
+  if (!s.fill) return finalize_pct(s, s.tlo, have_mm);
   const float a = key2f(s.tlo[8]), c = key2f(s.tlo[9]);
   const float med = s.med_ranks == 1 ? a : (a + c) / 2.0f;   // np.mean of the middle pair in float32
   s.med = med;
@@ -1335,14 +1461,14 @@ __device__ void finish_targets(SelState& s) {
     s.mode = 2;
     s.p2 = s.p98 = (double)med;
     s.phase = PH_DONE;
-    return;
+    return true;
   }
   const uint32_t mk = f2key(med);
   uint32_t pk[4];
   for (int t = 0; t < 4; ++t) pk[t] = s.tlo[t] < mk ? s.tlo[t] : (s.tlo[4 + t] > mk ? s.tlo[4 + t] : mk);
   s.kmin = min(s.kmin, mk);            // min / max of the filled map (app.py:198-199 branch)
   s.kmax = max(s.kmax, mk);
-  finalize_pct(s, pk);
+  return finalize_pct(s, pk, have_mm);
 }
 
 // One resolve per level (a workgroup per image): histogram slots -> the bin of each target
@@ -1728,19 +1854,22 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
   __shared__ uint32_t sc[kSlowBlock];
   __shared__ uint32_t red[2][kSlowBlock / 64];
   __shared__ uint32_t rbin, rrem, kmm[2], keys[4];
+  __shared__ int done;
   __shared__ SelState s;
   const int b = blockIdx.x;
   if (b >= B) return;
   if (threadIdx.x == 0) s = st[b];
   __syncthreads();
   if (s.phase == PH_INIT) {
-    // window path (k_sweep_w / k_resolve_w): every target resolved unless err
+    // window path (k_sweep_w / k_resolve_w): every target resolved unless err; the min / max
+    // branch (p98 <= p2: a near-constant map) is left to the slow path, which counts the range
     if (s.err == 0) {
       if (threadIdx.x == 0) {
-        finish_targets(s);
-        st[b] = s;
+        done = finish_targets(s, false) ? 1 : 0;
+        if (done) st[b] = s;
       }
-      return;
+      __syncthreads();
+      if (done) return;
     }
   } else if (s.phase != PH_SLOW) {
     return;

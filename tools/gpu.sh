@@ -125,6 +125,17 @@ case "$TASK" in
     timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/t -o t --output-format csv -- \
       python tools/bench_unproject.py ${1:-32} ${2:-high} > $D/bench.txt 2>&1 || { tail -5 $D/bench.txt; exit 1; }
     grep 'B=' $D/bench.txt; stats $D/t unproj ;;
+  sel-rows)   # k_sweep_w duration by output rows per workgroup (kernel trace only), then its SQ counters
+    for R in 8 16 32 64; do
+      D=gpurun_out/selrows_$R; rm -rf $D; mkdir -p $D
+      I2PC_SEL_ROWS=$R timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/t -o t --output-format csv -- \
+        python tools/bench_unproject.py 32 high > $D/bench.txt 2>&1 || { tail -5 $D/bench.txt; exit 1; }
+      echo "rows $R: $(grep -h 'B=32 high:' $D/bench.txt)"; stats $D/t k_sweep_w
+    done
+    D=gpurun_out/pmc_sw; rm -rf $D; mkdir -p $D
+    timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM --kernel-trace -d $D/p1 -o p1 --output-format csv -- python tools/bench_unproject.py 32 > $D/p1.txt 2>&1 || exit 1
+    timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA --kernel-trace -d $D/p2 -o p2 --output-format csv -- python tools/bench_unproject.py 32 > $D/p2.txt 2>&1 || exit 1
+    python tools/pmc_summary.py $D/p1 k_sweep_w && python tools/pmc_summary.py $D/p2 k_sweep_w ;;
   pmc-unp)
     D=gpurun_out/pmc_unp; rm -rf $D; mkdir -p $D
     timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -d $D/p1 -o p1 --output-format csv -- python tools/bench_unproject.py 32 > $D/p1.txt 2>&1 || exit 1
