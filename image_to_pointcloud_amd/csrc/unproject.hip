@@ -28,6 +28,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 #include <cmath>
@@ -238,6 +239,19 @@ __device__ Tap make_tap(int dx, int in, double scale) {
   return t;
 }
 
+// cv2 taps of output column u / row v (the vertical pass always uses two rows: the second
+// clamps to the last row) -- as k_prepare's tables
+__device__ __forceinline__ Tap xtap(const Geo& g, int u) {
+  Tap t = make_tap(u, g.dw, g.sx);
+  if (g.dw == 1) { t.i0 = 0; t.i1 = -1; t.w0 = 1.f; t.w1 = 0.f; }
+  return t;
+}
+__device__ __forceinline__ Tap ytap(const Geo& g, int v) {
+  Tap t = make_tap(v, g.dh, g.sy);
+  if (t.i1 < 0) t.i1 = t.i0;
+  return t;
+}
+
 // ---------------------------------------------------------------- selection
 //
 // Exact p2 / p98 ranks of the full-resolution map (np.percentile, app.py:197) by narrowing
@@ -361,7 +375,8 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
     if (t.i1 < 0) t.i1 = t.i0;
     yt[i] = t;
   }
-  for (size_t i = gtid; i < (size_t)B * kSlots * kBins; i += nthr) hist[i] = 0;
+  if (hist)        // (the level histograms: band path only)
+    for (size_t i = gtid; i < (size_t)B * kSlots * kBins; i += nthr) hist[i] = 0;
   if (trig) {       // equirectangular ray tables (the oracle evaluates the same expressions)
     const double pi = 3.141592653589793;
     for (int i = gtid; i < W + H; i += nthr) {
@@ -837,7 +852,9 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
   };
   auto interp = [&](const float (&q)[8], float (&h)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) h[j] = q[2 * j] * tx[j].w0 + q[2 * j + 1] * tx[j].w1;   // cv2 HResizeLinear
+    for (int j = 0; j < 4; ++j)     // cv2 HResizeLinear (a single-tap column: the raw value, as sample())
+      h[j] = !act[j] ? __builtin_nanf("")      // (past the tile: NaN, in no window, below none)
+                     : (tx[j].i1 < 0 ? q[2 * j] : q[2 * j] * tx[j].w0 + q[2 * j + 1] * tx[j].w1);
   };
   float cur[4];
   if (SAME) {
@@ -845,10 +862,7 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
     for (int j = 0; j < 4; ++j) cur[j] = Dimg[(size_t)v0 * g.dw + ucol[j]];
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      tx[j] = g.xt[ucol[j]];
-      if (!act[j]) tx[j].w0 = __builtin_nanf("");   // (interpolates to NaN)
-    }
+    for (int j = 0; j < 4; ++j) tx[j] = g.xt[ucol[j]];
     ra = tys[0].i0;
     float q0[8], q1[8];
     load_raw(ra, q0);
@@ -1683,6 +1697,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32
   __shared__ SelState s;
   const int b = blockIdx.x / 3, w = blockIdx.x % 3;
   if (b >= B) return;
+  auto body = [&]() {
   if (threadIdx.x == 0) s = st[b];
   __syncthreads();
   if (s.phase != PH_INIT) return;
@@ -1777,6 +1792,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32
     const int t = tq[threadIdx.x];
     S->tlo[t] = S->thi[t] = qk[threadIdx.x];
   }
+  };
+  body();
 }
 
 // Non-finite maps (app.py:194-196: NaN / +-Inf filled with np.nanmedian, then the
@@ -1858,6 +1875,12 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
   __shared__ SelState s;
   const int b = blockIdx.x;
   if (b >= B) return;
+  if (threadIdx.x == 0) {     // (usually done: only the phase is read)
+    const uint32_t ph = st[b].phase;
+    done = ph == PH_INIT || ph == PH_SLOW ? 0 : 1;
+  }
+  __syncthreads();
+  if (done) return;
   if (threadIdx.x == 0) s = st[b];
   __syncthreads();
   if (s.phase == PH_INIT) {
@@ -2159,17 +2182,6 @@ __global__ __launch_bounds__(kBlock) void k_unproject(Geo g, const SelState* st,
     if (k & 1) { if (x) atomicMax(dst, x); }
     else { if (x != 0xffffffffu) atomicMin(dst, x); }
   }
-}
-
-__device__ __forceinline__ Tap xtap(const Geo& g, int u) {
-  Tap t = make_tap(u, g.dw, g.sx);
-  if (g.dw == 1) { t.i0 = 0; t.i1 = -1; t.w0 = 1.f; t.w1 = 0.f; }
-  return t;
-}
-__device__ __forceinline__ Tap ytap(const Geo& g, int v) {
-  Tap t = make_tap(v, g.dh, g.sy);
-  if (t.i1 < 0) t.i1 = t.i0;
-  return t;
 }
 
 // Fast unprojection (no smoothing, N % 4 == 0, ceil(W/step) % 4 == 0, 3 channels):
@@ -2948,8 +2960,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   const int n = img_h * img_w;
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
   double* trig = params->projection == 1 ? reinterpret_cast<double*>(ws + L.trig) : nullptr;
-  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n, st, hist,
-                     rpart, xt, yt, dep_h, dep_w, img_h, img_w, cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig);
+  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n, st,
+                     (xch || !g_sel_windows) ? hist : nullptr, rpart, xt, yt, dep_h, dep_w, img_h, img_w, cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig);
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
@@ -3096,8 +3108,8 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
   Tap* yt = reinterpret_cast<Tap*>(ws + L.ytab);
   const int n = h * w;
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
-  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, n, n, st, hist, rpart, xt,
-                     yt, h, w, h, w, 1.0, 1.0, nullptr);
+  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, n, n, st,
+                     g_sel_windows ? nullptr : hist, rpart, xt, yt, h, w, h, w, 1.0, 1.0, nullptr);
   Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
   const Sweep ssel = plan_select(h, w, h, w, true, 0, h);
   int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart,

@@ -445,6 +445,10 @@ def _sel_cases():
     out["nan_inf"] = d
     d = base.copy(); d.ravel()[rng.permutation(d.size)[:d.size * 2 // 5]] = np.nan
     out["nan_40pct"] = d
+    # +-inf in the last model column and row: cv2's single-tap border copies them unblended, so the
+    # resized map holds +-inf there, not the NaN an inf * 0 weight would make
+    d = base.copy(); d[5:40, -1] = np.inf; d[-1, 7:30] = -np.inf
+    out["inf_border"] = d
     out["constant"] = np.full_like(base, 2.5)
     out["all_nan"] = np.full_like(base, np.nan)
     return out

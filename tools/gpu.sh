@@ -11,6 +11,7 @@
 #   bench                      the default bench line (with the CPU baseline), as the driver runs it
 #   ab-pipe [args]             tools/ab_pipeline.py: kernel-selection knobs A/B on the bench pipeline, one process
 #   census [args]              tools/gemm_census.py: every network launch with shape, kernel and rate
+#   gm                         census of the C2 network per GEMM tile-order GROUP_M (2, 4, 8, 16)
 #   ab-gemm                    GEMM engine tests + tools/bench_gemm_ab.py (engine modes, interleaved)
 #   unp                        geometry parity tests, unprojection microbench (warm / cold) per kernel variant
 #   trace-unp [B] [density]    kernel durations of the unprojection microbench (kernel trace only)
@@ -105,6 +106,12 @@ case "$TASK" in
         >> gpurun_out/stamps.txt 2>&1 || { tail -5 gpurun_out/stamps.txt; exit 1; }
     done
     cat gpurun_out/stamps.txt ;;
+  gm)         # GROUP_M of the GEMM tile order (an XCD's 32 concurrent tiles = GROUP_M x 32 / GROUP_M): census per value
+    for GM in 2 4 8 16; do
+      I2PC_GEMM_GM=$GM timeout -k 10 300 python -u tools/gemm_census.py --top 12 > gpurun_out/census_gm$GM.txt 2>&1 \
+        || { tail -5 gpurun_out/census_gm$GM.txt; exit 1; }
+      echo "== GM $GM"; grep -v amdgpu.ids gpurun_out/census_gm$GM.txt | head -16
+    done ;;
   ab-gemm)
     timeout -k 10 300 python -u -m pytest tests/test_gemm_engines_gpu.py -x -q --timeout 120 --timeout-method thread \
       > gpurun_out/eng.log 2>&1 || { tail -15 gpurun_out/eng.log; exit 1; }
