@@ -45,7 +45,8 @@ constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
 constexpr int kSlowBlock = 1024;
 constexpr int kRangeChunks = 32;
-constexpr int kSampleChunks = 8;    // k_model_hist workgroups (partial sample histograms) per image
+constexpr int kSampleChunks = 8;          // k_model_hist workgroups (partial sample histograms) per image
+constexpr int kHistBlock = 1024;          // k_model_hist: threads per (image, chunk) workgroup (~8 samples each)
 // Level 0 bins values (one bin ~ up to 2^31 keys near 0); levels 1-3 bin keys 2048 ways each:
 // 2^31 -> 2^20 -> 2^9 -> 1 key, so the last level always resolves.
 constexpr int kLastLevel = 3;
@@ -425,13 +426,13 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
 // one partial histogram per (image, chunk) in `mhist` [B][kSampleChunks][kBins], summed by k_window
 // (no global atomics: every chunk's workgroup sees most bins of its image).  The estimate k_window
 // predicts the target bins from.
-__global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* mhist,
+__global__ __launch_bounds__(kHistBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* mhist,
                                                        const uint32_t* rpart, int stride) {
   __shared__ __attribute__((aligned(16))) uint32_t lh[kBins];
   __shared__ uint32_t rr[2];
   const int b = blockIdx.x % B, c = blockIdx.x / B;
   SelState* S = st + b;
-  for (int i = threadIdx.x; i < kBins; i += kBlock) lh[i] = 0;
+  for (int i = threadIdx.x; i < kBins; i += kHistBlock) lh[i] = 0;
   if (threadIdx.x < 64) {     // the image's key range from k_prepare's partials
     uint32_t lo = 0xffffffffu, hi = 0u;
     if (threadIdx.x < kRangeChunks) {
@@ -456,7 +457,7 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   const int nsx = (g.W + stride - 1) / stride, nsy = (g.H + stride - 1) / stride, ns = nsx * nsy;
   const int per = (ns + kSampleChunks - 1) / kSampleChunks;
   const int i0 = c * per, i1 = min(ns, i0 + per);
-  const int tper = (per + kBlock - 1) / kBlock;
+  const int tper = (per + kHistBlock - 1) / kHistBlock;
   const int t0 = i0 + threadIdx.x * tper, t1 = min(i1, t0 + tper);
   int run = -1;
   uint32_t cnt = 0;
@@ -527,7 +528,7 @@ __global__ __launch_bounds__(kBlock) void k_model_hist(Geo g, int B, SelState* s
   __syncthreads();
   uint4* gh = reinterpret_cast<uint4*>(mhist + ((size_t)b * kSampleChunks + c) * kBins);
   const uint4* l4 = reinterpret_cast<const uint4*>(lh);
-  for (int i = threadIdx.x; i < kBins / 4; i += kBlock) gh[i] = l4[i];
+  for (int i = threadIdx.x; i < kBins / 4; i += kHistBlock) gh[i] = l4[i];
 }
 
 // Block histogram in LDS as packed 16-bit counts (bin pairs share a word; a sweep workgroup
@@ -2858,7 +2859,7 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
   // full-resolution sample of ~64 K points per image for the level-0 estimate
   const int stride = std::max(1, (int)std::sqrt((double)g.H * g.W / 65536.0));
   const int ns = ((g.H + stride - 1) / stride) * ((g.W + stride - 1) / stride);
-  hipLaunchKernelGGL(k_model_hist, dim3(B * kSampleChunks), dim3(kBlock), 0, s, g, B, st, mhist, rpart, stride);
+  hipLaunchKernelGGL(k_model_hist, dim3(B * kSampleChunks), dim3(kHistBlock), 0, s, g, B, st, mhist, rpart, stride);
   hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, mhist, cap, B, x ? 0 : 1, ns);
   if (!x && g_sel_windows) {
     // batch path: one window-only sweep + resolve; k_sel_slow finishes (or, for the rare image
