@@ -1,6 +1,6 @@
 // Device-side collectives of the tile-parallel panorama mode (BASELINE configs[3]):
-// an RCCL communicator owned by the C ABI, and the band unprojection whose histogram /
-// counter exchange is three RCCL all-reduces on the call's own stream -- no host callback,
+// an RCCL communicator owned by the C ABI, and the band unprojection whose counter exchange
+// (RCCL all-reduces) and window-candidate all-gather run on the call's own stream -- no host callback,
 // so a whole band call (sweeps, all-reduces, unprojection) can be captured into a HIP graph.
 //   i2pc_comm_unique_id / i2pc_comm_create / i2pc_comm_destroy : ncclGetUniqueId /
 //       ncclCommInitRank / ncclCommDestroy (the caller ships the 128-byte id from rank 0 to
@@ -24,7 +24,8 @@ int rccl_exchange(void* user, uint32_t* hist, int64_t hist_words, int64_t* count
   auto* c = static_cast<i2pc_comm*>(user);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (ncclGroupStart() != ncclSuccess) return 1;
-  ncclResult_t r = ncclAllReduce(hist, hist, (size_t)hist_words, ncclUint32, ncclSum, c->comm, s);
+  ncclResult_t r = hist_words > 0 ? ncclAllReduce(hist, hist, (size_t)hist_words, ncclUint32, ncclSum, c->comm, s)
+                                  : ncclSuccess;
   if (r == ncclSuccess && counters) {
     r = ncclAllReduce(counters, counters, 2 * (size_t)batch, ncclInt64, ncclSum, c->comm, s);
     if (r == ncclSuccess) r = ncclAllReduce(counters + 2 * batch, counters + 2 * batch, batch, ncclInt64, ncclMin, c->comm, s);
@@ -33,6 +34,17 @@ int rccl_exchange(void* user, uint32_t* hist, int64_t hist_words, int64_t* count
   const ncclResult_t e = ncclGroupEnd();
   if (r != ncclSuccess || e != ncclSuccess) {
     i2pc::set_error(I2PC_ELAUNCH, "RCCL all-reduce failed: %s", ncclGetErrorString(r != ncclSuccess ? r : e));
+    return 1;
+  }
+  return 0;
+}
+
+// the window-selection band mode's candidate lists: every rank's `words` into recv [nranks][words]
+int rccl_gather(void* user, const uint32_t* send, uint32_t* recv, int64_t words, void* stream) {
+  auto* c = static_cast<i2pc_comm*>(user);
+  const ncclResult_t r = ncclAllGather(send, recv, (size_t)words, ncclUint32, c->comm, static_cast<hipStream_t>(stream));
+  if (r != ncclSuccess) {
+    i2pc::set_error(I2PC_ELAUNCH, "RCCL all-gather failed: %s", ncclGetErrorString(r));
     return 1;
   }
   return 0;
@@ -77,6 +89,8 @@ extern "C" int i2pc_unproject_band_rccl(const float* depth, int dep_h, int dep_w
                                         i2pc_comm* comm, void* stream) {
   clear_error();
   I2PC_REQUIRE(comm != nullptr, "comm is NULL");
-  return i2pc_unproject_band(depth, dep_h, dep_w, image_band, channels, img_h, img_w, row0, row1, params, xyz_band,
-                             rgb_band, bbox, stats, workspace, workspace_bytes, rccl_exchange, comm, stream);
+  // window selection: one sweep, then the counters all-reduced and the candidate lists all-gathered
+  return i2pc_unproject_band_w(depth, dep_h, dep_w, image_band, channels, img_h, img_w, row0, row1, params, xyz_band,
+                               rgb_band, bbox, stats, workspace, workspace_bytes, comm->nranks, rccl_exchange,
+                               rccl_gather, comm, stream);
 }

@@ -45,7 +45,8 @@ constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
 constexpr int kSlowBlock = 1024;
 constexpr int kRangeChunks = 32;
-constexpr int kSampleChunks = 8;          // k_model_hist workgroups (partial sample histograms) per image
+constexpr int kSampleChunks = 8;          // k_model_hist workgroups (partial sample histograms) per image, at least
+constexpr int kMaxSampleChunks = 128;     // ... at most (large images: up to ~1 M samples, 8 K per workgroup)
 constexpr int kHistBlock = 1024;          // k_model_hist: threads per (image, chunk) workgroup (~8 samples each)
 // Level 0 bins values (one bin ~ up to 2^31 keys near 0); levels 1-3 bin keys 2048 ways each:
 // 2^31 -> 2^20 -> 2^9 -> 1 key, so the last level always resolves.
@@ -57,6 +58,14 @@ constexpr int kSlotWords = kBins / 2;   // sweep LDS per slot: 2048 packed 16-bi
 constexpr int kHrowBudget = 40 * 1024;   // LDS bytes of staged + horizontally interpolated model rows
 constexpr int kStageW = 1024;            // k_sweep_w: window keys a workgroup stages in LDS per window
 constexpr int kMaxSelRows = 64;          // k_sweep_w: output rows per workgroup at most
+// window-selection band runs (C4): after the window sweep each band bins its window keys into
+// kBins fine bins per window (all-reduced), then hands over only the keys of each target's fine
+// bin: per target slot its count, min / max key and up to kPick keys (the all-gather)
+constexpr int kPick = 1024;
+constexpr int kPickWords = 3 + kPick;
+constexpr int kBandWords = kMaxTgt * kPickWords;
+constexpr int kBandEx = 8;               // row length of the window exchange's int64 [4][8] counters
+constexpr int kMaxBandRanks = 256;
 
 // PH_INIT: level-0 sweep pending; PH_SEL: targets being narrowed; PH_SLOW: handed to
 // k_sel_slow (non-finite map); PH_DONE: p2 / p98 / mode final.
@@ -108,7 +117,9 @@ struct alignas(16) SelState {
   // window w as values (k_window): finite values < wvlo[w] lie below it, values in [wvlo, wvhi]
   // inside; a spike first bin ends at wvF[w], a spike last bin starts at wvL[w]
   float wvlo[3], wvhi[3], wvF[3], wvL[3];
+  uint32_t twin[kMaxTgt];  // window-selection band runs: the window of target t's fine bin
 };
+static_assert(sizeof(SelState) == 624, "tools/sel_diag.py mirrors this layout");
 
 // Correctly rounded a / b from r = RN(1 / b) (Markstein's correction: q0 = RN(a r),
 // rem = a - q0 b exactly by FMA, q = RN(q0 + rem r)).  Three FP64 ops instead of the
@@ -133,17 +144,36 @@ struct Geo {
 inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
-  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, mhist, field, tmp, total;
+  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, mhist, gsend, grecv, field, tmp, total;
   uint32_t cap;   // candidate keys per slot and image (compaction sweeps)
 };
 
 // Candidate capacity per target interval: a level-0 bin holds ~n / 2048 keys on average, so
 // n / 64 leaves a 32x margin for dense bins before the slower histogram level is taken.
 static uint32_t cand_cap(int64_t n) {
-  return (uint32_t)std::min<int64_t>(1 << 18, std::max<int64_t>(4096, n / 64)) / 256 * 256;   // DMA-able slots
+  return (uint32_t)std::min<int64_t>(1 << 20, std::max<int64_t>(4096, n / 64)) / 256 * 256;   // DMA-able slots
 }
 
-static Layout layout(int B, int H, int W, int smooth) {
+// nranks > 0: a window-selection band run's all-gather buffers (send: one band's
+// kBandWords, receive: nranks of them; the fine histograms use the level histograms' slots)
+// The full-resolution sample k_model_hist bins: a jittered lattice of stride `stride` (ns
+// points), nch partial histograms.  64 K points for images up to 2 M pixels; larger images
+// sample n / 32 (at most ~1 M points), so the windows' sampling noise -- n / sqrt(ns) keys --
+// stays a few tens of thousands of keys (an 8192 x 4096 panorama: ~1.1 M points).
+struct SamplePlan {
+  int stride, ns, nch;
+};
+static SamplePlan sample_plan(int H, int W) {
+  const double n = (double)H * W;
+  const double target = std::min(1048576.0, std::max(65536.0, n / 32.0));
+  SamplePlan sp;
+  sp.stride = std::max(1, (int)std::sqrt(n / target));
+  sp.ns = ((H + sp.stride - 1) / sp.stride) * ((W + sp.stride - 1) / sp.stride);
+  sp.nch = std::min(kMaxSampleChunks, std::max(kSampleChunks, (sp.ns + 8191) / 8192));
+  return sp;
+}
+
+static Layout layout(int B, int H, int W, int smooth, int nranks = 0) {
   Layout L{};
   size_t off = 0;
   L.cap = cand_cap((int64_t)H * W);
@@ -154,8 +184,10 @@ static Layout layout(int B, int H, int W, int smooth) {
   L.xtab = off;  off = align_up(off + sizeof(Tap) * (size_t)W, 256);
   L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
   L.trig = off;  off = align_up(off + sizeof(double) * 2 * ((size_t)W + H), 256);
-  L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)B, 256);
-  L.mhist = off; off = align_up(off + sizeof(uint32_t) * kSampleChunks * kBins * (size_t)B, 256);
+  L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)std::max(B, kBandEx), 256);
+  L.mhist = off; off = align_up(off + sizeof(uint32_t) * sample_plan(H, W).nch * kBins * (size_t)B, 256);
+  L.gsend = off; off = align_up(off + (nranks > 0 ? sizeof(uint32_t) * kBandWords : 0), 256);
+  L.grecv = off; off = align_up(off + sizeof(uint32_t) * kBandWords * (size_t)std::max(nranks, 0), 256);
   L.field = off;
   if (smooth) {
     off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
@@ -362,6 +394,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
     s.rhi = 0u;
     for (int i = 0; i < 6; i += 2) { s.bbox_key[i] = 0xffffffffu; s.bbox_key[i + 1] = 0u; }
     for (int w = 0; w < 3; ++w) { s.wminF[w] = s.wminL[w] = 0xffffffffu; }
+    for (int t = 0; t < kMaxTgt; ++t) s.tslot[t] = kNoSlot;
     s.med = __uint_as_float(0x7fc00000u);
     st[gtid] = s;
   }
@@ -427,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
 // (no global atomics: every chunk's workgroup sees most bins of its image).  The estimate k_window
 // predicts the target bins from.
 __global__ __launch_bounds__(kHistBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* mhist,
-                                                       const uint32_t* rpart, int stride) {
+                                                       const uint32_t* rpart, int stride, int nch) {
   __shared__ __attribute__((aligned(16))) uint32_t lh[kBins];
   __shared__ uint32_t rr[2];
   const int b = blockIdx.x % B, c = blockIdx.x / B;
@@ -449,49 +482,40 @@ __global__ __launch_bounds__(kHistBlock) void k_model_hist(Geo g, int B, SelStat
   }
   __syncthreads();
   const VBins vb = level0_vbins(rr[0], rr[1]);
-  // the histogram of a regular sample of the FULL-resolution map (every stride-th row and
-  // column, values recomputed with the cv2 taps): its quantiles are the full map's up to
-  // sampling noise, unlike the model pixels' (a zero floor of isolated model pixels all but
-  // vanishes in the resize).  Each thread bins a contiguous run of samples (neighbours share
-  // bins: one LDS atomic per run), 8 samples' loads in flight at a time.
+  // the histogram of a stratified random sample of the FULL-resolution map (values recomputed
+  // with the cv2 taps): one point per cell at a hashed offset (lowbias32 of the cell index), so
+  // its quantiles are the full map's up to sampling noise, unlike the model
+  // pixels' (a zero floor of isolated model pixels all but vanishes in the resize).  A lattice
+  // with a deterministic jitter aliased with the resize's tap phases: on a noisy 518 x 1036 map
+  // upsampled 7.9x its p2 was 10 standard deviations off (phase-0 pixels, the raw model values,
+  // make the tails).  Each thread walks a run of consecutive cells (neighbours share bins: one
+  // LDS atomic per run), 8 samples' loads in flight at a time.
   const int nsx = (g.W + stride - 1) / stride, nsy = (g.H + stride - 1) / stride, ns = nsx * nsy;
-  const int per = (ns + kSampleChunks - 1) / kSampleChunks;
+  const int per = (ns + nch - 1) / nch;
   const int i0 = c * per, i1 = min(ns, i0 + per);
   const int tper = (per + kHistBlock - 1) / kHistBlock;
   const int t0 = i0 + threadIdx.x * tper, t1 = min(i1, t0 + tper);
   int run = -1;
   uint32_t cnt = 0;
-  // lattice position of sample t0, then stepped (no division per sample): the jitter offsets
-  // jy = (7 sx + 3 sy) mod stride, jx = (5 sy + 3 sx) mod stride advance by 7 / 3 per column
   int sy = t0 / nsx, sx = t0 - sy * nsx;
-  int jy = (sx * 7 + sy * 3) % stride, jx = (sy * 5 + sx * 3) % stride;
-  const int d7 = 7 % stride, d3 = 3 % stride;
-  auto step = [&]() {
-    if (++sx == nsx) {
-      sx = 0;
-      ++sy;
-      jy = (sy * 3) % stride;
-      jx = (sy * 5) % stride;
-    } else {
-      jy += d7; jy -= jy >= stride ? stride : 0;
-      jx += d3; jx -= jx >= stride ? stride : 0;
-    }
-  };
+  // cells of H / nsy x W / nsx pixels exactly (integer strides would leave a partial last cell
+  // whose few rows get a whole cell's weight: the image's border, often extreme, over-sampled)
+  const float cy = (float)g.H / (float)nsy, cx = (float)g.W / (float)nsx;
   for (int i = t0; i < t1; i += 8) {
     int py[8], px[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {       // (past t1: a repeat of the last sample, not counted)
-      py[k] = min(sy * stride + jy, g.H - 1);
-      px[k] = min(sx * stride + jx, g.W - 1);
-      if (i + k + 1 < t1) step();
+      uint32_t h = (uint32_t)min(i + k, t1 - 1);
+      h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
+      py[k] = min((int)(((float)sy + (float)(h & 0xffffu) * (1.f / 65536.f)) * cy), g.H - 1);
+      px[k] = min((int)(((float)sx + (float)(h >> 16) * (1.f / 65536.f)) * cx), g.W - 1);
+      if (i + k + 1 < t1 && ++sx == nsx) { sx = 0; ++sy; }
     }
     float v[8];
     if (g.same) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = sample(g, b, py[k], px[k]);
     } else {
-      // jittered lattice: the offset inside each stride x stride cell cycles with the cell, so
-      // every residue of the cv2 tap pattern (single-tap columns/rows included) is sampled
       Tap ty[8], tx[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -526,7 +550,7 @@ __global__ __launch_bounds__(kHistBlock) void k_model_hist(Geo g, int B, SelStat
   }
   if (run >= 0) atomicAdd(&lh[run], cnt);
   __syncthreads();
-  uint4* gh = reinterpret_cast<uint4*>(mhist + ((size_t)b * kSampleChunks + c) * kBins);
+  uint4* gh = reinterpret_cast<uint4*>(mhist + ((size_t)b * nch + c) * kBins);
   const uint4* l4 = reinterpret_cast<const uint4*>(lh);
   for (int i = threadIdx.x; i < kBins / 4; i += kHistBlock) gh[i] = l4[i];
 }
@@ -1288,7 +1312,7 @@ __device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint3
 // window did not overflow), the level-0 resolve selects the exact key from those candidates
 // and the later levels are no-ops; otherwise they run as usual.  Consumes histogram slot 3.
 __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t* mhist, uint32_t cap, int B,
-                                                   int enable, int m) {
+                                                   int enable, int m, int nch) {
   __shared__ __attribute__((aligned(16))) uint32_t mh[kBins];
   __shared__ uint32_t wsum[kBlock / 64], wb[6], tot;
   const int b = blockIdx.x;
@@ -1298,10 +1322,10 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
   uint32_t local = 0;
   {
     static_assert(kBins == 8 * kBlock, "k_window: 8 bins per thread");
-    const uint4* src = reinterpret_cast<const uint4*>(mhist + (size_t)b * kSampleChunks * kBins) + 2 * threadIdx.x;
+    const uint4* src = reinterpret_cast<const uint4*>(mhist + (size_t)b * nch * kBins) + 2 * threadIdx.x;
     uint4 acc0 = make_uint4(0, 0, 0, 0), acc1 = make_uint4(0, 0, 0, 0);
 #pragma unroll 8
-    for (int c = 0; c < kSampleChunks; ++c) {
+    for (int c = 0; c < nch; ++c) {
       const uint4 x = src[c * (kBins / 4)], y = src[c * (kBins / 4) + 1];
       acc0.x += x.x; acc0.y += x.y; acc0.z += x.z; acc0.w += x.w;
       acc1.x += y.x; acc1.y += y.y; acc1.z += y.z; acc1.w += y.w;
@@ -1342,17 +1366,26 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
   uint32_t off = 0;
   for (int i = 0; i < wv; ++i) off += wsum[i];
   double cum = (double)(x + off - seg);   // exclusive prefix of this thread's first bin
+  // half-width of window k in sample counts: the candidate budget, but at least 4.5 standard
+  // deviations of the sample's rank of the quantile (large images: a sample point stands for
+  // hundreds of keys), at most 0.8 of a candidate list
+  double hks[3];
+  for (int k = 0; k < nq; ++k) {
+    const double q = k == 0 ? 0.02 : (k == nq - 1 ? 0.98 : 0.5);
+    hks[k] = fmin(fmax(h, 4.5 * sqrt((double)mtot * q * (1.0 - q)) + 1.0), 0.4 * (double)cap / scale);
+  }
   for (int k = 0; k < nq; ++k) {
     const double q = k == 0 ? 0.02 : (k == nq - 1 ? 0.98 : 0.5);
     const double r = floor((double)(mtot - 1) * q);
+    const double hk = hks[k];
     double c = cum;
     for (int i = 0; i < per; ++i) {
       const int bn = threadIdx.x * per + i;
       const double c1 = c + mh[bn];
       // a bin that alone outgrows the window (a spike such as the zero floor) stays out of it
       // unless it holds the rank itself (then no window can help; the levels take over)
-      const bool fits = (double)mh[bn] * scale <= (double)kWinKeys || (c <= r && r < c1);
-      if (c1 > r - h && c <= r + h && fits) { atomicMin(&wb[2 * k], (uint32_t)bn); atomicMax(&wb[2 * k + 1], (uint32_t)bn); }
+      const bool fits = (double)mh[bn] <= 2.0 * hk || (c <= r && r < c1);
+      if (c1 > r - hk && c <= r + hk && fits) { atomicMin(&wb[2 * k], (uint32_t)bn); atomicMax(&wb[2 * k + 1], (uint32_t)bn); }
       c = c1;
     }
   }
@@ -1361,15 +1394,18 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
     // ascending windows; overlapping neighbours merge (touching ones stay apart, so a spike
     // bin stays at a window's end)
     uint32_t w[6];
+    double lim[3];                   // spike limit of each window: more samples than its full width
     int nw = 0;
     for (int k = 0; k < nq; ++k) {
       const uint32_t lo = wb[2 * k], hi = wb[2 * k + 1];
       if (lo > hi) continue;
       if (nw > 0 && lo <= w[2 * nw - 1]) {
         w[2 * nw - 1] = max(w[2 * nw - 1], hi);
+        lim[nw - 1] = fmax(lim[nw - 1], 2.0 * hks[k]);
       } else {
         w[2 * nw] = lo;
         w[2 * nw + 1] = hi;
+        lim[nw] = 2.0 * hks[k];
         ++nw;
       }
     }
@@ -1381,8 +1417,8 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
     for (int k = 0; k < nw; ++k) {
       const uint32_t lo = w[2 * k], hi = w[2 * k + 1];
       uint32_t f = 0;
-      if ((double)mh[lo] * scale > (double)kWinKeys) f |= 1u;
-      if (hi > lo && (double)mh[hi] * scale > (double)kWinKeys) f |= 2u;
+      if ((double)mh[lo] > lim[k]) f |= 1u;
+      if (hi > lo && (double)mh[hi] > lim[k]) f |= 2u;
       S->wspike[k] = f;
     }
     S->nwin = (uint32_t)nw;
@@ -2577,18 +2613,22 @@ __global__ __launch_bounds__(kBlock) void k_unproject_rows(Geo g, const SelState
   }
 }
 
-// Smooth path (app.py:209-214): materialise the normalised field, blur, unproject.
-__global__ void k_norm_field(Geo g, const SelState* st, int B, int invert, double* field) {
+// Smooth path (app.py:209-214): materialise the normalised field, blur, unproject.  The field
+// is addressed as the whole image; a band run (C4) fills only image rows [r0, r1): its band
+// plus the blur's halo, recomputed from the model-resolution depth every rank holds, so
+// smoothing needs no exchange beyond the selection's.
+__global__ void k_norm_field(Geo g, const SelState* st, int B, int invert, double* field, int r0, int r1) {
   const size_t n = (size_t)g.H * g.W;
-  const size_t total = n * B;
+  const size_t nr = (size_t)(r1 - r0) * g.W;
+  const size_t total = nr * B;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int b = (int)(i / n);
-    const int p = (int)(i - (size_t)b * n);
-    const int v = p / g.W, u = p - v * g.W;
+    const int b = (int)(i / nr);
+    const int p = (int)(i - (size_t)b * nr);
+    const int v = r0 + p / g.W, u = p % g.W;
     const SelState* S = st + b;
     float val = sample(g, b, v, u);
     if (S->has_med && !isfinite(val)) val = S->med;
-    field[i] = normalize(val, load_norm(S, invert));
+    field[(size_t)b * n + (size_t)v * g.W + u] = normalize(val, load_norm(S, invert));
   }
 }
 
@@ -2608,16 +2648,19 @@ struct BlurTaps {
 };
 
 // Tap-order accumulation (k taps, BORDER_REFLECT_101) in the branch dtype (float64 for
-// mode 0, float32 with float32 taps otherwise).
+// mode 0, float32 with float32 taps otherwise).  Output rows [r0, r1) of every image.
 template <bool kRows>
-__global__ void k_blur(const double* src, double* dst, const SelState* st, int B, int H, int W, BlurTaps taps) {
+__global__ void k_blur(const double* src, double* dst, const SelState* st, int B, int H, int W, BlurTaps taps,
+                       int r0, int r1) {
   const size_t n = (size_t)H * W;
-  const size_t total = n * B;
+  const size_t nr = (size_t)(r1 - r0) * W;
+  const size_t total = nr * B;
   const int r = taps.k / 2;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int b = (int)(i / n);
-    const int p = (int)(i - (size_t)b * n);
-    const int v = p / W, u = p - v * W;
+  for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < total; j += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(j / nr);
+    const int p = (int)(j - (size_t)b * nr);
+    const int v = r0 + p / W, u = p % W;
+    const size_t i = (size_t)b * n + (size_t)v * W + u;
     const double* s = src + (size_t)b * n;
     if (st[b].mode == 0) {
       double acc = 0.0;
@@ -2635,6 +2678,12 @@ __global__ void k_blur(const double* src, double* dst, const SelState* st, int B
       dst[i] = (double)acc;
     }
   }
+}
+
+static int reflect101_host(int i, int n) {
+  if (n == 1) return 0;
+  while ((unsigned)i >= (unsigned)n) i = i < 0 ? -i : 2 * (n - 1) - i;
+  return i;
 }
 
 static BlurTaps gaussian_taps(int k) {
@@ -2783,10 +2832,292 @@ __global__ void k_band_import(SelState* st, int B, const int64_t* ex) {
   }
 }
 
+// Window-selection band runs (C4).  After k_sweep_w over its band, a rank holds its band's
+// window keys (local candidate lists), below-window counts, spike counts and non-finite
+// counts.  1) k_bandw_hist: per window a kBins-bin histogram of the local keys over the
+// window's key range (the same range on every rank: the windows come from the whole image's
+// sample) and the counters as int64 [4][kBandEx] (rows 0-1 SUM, row 2 MIN, row 3 MAX) -> one
+// all-reduce.  2) k_bandw_pick: from the SUMMED counts every rank derives the same targets and,
+// for a target in a window's compacted part, its fine bin and its rank inside the bin; the local
+// keys of that bin (count, min, max, up to kPick keys) go to the target's slot -> one all-gather.
+// 3) k_bandw_final: each target's bin keys of every band merged, the exact key selected.
+// A bin holding more than kPick keys in one band (and more than one distinct key), or a target
+// outside every window, sets `err`: every rank then selects the whole image from scratch in
+// k_sel_slow (identical decisions everywhere: the inputs are identical on every rank).
+__device__ __forceinline__ void window_keys(const SelState& s, int w, uint32_t& k0, uint32_t& k1) {
+  k0 = f2key(s.wvlo[w]);
+  k1 = f2key(s.wvhi[w]);
+  if (k1 < k0) k1 = k0;
+}
+
+constexpr int kBandSplit = 32;   // workgroups per window of the band histogram / compaction passes
+
+__global__ __launch_bounds__(kBlock) void k_bandw_hist(const SelState* st, const uint32_t* cand, uint32_t cap,
+                                                       uint32_t* hist, int64_t* ex) {
+  __shared__ uint32_t lh[kBins];
+  const int w = blockIdx.x % 3, j = blockIdx.x / 3;
+  const SelState& s = st[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int64_t* e = ex;
+    e[0] = s.nonfinite_count; e[1] = s.nan_count; e[2] = s.ninf_neg; e[3] = s.ninf_pos;
+    for (int q = 0; q < 3; ++q) {
+      e[4 + q] = s.wbelow[q];
+      e[8 + q] = s.wcntF[q];
+      e[11 + q] = s.wcntL[q];
+      e[16 + q] = s.wminF[q];
+      e[19 + q] = s.wminL[q];
+      e[24 + q] = s.wmaxF[q];
+      e[27 + q] = s.wmaxL[q];
+    }
+    e[7] = e[14] = e[15] = 0;
+    e[22] = e[23] = 0xffffffffll;
+    e[30] = e[31] = 0;
+  }
+  if (w >= (int)s.nwin) return;
+  const uint32_t c = min(s.ccount[w], cap);
+  const uint32_t i0 = (uint32_t)((uint64_t)c * j / kBandSplit), i1 = (uint32_t)((uint64_t)c * (j + 1) / kBandSplit);
+  if (i0 == i1) return;
+  for (int i = threadIdx.x; i < kBins; i += kBlock) lh[i] = 0;
+  __syncthreads();
+  uint32_t k0, k1;
+  window_keys(s, w, k0, k1);
+  const uint32_t mult = bin_mult(k0, k1);
+  const uint32_t* keys = cand + (size_t)w * cap;
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += kBlock) atomicAdd(&lh[bin_of(keys[i], k0, mult)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += kBlock)      // (hist zeroed by k_prepare)
+    if (lh[i]) atomicAdd(&hist[(size_t)w * kBins + i], lh[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bandw_pick(SelState* st, const uint32_t* cand, uint32_t cap,
+                                                       const uint32_t* hist, const int64_t* ex, uint32_t* send) {
+  __shared__ SelState s;
+  __shared__ uint32_t qr[kMaxTgt], rbin[kMaxTgt], rrem[kMaxTgt], wsum[kBlock / 64];
+  __shared__ uint32_t sl[kMaxTgt], sz[kMaxTgt];
+  __shared__ int tq[kMaxTgt], slot[kMaxTgt], nc, fail, nslot;
+  const int w = blockIdx.x;
+  SelState* S = st;
+  if (threadIdx.x == 0) {
+    s = st[0];
+    const uint32_t local = s.ccount[w];
+    const int64_t* e = ex;
+    s.nonfinite_count = (uint32_t)e[0]; s.nan_count = (uint32_t)e[1];
+    s.ninf_neg = (uint32_t)e[2]; s.ninf_pos = (uint32_t)e[3];
+    for (int q = 0; q < 3; ++q) {
+      s.wbelow[q] = (uint32_t)e[4 + q];
+      s.wcntF[q] = (uint32_t)e[8 + q];
+      s.wcntL[q] = (uint32_t)e[11 + q];
+      s.wminF[q] = (uint32_t)e[16 + q];
+      s.wminL[q] = (uint32_t)e[19 + q];
+      s.wmaxF[q] = (uint32_t)e[24 + q];
+      s.wmaxL[q] = (uint32_t)e[27 + q];
+    }
+    fail = local > cap ? 1 : 0;          // this band's list overflowed: its histogram is short
+    nc = 0;
+    nslot = 0;
+  }
+  __syncthreads();
+  // summed compacted count of every window (each workgroup needs all of them to place targets)
+  __shared__ uint32_t ctot[3];
+  if (threadIdx.x < 64) {
+    for (int q = 0; q < 3; ++q) {
+      uint32_t a = 0;
+      if (q < (int)s.nwin)
+        for (int i = threadIdx.x; i < kBins; i += 64) a += hist[(size_t)q * kBins + i];
+      a = wave_sum_u32(a);
+      if (threadIdx.x == 0) ctot[q] = a;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool done = false;
+    if (s.nonfinite_count == 0) {
+      pct_ranks(s.n, s.rank);
+      s.ntgt = 4;
+      for (int t = 0; t < 4; ++t) { s.tlo[t] = 0; s.thi[t] = 0xffffffffu; }
+    } else if (s.nan_count == s.n) {     // all-NaN: nanmedian is NaN, every value stays NaN
+      if (w == 0) {
+        S->has_med = 1;
+        S->mode = 2;
+        S->p2 = S->p98 = (double)__uint_as_float(0x7fc00000u);
+        S->phase = PH_DONE;
+      }
+      done = true;
+    } else {
+      fill_targets(s);
+    }
+    if (!done) {
+      if (w == 0) {
+        S->ntgt = s.ntgt;
+        S->fill = s.fill;
+        S->med_ranks = s.med_ranks;
+        S->nonfinite_count = s.nonfinite_count;
+        S->nan_count = s.nan_count;
+        for (int t = 0; t < (int)s.ntgt; ++t)     // (the others belong to their window's workgroup)
+          if (s.tlo[t] == s.thi[t]) { S->tlo[t] = s.tlo[t]; S->thi[t] = s.thi[t]; S->tslot[t] = kNoSlot; }
+      }
+      const uint32_t nwin = s.nwin;
+      for (int t = 0; t < (int)s.ntgt; ++t) {
+        if (s.tlo[t] == s.thi[t]) continue;
+        const uint64_t r = s.rank[t];
+        int in = -1;
+        for (uint32_t k = 0; k < nwin; ++k) {
+          const uint64_t lo = s.wbelow[k];
+          const uint64_t c = (uint64_t)((s.wspike[k] & 1u) ? s.wcntF[k] : 0u) + ctot[k] +
+                             ((s.wspike[k] & 2u) ? s.wcntL[k] : 0u);
+          if (r >= lo && r < lo + c) in = (int)k;
+        }
+        if (in < 0) { fail = 1; continue; }
+        if (in != w) continue;
+        const uint32_t cF = (s.wspike[w] & 1u) ? s.wcntF[w] : 0u;
+        const uint64_t rp = r - s.wbelow[w];
+        if (rp < cF) {
+          if (s.wminF[w] == s.wmaxF[w]) { S->tlo[t] = S->thi[t] = s.wminF[w]; S->tslot[t] = kNoSlot; } else fail = 1;
+        } else if (rp < (uint64_t)cF + ctot[w]) {
+          qr[nc] = (uint32_t)(rp - cF);
+          tq[nc++] = t;
+        } else {
+          if (s.wminL[w] == s.wmaxL[w]) { S->tlo[t] = S->thi[t] = s.wminL[w]; S->tslot[t] = kNoSlot; } else fail = 1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (fail) atomicOr(&S->err, 1u);
+  if (nc == 0 || fail) return;
+  find_bins(hist + (size_t)w * kBins, kBins, qr, nc, wsum, rbin, rrem);
+  if (threadIdx.x == 0) {
+    uint32_t k0, k1;
+    window_keys(s, w, k0, k1);
+    const uint32_t mult = bin_mult(k0, k1);
+    for (int j = 0; j < nc; ++j) {
+      uint32_t a, z;
+      bin_interval(rbin[j], k0, mult, 0u, 0xffffffffu, a, z);
+      int own = -1;                      // targets sharing a bin share the first one's slot
+      for (int q = 0; q < nslot; ++q)
+        if (sl[q] == a && sz[q] == z) own = q;
+      if (own < 0) {
+        own = nslot++;
+        sl[own] = a; sz[own] = z;
+        slot[own] = tq[j];
+      }
+      const int t = tq[j];
+      S->tlo[t] = a;
+      S->thi[t] = z;
+      S->rank[t] = rrem[j];              // rank inside the fine bin
+      S->tslot[t] = (uint32_t)slot[own];
+      S->twin[t] = (uint32_t)w;
+    }
+    for (int q = 0; q < nslot; ++q) {    // the slot's header: count, min key, max key (k_bandw_compact)
+      uint32_t* h = send + (size_t)slot[q] * kPickWords;
+      h[0] = 0u;
+      h[1] = 0xffffffffu;
+      h[2] = 0u;
+    }
+  }
+}
+
+// The band's keys of every target slot (count, min, max, up to kPick keys): kBandSplit
+// workgroups per window, each over a slice of the band's window keys.
+__global__ __launch_bounds__(kBlock) void k_bandw_compact(const SelState* st, const uint32_t* cand, uint32_t cap,
+                                                          uint32_t* send) {
+  __shared__ uint32_t sl[kMaxTgt], sz[kMaxTgt];
+  __shared__ int slot[kMaxTgt], nslot;
+  const int w = blockIdx.x % 3, j = blockIdx.x / 3;
+  const SelState* S = st;
+  if (S->err || S->phase != PH_INIT) return;
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int t = 0; t < (int)S->ntgt; ++t)
+      if (S->tslot[t] == (uint32_t)t && S->twin[t] == (uint32_t)w) { sl[n] = S->tlo[t]; sz[n] = S->thi[t]; slot[n++] = t; }
+    nslot = n;
+  }
+  __syncthreads();
+  const int ns = nslot;
+  if (ns == 0) return;
+  const uint32_t c = min(S->ccount[w], cap);
+  const uint32_t i0 = (uint32_t)((uint64_t)c * j / kBandSplit), i1 = (uint32_t)((uint64_t)c * (j + 1) / kBandSplit);
+  const uint32_t* keys = cand + (size_t)w * cap;
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
+    const uint32_t k = keys[i];
+    for (int q = 0; q < ns; ++q) {
+      if (k >= sl[q] && k <= sz[q]) {
+        uint32_t* h = send + (size_t)slot[q] * kPickWords;
+        const uint32_t pos = atomicAdd(&h[0], 1u);
+        atomicMin(&h[1], k);
+        atomicMax(&h[2], k);
+        if (pos < (uint32_t)kPick) h[3 + pos] = k;
+      }
+    }
+  }
+}
+
+// Every band's keys of each target slot merged (into `scratch`), then the exact key of each
+// target sharing the slot (rank inside the bin) selected: one workgroup.
+__global__ __launch_bounds__(kBlock) void k_bandw_final(SelState* st, const uint32_t* recv, int nranks,
+                                                        uint32_t* scratch, uint32_t scratch_cap) {
+  __shared__ uint32_t lh[kBins];
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t rbin[kMaxTgt], rrem[kMaxTgt], tl[kMaxTgt], tz[kMaxTgt], tr[kMaxTgt], out[kMaxTgt];
+  __shared__ uint32_t ranks[kMaxTgt], offs[kMaxBandRanks + 1];
+  __shared__ int who[kMaxTgt], ng, bad;
+  __shared__ uint32_t tot, gmn, gmx;
+  SelState* S = st;
+  if (S->phase != PH_INIT || S->err) return;
+  const int ntgt = (int)S->ntgt;
+  uint32_t base = 0;                     // each slot's keys in their own scratch range
+  for (int t0 = 0; t0 < ntgt; ++t0) {
+    if (S->tslot[t0] != (uint32_t)t0) continue;      // not a slot owner (or resolved)
+    if (threadIdx.x == 0) {
+      ng = 0;
+      for (int t = t0; t < ntgt; ++t)
+        if (S->tslot[t] == (uint32_t)t0) { who[ng] = t; ranks[ng++] = S->rank[t]; }
+      uint32_t acc = 0, a = 0xffffffffu, z = 0u;
+      bad = 0;
+      for (int r = 0; r < nranks; ++r) {
+        const uint32_t* h = recv + (size_t)r * kBandWords + (size_t)t0 * kPickWords;
+        offs[r] = acc;
+        if (h[0]) { a = min(a, h[1]); z = max(z, h[2]); }
+        if (h[0] > (uint32_t)kPick) bad = 1;
+        acc += min(h[0], (uint32_t)kPick);
+      }
+      offs[nranks] = acc;
+      tot = acc;
+      gmn = a;
+      gmx = z;
+      if (bad && a == z) {              // one distinct key: every target of the slot is it
+        for (int q = 0; q < ng; ++q) { S->tlo[who[q]] = S->thi[who[q]] = a; }
+        ng = 0;
+        bad = 0;
+      }
+      if (!bad && ng > 0 && base + acc > scratch_cap) bad = 1;
+      if (bad) S->err = 1u;
+    }
+    __syncthreads();
+    if (bad) return;
+    if (ng == 0) continue;
+    uint32_t* keys = scratch + base;
+    for (int r = 0; r < nranks; ++r) {
+      const uint32_t o = offs[r], n = offs[r + 1] - o;
+      const uint32_t* src = recv + (size_t)r * kBandWords + (size_t)t0 * kPickWords + 3;
+      for (uint32_t i = threadIdx.x; i < n; i += kBlock) keys[o + i] = src[i];
+    }
+    __syncthreads();
+    cand_select(keys, tot, gmn, gmx < gmn ? gmn : gmx, ranks, ng, out, lh, wsum, rbin, rrem, tl, tz, tr);
+    if (threadIdx.x < ng) S->tlo[who[threadIdx.x]] = S->thi[who[threadIdx.x]] = out[threadIdx.x];
+    base += tot;
+    __syncthreads();
+  }
+}
+
 struct Exchange {
   i2pc_exchange_fn fn;
   void* user;
-  int64_t* ex;     // device int64 [4][B]
+  int64_t* ex;     // device int64 [4][max(B, kBandEx)]
+  i2pc_gather_fn gather;   // window-selection band runs: the candidate all-gather (else NULL)
+  int nranks;
+  uint32_t* send;          // [kBandWords]
+  uint32_t* recv;          // [nranks][kBandWords]
 };
 
 // Between a histogram sweep and its resolve, a band run hands the partial histograms (and,
@@ -2857,11 +3188,12 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
                          uint32_t* mhist, uint32_t cap, int B, const Sweep& sw, hipStream_t s,
                          const Exchange* x = nullptr) {
   // full-resolution sample of ~64 K points per image for the level-0 estimate
-  const int stride = std::max(1, (int)std::sqrt((double)g.H * g.W / 65536.0));
-  const int ns = ((g.H + stride - 1) / stride) * ((g.W + stride - 1) / stride);
-  hipLaunchKernelGGL(k_model_hist, dim3(B * kSampleChunks), dim3(kHistBlock), 0, s, g, B, st, mhist, rpart, stride);
-  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, mhist, cap, B, x ? 0 : 1, ns);
-  if (!x && g_sel_windows) {
+  const SamplePlan sp = sample_plan(g.H, g.W);
+  // windows: the batch path, and band runs that can all-gather their candidate lists
+  const bool win = x ? x->gather != nullptr : g_sel_windows != 0;
+  hipLaunchKernelGGL(k_model_hist, dim3(B * sp.nch), dim3(kHistBlock), 0, s, g, B, st, mhist, rpart, sp.stride, sp.nch);
+  hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, mhist, cap, B, win ? 1 : 0, sp.ns, sp.nch);
+  if (win) {
     // batch path: one window-only sweep + resolve; k_sel_slow finishes (or, for the rare image
     // a window missed, selects from scratch).  Sweep workgroup = kSelRows output rows x a
     // kTileW-column tile (register-streamed model rows, no LDS row window).
@@ -2876,6 +3208,20 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
       hipLaunchKernelGGL((k_sweep_w<true>), grid, block, 0, s, g, st, cand, cap, B, sww);
     else
       hipLaunchKernelGGL((k_sweep_w<false>), grid, block, 0, s, g, st, cand, cap, B, sww);
+    if (x) {
+      // band run (B = 1): fine histograms + counters all-reduced, each target's bin keys
+      // all-gathered, every rank selects the same keys (2 collectives, ~40 KB per rank)
+      hipLaunchKernelGGL(k_bandw_hist, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex);
+      if (x->fn(x->user, hist, 3 * kBins, x->ex, kBandEx, s) != 0)
+        return set_error(I2PC_ELAUNCH, "exchange callback failed (window histograms)");
+      hipLaunchKernelGGL(k_bandw_pick, dim3(3), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex, x->send);
+      hipLaunchKernelGGL(k_bandw_compact, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, x->send);
+      if (x->gather(x->user, x->send, x->recv, kBandWords, s) != 0)
+        return set_error(I2PC_ELAUNCH, "gather callback failed (target bins)");
+      hipLaunchKernelGGL(k_bandw_final, dim3(1), dim3(kBlock), 0, s, st, x->recv, x->nranks, cand, kSlots * cap);
+      hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
+      return check_launch("select");
+    }
     hipLaunchKernelGGL(k_resolve_w, dim3(B * 3), dim3(kBlock), 0, s, st, cand, cap, B);
     hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
     return check_launch("select");
@@ -2949,7 +3295,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   const int blur_k = params->smooth_ksize < 3 ? 3 : params->smooth_ksize / 2 * 2 + 1;   // app.py:211
   if (params->smooth)
     I2PC_REQUIRE(blur_k <= kMaxBlur, "smooth_ksize -> kernel %d: at most %d taps", blur_k, kMaxBlur);
-  const Layout L = layout(batch, img_h, img_w, params->smooth);
+  const int granks = xch && xch->gather ? xch->nranks : 0;
+  const Layout L = layout(batch, img_h, img_w, params->smooth, granks);
   if (workspace_bytes < L.total) return set_error(I2PC_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
   hipStream_t s = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
@@ -2970,8 +3317,10 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   // tile; measured r02, B = 32 x 1024^2 whole call: 4096 pts 334 us, 8192 299 us, 16384 = 8192
   // (the LDS budget caps the rows at 8))
   const Sweep ssel = plan_select(img_h, img_w, dep_h, dep_w, g.same != 0, row0, row1);
-  Exchange xb = xch ? *xch : Exchange{nullptr, nullptr, nullptr};
+  Exchange xb = xch ? *xch : Exchange{nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr};
   xb.ex = reinterpret_cast<int64_t*>(ws + L.ex);
+  xb.send = reinterpret_cast<uint32_t*>(ws + L.gsend);
+  xb.recv = reinterpret_cast<uint32_t*>(ws + L.grecv);
   uint32_t* cand = reinterpret_cast<uint32_t*>(ws + L.cand);
   int rc = launch_select(g, st, hist, cand, rpart, reinterpret_cast<uint32_t*>(ws + L.mhist), L.cap, batch, ssel, s,
                          xch ? &xb : nullptr);
@@ -3007,10 +3356,22 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
     double* f0 = reinterpret_cast<double*>(ws + L.field);
     double* f1 = reinterpret_cast<double*>(ws + L.tmp);
     const int nb = 2048;
-    hipLaunchKernelGGL(k_norm_field, dim3(nb), dim3(256), 0, s, g, st, batch, params->invert, f0);
+    // image rows the vertical pass reads for the band's output rows (reflect-101 included):
+    // the band plus a k/2 halo, or reflected rows near the image's top and bottom
+    const int hr = blur_k / 2;
+    int f_lo = row0, f_hi = row1;
+    for (int v = row0; v < row1; ++v) {
+      if (v >= row0 + hr && v < row1 - hr) { v = row1 - hr - 1; continue; }   // interior rows add nothing
+      for (int t = -hr; t <= hr; ++t) {
+        const int rr = reflect101_host(v + t, img_h);
+        f_lo = std::min(f_lo, rr);
+        f_hi = std::max(f_hi, rr + 1);
+      }
+    }
+    hipLaunchKernelGGL(k_norm_field, dim3(nb), dim3(256), 0, s, g, st, batch, params->invert, f0, f_lo, f_hi);
     const BlurTaps taps = gaussian_taps(blur_k);
-    hipLaunchKernelGGL((k_blur<true>), dim3(nb), dim3(256), 0, s, f0, f1, st, batch, img_h, img_w, taps);
-    hipLaunchKernelGGL((k_blur<false>), dim3(nb), dim3(256), 0, s, f1, f0, st, batch, img_h, img_w, taps);
+    hipLaunchKernelGGL((k_blur<true>), dim3(nb), dim3(256), 0, s, f0, f1, st, batch, img_h, img_w, taps, f_lo, f_hi);
+    hipLaunchKernelGGL((k_blur<false>), dim3(nb), dim3(256), 0, s, f1, f0, st, batch, img_h, img_w, taps, row0, row1);
     field = f0;
     hipLaunchKernelGGL((k_unproject<true>), dim3(batch * sunp.nrb), dim3(kBlock), 0, s, g, st, field, image,
                        channels, batch, sunp, params->invert, cam, xyz, rgb, st);
@@ -3056,12 +3417,45 @@ extern "C" int i2pc_unproject(const float* depth, int dep_h, int dep_w, const ui
                        workspace, workspace_bytes, stream, 0, img_h, nullptr);
 }
 
+static int run_band(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
+                    int img_h, int img_w, int row0, int row1, const i2pc_unproject_params* params,
+                    float* xyz_band, uint8_t* rgb_band, double* bbox, double* stats,
+                    void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange_fn,
+                    i2pc_gather_fn gather_fn, int nranks, void* user, void* stream);
+
+extern "C" size_t i2pc_unproject_band_workspace_bytes(int img_h, int img_w, int smooth, int nranks) {
+  if (img_h <= 0 || img_w <= 0 || nranks <= 0 || nranks > kMaxBandRanks) return 0;
+  return layout(1, img_h, img_w, smooth, nranks).total;
+}
+
 extern "C" int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
                                    int img_h, int img_w, int row0, int row1, const i2pc_unproject_params* params,
                                    float* xyz_band, uint8_t* rgb_band, double* bbox, double* stats,
                                    void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange_fn,
                                    void* user, void* stream) {
   clear_error();
+  return run_band(depth, dep_h, dep_w, image_band, channels, img_h, img_w, row0, row1, params, xyz_band, rgb_band,
+                  bbox, stats, workspace, workspace_bytes, exchange_fn, nullptr, 0, user, stream);
+}
+
+extern "C" int i2pc_unproject_band_w(const float* depth, int dep_h, int dep_w, const uint8_t* image_band,
+                                     int channels, int img_h, int img_w, int row0, int row1,
+                                     const i2pc_unproject_params* params, float* xyz_band, uint8_t* rgb_band,
+                                     double* bbox, double* stats, void* workspace, size_t workspace_bytes,
+                                     int nranks, i2pc_exchange_fn exchange_fn, i2pc_gather_fn gather_fn, void* user,
+                                     void* stream) {
+  clear_error();
+  I2PC_REQUIRE(exchange_fn && gather_fn, "the window band mode needs both the exchange and the gather");
+  I2PC_REQUIRE(nranks > 0 && nranks <= kMaxBandRanks, "nranks %d outside [1, %d]", nranks, kMaxBandRanks);
+  return run_band(depth, dep_h, dep_w, image_band, channels, img_h, img_w, row0, row1, params, xyz_band, rgb_band,
+                  bbox, stats, workspace, workspace_bytes, exchange_fn, gather_fn, nranks, user, stream);
+}
+
+static int run_band(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
+                    int img_h, int img_w, int row0, int row1, const i2pc_unproject_params* params,
+                    float* xyz_band, uint8_t* rgb_band, double* bbox, double* stats,
+                    void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange_fn,
+                    i2pc_gather_fn gather_fn, int nranks, void* user, void* stream) {
   I2PC_REQUIRE(params != nullptr, "params is NULL");
   I2PC_REQUIRE(image_band && xyz_band && rgb_band, "NULL device pointer");
   I2PC_REQUIRE(img_h > 0 && img_w > 0 && channels >= 1 && channels <= 4, "bad image shape");
@@ -3070,13 +3464,14 @@ extern "C" int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, con
   I2PC_REQUIRE(0 <= row0 && row0 < row1 && row1 <= img_h, "band rows [%d, %d) outside [0, %d)", row0, row1, img_h);
   I2PC_REQUIRE(row0 % step == 0 && (row1 % step == 0 || row1 == img_h),
                "band rows must start (and end, unless at the bottom) on a multiple of the step %d", step);
-  if (params->smooth) return set_error(I2PC_EUNSUPPORTED, "smooth_depth blurs across bands: not in tile-parallel mode");
+  // smooth_depth: the band's field plus the blur's halo rows are recomputed locally (the
+  // model-resolution depth and, after the exchange, the stats are whole on every rank)
   // the kernels address the full image: shift the band buffers back to row 0
   const int Wn = (img_w + step - 1) / step;
   const uint8_t* image = image_band - (ptrdiff_t)row0 * img_w * channels;
   float* xyz = xyz_band - (ptrdiff_t)(row0 / step) * Wn * 3;
   uint8_t* rgb = rgb_band - (ptrdiff_t)(row0 / step) * Wn * 3;
-  const Exchange x{exchange_fn, user, nullptr};
+  const Exchange x{exchange_fn, user, nullptr, gather_fn, nranks, nullptr, nullptr};
   return run_unproject(depth, dep_h, dep_w, image, channels, 1, img_h, img_w, params, xyz, rgb, bbox, stats,
                        workspace, workspace_bytes, stream, row0, row1, exchange_fn ? &x : nullptr);
 }

@@ -127,7 +127,10 @@ def band_exchange(group=None):
     import torch.distributed as dist
 
     def _exchange(hist, counters):
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+        if not dist.is_initialized():       # one rank: the sums / min / max are its own values
+            return
+        if hist is not None:                # (None: the window mode's counters-only exchange)
+            dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
         if counters is not None:
             sums, kmin, kmax = counters[:2].contiguous(), counters[2].contiguous(), counters[3].contiguous()
             dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
@@ -137,6 +140,19 @@ def band_exchange(group=None):
             counters[2].copy_(kmin)
             counters[3].copy_(kmax)
     return _exchange
+
+
+def band_gather(group=None):
+    """The all-gather of the window-selection band mode (i2pc_unproject_band_w): every rank's
+    candidate words into recv [nranks, words]."""
+    import torch.distributed as dist
+
+    def _gather(send, recv):
+        if not dist.is_initialized():
+            recv[0].copy_(send)
+            return
+        dist.all_gather(list(recv.unbind(0)), send, group=group)
+    return _gather
 
 
 def reduce_bbox(bbox, group=None):

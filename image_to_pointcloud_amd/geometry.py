@@ -230,6 +230,15 @@ _lib.register("i2pc_unproject_band_rccl", ctypes.c_int,
               [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                ctypes.c_int, ctypes.c_int, ctypes.POINTER(_lib.UnprojectParams), ctypes.c_void_p, ctypes.c_void_p,
                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p])
+GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                             ctypes.c_void_p)
+_lib.register("i2pc_unproject_band_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                                       ctypes.c_int])
+_lib.register("i2pc_unproject_band_w", ctypes.c_int,
+              [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+               ctypes.c_int, ctypes.c_int, ctypes.POINTER(_lib.UnprojectParams), ctypes.c_void_p, ctypes.c_void_p,
+               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, EXCHANGE_FN,
+               GATHER_FN, ctypes.c_void_p, ctypes.c_void_p])
 _lib.register("i2pc_unproject_band", ctypes.c_int,
               [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                ctypes.c_int, ctypes.c_int, ctypes.POINTER(_lib.UnprojectParams), ctypes.c_void_p, ctypes.c_void_p,
@@ -249,6 +258,11 @@ def _as_tensor(ptr: int, n: int, typestr: str):
     return torch.as_tensor(_DevView(ptr, n, typestr), device="cuda")
 
 
+def band_workspace_bytes(img_h: int, img_w: int, smooth: bool = False, nranks: int = 1) -> int:
+    """Workspace of a window-selection band call (an RcclComm, or `gather=`) over `nranks` bands."""
+    return int(_lib.load().i2pc_unproject_band_workspace_bytes(img_h, img_w, int(bool(smooth)), int(nranks)))
+
+
 def band_rows(img_h: int, parts: int, step: int = 1) -> list:
     """Split image rows into `parts` contiguous bands [row0, row1) whose starts are multiples
     of the density step (so every band owns whole point rows), as even as that allows."""
@@ -264,12 +278,19 @@ def band_rows(img_h: int, parts: int, step: int = 1) -> list:
 def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: int, exchange=None,
                    density: str = "high", invert: bool = True, depth_scale: float = 10.0,
                    fov: Optional[float] = None, workspace=None, comm=None, out=None,
-                   projection: str = "pinhole"):
+                   projection: str = "pinhole", smooth: bool = False, smooth_ksize: int = 5,
+                   gather=None, nranks: Optional[int] = None):
     """This rank's band [row0, row1) of one image's unprojection (i2pc_unproject_band).
 
-    comm       : a distributed.RcclComm: the exchange runs on the device (RCCL all-reduces on
-                 the current stream, i2pc_unproject_band_rccl) -- no host callback, graph-capturable;
-                 otherwise `exchange` (host callable, below) is used
+    smooth     : smooth_depth (app.py:208-214): the band's blurred field is recomputed with its
+                 k/2 halo rows locally, bit-identical to the whole image's
+    comm       : a distributed.RcclComm: the exchange runs on the device (RCCL all-reduce and
+                 all-gather on the current stream, i2pc_unproject_band_rccl, window selection) --
+                 no host callback, graph-capturable; otherwise `exchange` (host callable, below)
+    gather     : with `exchange`: callable(send: int32 [words], recv: int32 [nranks, words]) that
+                 all-gathers every rank's words (e.g. distributed.band_gather(group)); selects the
+                 one-sweep window mode (i2pc_unproject_band_w) instead of the four histogram levels
+    nranks     : the number of bands (ranks) of a `gather` run
     out        : optional (xyz, rgb, bbox, stats) device tensors to write (graph capture)
 
     depth      : torch.float32 [h, w] model-resolution depth of the WHOLE image (device)
@@ -312,11 +333,24 @@ def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: i
         bbox = torch.empty(6, dtype=torch.float64, device=dev)
         stats = torch.empty(4, dtype=torch.float64, device=dev)
     lib = _lib.load()
-    ws = workspace if workspace is not None else _workspace(lib.i2pc_unproject_workspace_bytes(1, img_h, img_w, 0), dev)
+    if comm is not None:
+        ws_bytes = band_workspace_bytes(img_h, img_w, smooth, comm.nranks)
+    elif gather is not None:
+        if not nranks or nranks < 1:
+            raise ValueError("a gather band run needs nranks (the number of bands)")
+        ws_bytes = band_workspace_bytes(img_h, img_w, smooth, nranks)
+    else:
+        ws_bytes = lib.i2pc_unproject_workspace_bytes(1, img_h, img_w, int(bool(smooth)))
+    if workspace is not None:
+        if workspace.dtype != torch.uint8 or not workspace.is_cuda or workspace.numel() < ws_bytes:
+            raise ValueError(f"workspace must be a device uint8 buffer of >= {ws_bytes} bytes")
+        ws = workspace
+    else:
+        ws = _workspace(ws_bytes, dev)
     if comm is not None:
         p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
-                                 fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5,
-                                 projection=PROJECTION[projection])
+                                 fov_deg=float(fov) if fov else 0.0, smooth=int(bool(smooth)),
+                                 smooth_ksize=int(smooth_ksize), projection=PROJECTION[projection])
         _lib.call("i2pc_unproject_band_rccl", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
                   img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),
                   _ptr(ws), ws.numel(), comm.handle, _stream_handle())
@@ -327,7 +361,7 @@ def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: i
 
     def _cb(user, hist, words, counters, batch, stream):
         try:
-            h = _as_tensor(hist, int(words), "<i4")
+            h = _as_tensor(hist, int(words), "<i4") if hist and words > 0 else None
             c = _as_tensor(counters, 4 * int(batch), "<i8").view(4, int(batch)) if counters else None
             exchange(h, c)
             return 0
@@ -335,14 +369,29 @@ def unproject_band(depth, image_band, img_h: int, img_w: int, row0: int, row1: i
             errors.append(e)
             return 1
 
+    def _gcb(user, send, recv, words, stream):
+        try:
+            gather(_as_tensor(send, int(words), "<i4"), _as_tensor(recv, int(nranks) * int(words), "<i4")
+                   .view(int(nranks), int(words)))
+            return 0
+        except Exception as e:
+            errors.append(e)
+            return 1
+
     cb = EXCHANGE_FN(_cb)
+    gcb = GATHER_FN(_gcb) if gather is not None else None
     p = _lib.UnprojectParams(step=step, invert=int(bool(invert)), depth_scale=float(depth_scale),
-                             fov_deg=float(fov) if fov else 0.0, smooth=0, smooth_ksize=5,
-                                 projection=PROJECTION[projection])
+                             fov_deg=float(fov) if fov else 0.0, smooth=int(bool(smooth)),
+                             smooth_ksize=int(smooth_ksize), projection=PROJECTION[projection])
     try:
-        _lib.call("i2pc_unproject_band", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
-                  img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),
-                  _ptr(ws), ws.numel(), cb, None, _stream_handle())
+        if gcb is not None:
+            _lib.call("i2pc_unproject_band_w", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
+                      img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),
+                      _ptr(ws), ws.numel(), int(nranks), cb, gcb, None, _stream_handle())
+        else:
+            _lib.call("i2pc_unproject_band", _ptr(depth), depth.shape[-2], depth.shape[-1], _ptr(image_band), C,
+                      img_h, img_w, row0, row1, ctypes.byref(p), _ptr(xyz), _ptr(rgb), _ptr(bbox), _ptr(stats),
+                      _ptr(ws), ws.numel(), cb, None, _stream_handle())
     except _lib.I2PCError:
         if errors:
             raise errors[0]

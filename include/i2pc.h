@@ -104,9 +104,11 @@ int i2pc_unproject(const float* depth, int dep_h, int dep_w,
  *              slice [row0/step * ceil(img_w/step), ...) of the whole image's points
  * bbox       : float64 [6] of this band's points (the caller min/max-reduces them)
  * stats      : float64 [4] as i2pc_unproject (identical on every rank)
- * row0 must be a multiple of step, and row1 too unless row1 == img_h; smooth is not
- * supported (the blur crosses bands).  workspace: i2pc_unproject_workspace_bytes(1,
- * img_h, img_w, 0). */
+ * row0 must be a multiple of step, and row1 too unless row1 == img_h.  smooth: each rank
+ * recomputes its band's normalised field plus the blur's k/2 halo rows (reflect-101 at the
+ * image edges) from the whole model-resolution depth, so smoothed bands concatenate to the
+ * whole image's smoothed points with no extra exchange.  workspace:
+ * i2pc_unproject_workspace_bytes(1, img_h, img_w, smooth). */
 typedef int (*i2pc_exchange_fn)(void* user, uint32_t* hist, int64_t hist_words, int64_t* counters, int batch,
                                 void* stream);
 int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
@@ -115,9 +117,32 @@ int i2pc_unproject_band(const float* depth, int dep_h, int dep_w, const uint8_t*
                         void* workspace, size_t workspace_bytes, i2pc_exchange_fn exchange, void* user,
                         void* stream);
 
-/* The same band call with the exchange done on the device by RCCL (all-reduces on
- * `stream` per selection sweep: histogram SUM, counters SUM / MIN / MAX), so the call is
- * stream-ordered end to end and can be captured into a HIP graph.  `comm` comes from
+/* Window-selection band mode: the same band call with ONE selection sweep instead of four.
+ * Every rank derives the same value windows around p2 / p98 (and the median) from a sample of
+ * the whole image, sweeps its band once (compacting its window keys locally), then
+ *   exchange(user, hist, 6144, counters, 8, stream)  hist: 2048 fine bins per window of the
+ *                                                band's window keys (SUM); counters int64 [4][8]:
+ *                                                rows 0-1 SUM, row 2 MIN, row 3 MAX
+ *   gather(user, send, recv, words, stream)      all-gather: every rank's `words` uint32 into
+ *                                                recv [nranks][words] (any fixed rank order):
+ *                                                per target the band's keys of its fine bin
+ * and every rank selects the same exact keys (about 25 KB all-reduced + 41 KB gathered per
+ * rank, whatever the image size).  A target the windows missed, or a fine bin holding more than
+ * 1024 distinct-valued keys in one band, falls back to an exact whole-image selection on every
+ * rank (same result, much slower).  workspace: i2pc_unproject_band_workspace_bytes(img_h, img_w,
+ * smooth, nranks). */
+typedef int (*i2pc_gather_fn)(void* user, const uint32_t* send, uint32_t* recv, int64_t words, void* stream);
+size_t i2pc_unproject_band_workspace_bytes(int img_h, int img_w, int smooth, int nranks);
+int i2pc_unproject_band_w(const float* depth, int dep_h, int dep_w, const uint8_t* image_band, int channels,
+                          int img_h, int img_w, int row0, int row1, const i2pc_unproject_params* params,
+                          float* xyz_band, uint8_t* rgb_band, double* bbox, double* stats,
+                          void* workspace, size_t workspace_bytes, int nranks, i2pc_exchange_fn exchange,
+                          i2pc_gather_fn gather, void* user, void* stream);
+
+/* The window-selection band call with the exchange done on the device by RCCL (the counters'
+ * all-reduces and the candidates' all-gather on `stream`), so the call is stream-ordered end to
+ * end and can be captured into a HIP graph; workspace: i2pc_unproject_band_workspace_bytes(
+ * img_h, img_w, smooth, nranks of the communicator).  `comm` comes from
  * i2pc_comm_create on every rank with the id rank 0 got from i2pc_comm_unique_id
  * (ncclGetUniqueId / ncclCommInitRank; 128 bytes, shipped by the caller); the current HIP
  * device must be the rank's GPU. */

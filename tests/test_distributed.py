@@ -87,15 +87,23 @@ def _band_worker(rank, ws, port, q):
         hist = torch.arange(8, dtype=torch.int32) * (rank + 1)
         cnt = torch.tensor([[rank + 1], [10 * rank], [100 - rank], [7 + rank]], dtype=torch.int64)
         ex(hist, cnt)
+        # the window mode: a counters-only exchange (no histogram) and the candidate all-gather
+        wcnt = torch.tensor([[rank + 1] * 8, [2] * 8, [50 - rank] * 8, [rank] * 8], dtype=torch.int64)
+        ex(None, wcnt)
+        send = torch.arange(6, dtype=torch.int32) + 100 * rank
+        recv = torch.zeros((ws, 6), dtype=torch.int32)
+        D.band_gather()(send, recv)
         bb = torch.tensor([rank, rank + 5.0, -rank, 2.0, 0.5 * rank, 1.0 + rank], dtype=torch.float64)
-        q.put((rank, hist.numpy().copy(), cnt.numpy().copy(), D.reduce_bbox(bb).numpy().copy()))
+        q.put((rank, hist.numpy().copy(), cnt.numpy().copy(), D.reduce_bbox(bb).numpy().copy(),
+               wcnt.numpy().copy(), recv.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
 
 def test_band_exchange_protocol():
     """The C4 exchange i2pc_unproject_band calls between selection sweeps: histogram SUM,
-    level-0 counts SUM, key MIN / MAX; and the band bbox min / max."""
+    level-0 counts SUM, key MIN / MAX; the window mode's counters-only exchange and candidate
+    all-gather (i2pc_unproject_band_w); and the band bbox min / max."""
     ws, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -106,7 +114,9 @@ def test_band_exchange_protocol():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for _, hist, cnt, bb in out:
+    for _, hist, cnt, bb, wcnt, recv in out:
+        assert wcnt.tolist() == [[3] * 8, [4] * 8, [49] * 8, [1] * 8]
+        assert recv.tolist() == [list(range(6)), [100 + i for i in range(6)]]
         assert hist.tolist() == [3 * i for i in range(8)]
         assert cnt[:, 0].tolist() == [3, 10, 99, 8]
         assert bb.tolist() == [0.0, 6.0, -1.0, 2.0, 0.0, 2.0]

@@ -201,15 +201,36 @@ def test_bad_arguments_raise():
         g.depth_to_point_cloud(_rgb(8, 8, 1), _smooth_depth(8, 8, 1), smooth=True, smooth_ksize=99)
 
 
+@pytest.mark.parametrize("window", [False, True])
 @pytest.mark.parametrize("density,parts", [("high", 1), ("high", 3), ("medium", 2), ("low", 4)])
-def test_band_unproject_matches_whole_image(density, parts):
+def test_band_unproject_matches_whole_image(density, parts, window):
     """C4 tile-parallel mode: `parts` ranks (threads on their own streams here, with an
     in-process all-reduce as the exchange) each unproject a row band of one image; the
     concatenated bands are bit-identical to the whole-image unprojection, every rank gets
     the same p2/p98 / nanmedian stats, and the min/max of the band bboxes is the bbox."""
     dep = _smooth_depth(48, 64, 51)
     dep[3, 4] = np.nan                      # exercises the nanmedian pass as well
-    _band_check(dep, _rgb(301, 410, 52), parts, density)
+    _band_check(dep, _rgb(301, 410, 52), parts, density, window=window)
+
+
+@pytest.mark.parametrize("ksize,parts,shape,density", [(5, 3, (48, 64, 301, 410), "high"),
+                                                      (9, 4, (60, 50, 120, 100), "medium"),
+                                                      (31, 5, (12, 9, 40, 30), "high"),     # halo wider than a band
+                                                      (15, 8, (96, 128, 64, 128), "low")])
+def test_band_smoothing_matches_whole_image_and_oracle(ksize, parts, shape, density):
+    window = parts % 2 == 1                 # both selection modes
+    """smooth_depth in C4's band mode (app.py:208-214): each band recomputes its normalised
+    field plus the blur's k/2 halo rows (reflect-101 at the image edges, repeated for a kernel
+    wider than the image), so the smoothed bands concatenate bit-identically to the whole
+    image's smoothed points, which are bit-exact with the oracle's GaussianBlur."""
+    h, w, H, W = shape
+    dep = _smooth_depth(h, w, 111)
+    dep[2, 3] = np.nan
+    img = _rgb(H, W, 112)
+    whole = _band_check(dep, img, parts, density, depth_scale=10.0, smooth=True, smooth_ksize=ksize, window=window)
+    ep, ec = ref.depth_to_point_cloud(img, dep, density=density, depth_scale=10.0, smooth=True,
+                                      smooth_ksize=ksize, loop=False)
+    assert _same_bits(whole.xyz[0].cpu().numpy(), ep), _first_diff(whole.xyz[0].cpu().numpy(), ep)
 
 
 def test_c4_panorama_full_size_bands_and_oracle():
@@ -220,12 +241,17 @@ def test_c4_panorama_full_size_bands_and_oracle():
     dep = _smooth_depth(518, 1036, 71)
     img = _rgb(4096, 8192, 72)
     whole = _band_check(dep, img, 8, "high", depth_scale=10.0)
+    _band_check(dep, img, 8, "high", depth_scale=10.0, window=True)
     ep, ec = ref.depth_to_point_cloud(img, dep, density="high", depth_scale=10.0, loop=False)
     assert _same_bits(whole.xyz[0].cpu().numpy(), ep), _first_diff(whole.xyz[0].cpu().numpy(), ep)
     assert _same_bits(whole.rgb[0].cpu().numpy().astype(np.float32), ec)
 
 
-def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole"):
+def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole", smooth=False, smooth_ksize=5,
+                window=False):
+    """`parts` ranks (threads on their own streams, an in-process all-reduce / all-gather as the
+    exchange) each unproject a row band; checks the bands against the whole image.  window:
+    the one-sweep window mode (i2pc_unproject_band_w) instead of the histogram levels."""
     import threading
     g = _geom()
     dev = torch.device("cuda")
@@ -233,20 +259,34 @@ def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole"
     tdep = torch.from_numpy(dep).to(dev)
     timg = torch.from_numpy(img).to(dev)
     whole = g.unproject_batch(tdep[None], timg[None], density=density, depth_scale=depth_scale,
-                              projection=projection)
+                              projection=projection, smooth=smooth, smooth_ksize=smooth_ksize)
     torch.cuda.synchronize()
     step = g.DENSITY_STEP[density]
     bands = g.band_rows(H, parts, step)
     results, slots, errs = [None] * parts, [None] * parts, []
     bar = threading.Barrier(parts)
-    nbytes = g._lib.load().i2pc_unproject_workspace_bytes(1, H, W, 0)
+    nbytes = (g.band_workspace_bytes(H, W, smooth, parts) if window
+              else g._lib.load().i2pc_unproject_workspace_bytes(1, H, W, int(smooth)))
+    gslots = [None] * parts
+
+    def gather_for(i):
+        def ga(send, recv):
+            torch.cuda.current_stream().synchronize()
+            gslots[i] = send.clone()
+            bar.wait()
+            for r in range(parts):
+                recv[parts - 1 - r].copy_(gslots[r])     # (any fixed rank order works)
+            torch.cuda.current_stream().synchronize()
+            bar.wait()
+        return ga
 
     def exchange_for(i):
         def ex(hist, cnt):
             torch.cuda.current_stream().synchronize()
-            slots[i] = (hist.clone(), None if cnt is None else cnt.clone())
+            slots[i] = (None if hist is None else hist.clone(), None if cnt is None else cnt.clone())
             bar.wait()
-            hist.copy_(torch.stack([s[0] for s in slots]).sum(0).to(torch.int32))
+            if hist is not None:
+                hist.copy_(torch.stack([s[0] for s in slots]).sum(0).to(torch.int32))
             if cnt is not None:
                 c = torch.stack([s[1] for s in slots])
                 cnt[:2] = c[:, :2].sum(0)
@@ -262,7 +302,10 @@ def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole"
                 r0, r1 = bands[i]
                 ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
                 results[i] = g.unproject_band(tdep, timg[r0:r1], H, W, r0, r1, exchange_for(i), density=density,
-                                              depth_scale=depth_scale, workspace=ws, projection=projection)
+                                              depth_scale=depth_scale, workspace=ws, projection=projection,
+                                              smooth=smooth, smooth_ksize=smooth_ksize,
+                                              gather=gather_for(i) if window else None,
+                                              nranks=parts if window else None)
                 torch.cuda.current_stream().synchronize()
         except Exception as e:   # pragma: no cover - reported below
             errs.append(e)
@@ -304,6 +347,7 @@ def test_selection_with_a_spike_of_equal_values(zero_frac, shape):
         blocks += 1
     img = _rgb(H, W, 103)
     whole = _band_check(dep, img, 3, "high", depth_scale=10.0)
+    _band_check(dep, img, 3, "high", depth_scale=10.0, window=True)   # spikes through the window exchange
     ep, ec = ref.depth_to_point_cloud(img, dep, density="high", depth_scale=10.0, loop=False)
     assert _same_bits(whole.xyz[0].cpu().numpy(), ep), _first_diff(whole.xyz[0].cpu().numpy(), ep)
 
@@ -316,7 +360,7 @@ def test_equirect_projection_matches_oracle_and_bands(density):
     4-band split bit-identical to the whole image."""
     dep = _smooth_depth(64, 128, 91)
     img = _rgb(512, 1024, 92)
-    whole = _band_check(dep, img, 4, density, depth_scale=10.0, projection="equirect")
+    whole = _band_check(dep, img, 4, density, depth_scale=10.0, projection="equirect", window=density == "high")
     ep, ec = ref.depth_to_point_cloud_equirect(img, dep, density=density, depth_scale=10.0)
     got = whole.xyz[0].cpu().numpy()
     assert got.shape == ep.shape
@@ -344,7 +388,7 @@ def test_band_rccl_exchange_single_rank_and_graph_capture():
     tdep, timg = torch.from_numpy(dep).to(dev), torch.from_numpy(img).to(dev)
     whole = g.unproject_batch(tdep[None], timg[None], density="high")
     comm = RcclComm(nranks=1, rank=0)
-    ws = torch.empty(g.workspace_bytes(1, 600, 800), dtype=torch.uint8, device=dev)
+    ws = torch.empty(g.band_workspace_bytes(600, 800, False, 1), dtype=torch.uint8, device=dev)
     xyz, rgb, bbox, stats = g.unproject_band(tdep, timg, 600, 800, 0, 600, comm=comm, workspace=ws)
     torch.cuda.synchronize()
     assert _same_bits(xyz.cpu().numpy(), whole.xyz[0].cpu().numpy())

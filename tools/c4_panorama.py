@@ -12,11 +12,15 @@ and --graph captures each rank's whole band call into a HIP graph); when ranks s
 it falls back to the host-callback exchange over gloo (correctness runs only).  Rank 0 prints one JSON line (points/s over the job, max
 over ranks), and --check compares every band bit-for-bit with the whole-image unprojection.
 
---network runs the depth network too: rank 0 holds the whole panorama, preprocesses it to the
-Depth-Anything-V2-Small input (518 x 1036, keep-aspect /14), runs the network (seeded random
-weights) and broadcasts the 518 x 1036 depth over RCCL; every rank then unprojects its band
-(ms_per_image then covers network + broadcast + band unprojection).  --projection equirect
-back-projects the panorama on the sphere (i2pc.h; the reference only has the pinhole model).
+--network runs the depth network too, on a STREAM of panoramas: a step takes one panorama per
+rank, and rank k preprocesses panorama k to the Depth-Anything-V2-Small input (518 x 1036,
+keep-aspect /14) and runs the network (seeded random weights) -- all ranks at once -- then
+for each panorama its owner broadcasts the 518 x 1036 depth over RCCL and every rank
+unprojects its band of it (ms_per_image = a step / its N panoramas: network / N + broadcast +
+band call).  --projection equirect back-projects the panorama on the sphere (i2pc.h; the
+reference only has the pinhole model); --smooth applies smooth_depth (the band's blurred field
+with its halo rows, recomputed locally); --levels takes the four histogram levels with a host
+exchange instead of the one-sweep window selection.
 """
 import argparse
 import json
@@ -44,6 +48,9 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay each rank's band call as a HIP graph (RCCL mode)")
     ap.add_argument("--network", action="store_true", help="depth from Depth-Anything-V2-Small on rank 0, broadcast")
     ap.add_argument("--projection", default="pinhole", choices=["pinhole", "equirect"])
+    ap.add_argument("--smooth", action="store_true", help="smooth_depth (GaussianBlur, --ksize)")
+    ap.add_argument("--ksize", type=int, default=5)
+    ap.add_argument("--levels", action="store_true", help="histogram-level selection, host-callback exchange")
     a = ap.parse_args()
     rank, local, world = D.world()
     ngpu = torch.cuda.device_count()
@@ -68,42 +75,53 @@ def main():
     for y in range(r0, r1):
         band[y - r0] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
     timg = torch.from_numpy(band).to(dev)
-    net = None
+    nets = world if a.network else 1        # panoramas per step
     if a.network:
         from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL
         from image_to_pointcloud_amd.pipeline import PointCloudPipeline
-        if rank == 0:
-            full = np.empty((H, W, 3), np.uint8)
-            for y in range(H):
-                full[y] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
-            tfull = torch.from_numpy(full).to(dev)[None]
-            net = PointCloudPipeline(1, H, W, spec=DA_V2_SMALL, density=a.density, device=dev)
-            h, w = net.pre.out_h, net.pre.out_w
-            del full
-        hw = torch.tensor([h, w], device=dev)
-        if world > 1:
-            dist.broadcast(hw, 0)
-        h, w = int(hw[0]), int(hw[1])
-        tdep = torch.empty((h, w), dtype=torch.float32, device=dev)
+        full = np.empty((H, W, 3), np.uint8)    # this rank's panorama of the step (same content on every rank)
+        for y in range(H):
+            full[y] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
+        tfull = torch.from_numpy(full).to(dev)[None]
+        net = PointCloudPipeline(1, H, W, spec=DA_V2_SMALL, density=a.density, device=dev)
+        h, w = net.pre.out_h, net.pre.out_w
+        del full
+        own = torch.empty((h, w), dtype=torch.float32, device=dev)
+        deps = [torch.empty((h, w), dtype=torch.float32, device=dev) for _ in range(world)]
 
         def infer():
-            if rank == 0:
-                tdep.copy_(net.infer_depth(tfull)[0])
-            if world > 1:
-                dist.broadcast(tdep, 0)
+            own.copy_(net.infer_depth(tfull)[0])        # every rank: its own panorama's depth
+            for k in range(world):                      # then panorama k's depth from its owner
+                if world > 1:
+                    if k == rank:
+                        deps[k].copy_(own)
+                    dist.broadcast(deps[k], k)
+                else:
+                    deps[k].copy_(own)
         infer()
-    comm = D.RcclComm() if world > 1 and backend == "nccl" else (D.RcclComm(nranks=1, rank=0) if world == 1 else None)
+        tdep = deps[0]
+    if a.levels:
+        comm = None
+    else:
+        comm = D.RcclComm() if world > 1 and backend == "nccl" else (D.RcclComm(nranks=1, rank=0) if world == 1 else None)
     ex = D.band_exchange() if comm is None else None
-    ws = torch.empty(G.workspace_bytes(1, H, W), dtype=torch.uint8, device=dev)
+    gather = D.band_gather() if comm is None and not a.levels else None
+    nbytes = (G.band_workspace_bytes(H, W, a.smooth, world) if comm is not None or gather is not None
+              else G.workspace_bytes(1, H, W, a.smooth))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     res = None
 
-    def band_call():
-        return G.unproject_band(tdep, timg, H, W, r0, r1, ex, density=a.density, comm=comm, workspace=ws, out=res,
-                                projection=a.projection)
+    def band_call(d=None):
+        return G.unproject_band(tdep if d is None else d, timg, H, W, r0, r1, ex, density=a.density, comm=comm,
+                                workspace=ws, out=res, projection=a.projection, smooth=a.smooth,
+                                smooth_ksize=a.ksize, gather=gather, nranks=world if gather else None)
 
     def run():
         if a.network:
             infer()
+            for k in range(world):
+                r = band_call(deps[k])
+            return r
         return band_call()
     for _ in range(max(1, a.warmup)):
         res = run()
@@ -113,7 +131,16 @@ def main():
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             band_call()
-        step_fn = (lambda: (infer(), graph.replay())) if a.network else graph.replay
+        if a.network:
+            graphs = []
+            for k in range(world):
+                gk = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gk):
+                    band_call(deps[k])
+                graphs.append(gk)
+            step_fn = lambda: (infer(), [gk.replay() for gk in graphs])   # noqa: E731
+        else:
+            step_fn = graph.replay
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -129,8 +156,10 @@ def main():
         full = np.empty((H, W, 3), np.uint8)
         for y in range(H):
             full[y] = np.random.Generator(np.random.PCG64(1000 + y)).integers(0, 256, (W, 3), dtype=np.uint8)
+        if a.network:
+            tdep = deps[world - 1]      # the last band call of the step unprojected the last panorama
         whole = G.unproject_batch(tdep[None], torch.from_numpy(full).to(dev)[None], density=a.density,
-                                  projection=a.projection)
+                                  projection=a.projection, smooth=a.smooth, smooth_ksize=a.ksize)
         wn = (W + step - 1) // step
         p0 = (r0 // step) * wn
         ok = bool(torch.equal(whole.xyz[0][p0:p0 + res[0].shape[0]], res[0])
@@ -144,12 +173,17 @@ def main():
     n = ((H + step - 1) // step) * ((W + step - 1) // step)
     if rank == 0:
         print(json.dumps({"metric": "Mpoints/sec tile-parallel unprojection of one panorama (C4)",
-                          "value": round(n * a.steps / el / 1e6, 1), "unit": "Mpoints/s", "n_ranks": world,
+                          "value": round(n * nets * a.steps / el / 1e6, 1), "unit": "Mpoints/s", "n_ranks": world,
                           "backend": backend if world > 1 else None,
-                          "exchange": "RCCL on device (i2pc_unproject_band_rccl)" if comm is not None else "host callback",
-                          "hip_graph": bool(a.graph and comm is not None), "ms_per_image": round(el / a.steps * 1e3, 3),
+                          "exchange": ("RCCL on device (i2pc_unproject_band_rccl: counters all-reduce + window "
+                                       "candidates all-gather)" if comm is not None else
+                                       "host callback (" + ("histogram levels" if a.levels else "window selection") + ")"),
+                          "hip_graph": bool(a.graph and comm is not None),
+                          "ms_per_image": round(el / (a.steps * nets) * 1e3, 3), "panoramas_per_step": nets,
+                          "smooth": a.smooth,
                           "image": [H, W], "depth": [h, w], "density": a.density, "points": n,
-                          "depth_source": "depth-anything-v2-small (seeded weights) on rank 0 + RCCL broadcast"
+                          "depth_source": "depth-anything-v2-small (seeded weights): panorama k on rank k, "
+                                          "RCCL broadcast from its owner"
                           if a.network else "synthetic smooth field + NaN",
                           "projection": a.projection,
                           "bit_exact_vs_whole_image": ok, "stats": res[3].tolist(), "bbox": bbox.tolist()}))

@@ -16,6 +16,7 @@
 #   unp                        geometry parity tests, unprojection microbench (warm / cold) per kernel variant
 #   trace-unp [B] [density]    kernel durations of the unprojection microbench (kernel trace only)
 #   pmc-unp                    SQ counters of the unprojection microbench
+#   c4                         tools/c4_panorama.py on one rank: window / levels / smooth / equirect / network stream
 set -o pipefail
 R=${ROUND:-r03}
 TASK=$1; shift
@@ -148,5 +149,18 @@ case "$TASK" in
     timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -d $D/p1 -o p1 --output-format csv -- python tools/bench_unproject.py 32 > $D/p1.txt 2>&1 || exit 1
     timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS --kernel-trace -d $D/p2 -o p2 --output-format csv -- python tools/bench_unproject.py 32 > $D/p2.txt 2>&1 || exit 1
     python tools/pmc_summary.py $D/p1 unproj:: && python tools/pmc_summary.py $D/p2 unproj:: ;;
+  c4)         # C4 panorama, one rank: window selection (RCCL, graph), levels (host exchange), smooth, network stream
+    : > gpurun_out/c4.jsonl
+    for v in "--graph --check" "--levels --check" "--graph --smooth --check" "--graph --projection equirect --check" \
+             "--graph --network --check"; do
+      timeout -k 10 300 python -u tools/c4_panorama.py --steps 20 $v >> gpurun_out/c4.jsonl 2> gpurun_out/c4.err \
+        || { tail -5 gpurun_out/c4.err; exit 1; }
+    done
+    cut -c1-330 gpurun_out/c4.jsonl ;;
+  trace-c4)   # kernel durations of the one-rank C4 band call (window selection; args: extra c4_panorama flags)
+    D=gpurun_out/trace_c4; rm -rf $D; mkdir -p $D
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/t -o t --output-format csv -- \
+      python tools/c4_panorama.py --steps 10 "$@" > $D/run.txt 2>&1 || { tail -5 $D/run.txt; exit 1; }
+    grep -o '"ms_per_image": [0-9.]*' $D/run.txt; stats $D/t unproj ;;
   *) echo "unknown task '$TASK' (see the header of tools/gpu.sh)"; exit 2 ;;
 esac
