@@ -65,10 +65,13 @@ __global__ __launch_bounds__(256) void k_stem_im2col(const float* __restrict__ x
 // GroupNorm statistics in two launches, no atomics:
 //  k_gn_partial: one workgroup = one image x PIX pixels; thread t owns 8 consecutive channels
 //    of pixel lane t / (C / 8) and accumulates their sums / sums of squares over the tile in
-//    registers (fp32); the pixel lanes reduce through LDS and the workgroup writes one
-//    (sum, sumsq) pair per group to part[b][tile][g].
-//  k_gn_finalize: one wave per (image, group) adds the tile partials in fp64 and writes
-//    (mean, rstd) as float: stats[b][g] (biased variance, as nn.functional.group_norm).
+//    registers (fp32) SHIFTED by each channel's value at the tile's first pixel (so a mean far
+//    above the spread -- BiT activations after a residual -- does not cancel E[x^2] - mean^2
+//    away); the pixel lanes reduce through LDS and the workgroup writes one (mean, M2) pair per
+//    group to part[b][tile][g] (channels combined by Chan's formula).
+//  k_gn_finalize: one wave per (image, group) merges the tile pairs in fp64 (Chan's parallel
+//    formula) and writes (mean, rstd) as float: stats[b][g] (biased variance, as
+//    nn.functional.group_norm).
 // pixels per workgroup: up to 512, fewer when that would leave < ~8 workgroups per CU
 static int gn_pix(int batch, int hw) {
   const int64_t want = ((int64_t)batch * hw + 2047) / 2048;
@@ -85,24 +88,32 @@ __global__ __launch_bounds__(256) void k_gn_partial(const bf16_t* __restrict__ x
   const int p0 = tile * PIX;
   const int cc = threadIdx.x % chunks;
   const int pl = threadIdx.x / chunks;
-  float s[8] = {}, q[8] = {};
+  float s[8] = {}, q[8] = {}, k8[8];
+  {
+    // the shift: channel value at the tile's first pixel (the same for every pixel lane)
+    uint4 u0 = *reinterpret_cast<const uint4*>(x + ((int64_t)b * HW + p0) * C + cc * 8);
+    const uint32_t w0[4] = {u0.x, u0.y, u0.z, u0.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { k8[2 * e] = __uint_as_float(w0[e] << 16); k8[2 * e + 1] = __uint_as_float(w0[e] & 0xffff0000u); }
+  }
+  const int p1 = min(p0 + PIX, HW);
   if (pl < per_it) {
     const bf16_t* xb = x + (int64_t)b * HW * C + cc * 8;
-    const int p1 = min(p0 + PIX, HW);
     constexpr int U = 8;                           // 8 independent 16-B loads in flight
     for (int pb = p0 + pl; pb < p1; pb += U * per_it) {
       uint4 u[U];
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const int p = pb + k * per_it;
-        u[k] = p < p1 ? *reinterpret_cast<const uint4*>(xb + (int64_t)p * C) : make_uint4(0, 0, 0, 0);
+        u[k] = *reinterpret_cast<const uint4*>(xb + (int64_t)min(p, p1 - 1) * C);
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
+        if (pb + k * per_it >= p1) continue;      // (past the tile: loaded clamped, not counted)
         const uint32_t w[4] = {u[k].x, u[k].y, u[k].z, u[k].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float a = __uint_as_float(w[e] << 16), c = __uint_as_float(w[e] & 0xffff0000u);
+          const float a = __uint_as_float(w[e] << 16) - k8[2 * e], c = __uint_as_float(w[e] & 0xffff0000u) - k8[2 * e + 1];
           s[2 * e] += a; q[2 * e] = fmaf(a, a, q[2 * e]);
           s[2 * e + 1] += c; q[2 * e + 1] = fmaf(c, c, q[2 * e + 1]);
         }
@@ -119,19 +130,29 @@ __global__ __launch_bounds__(256) void k_gn_partial(const bf16_t* __restrict__ x
     }
   }
   __syncthreads();
+  // per channel: mean and M2 over the tile's pixels from the shifted sums
+  const float nt = (float)(p1 - p0);
   for (int c = threadIdx.x; c < C; c += 256) {
     float a = 0.f, d = 0.f;
     for (int l = 0; l < per_it; ++l) { a += red[0][l * C + c]; d += red[1][l * C + c]; }
-    red[0][c] = a;            // (only this thread reads column c, and row 0 is its own slot)
-    red[1][c] = d;
+    const bf16_t kc = x[((int64_t)b * HW + p0) * C + c];
+    const float m = a / nt;
+    red[0][c] = __uint_as_float((uint32_t)kc << 16) + m;   // (only this thread reads column c, and row 0 is its own slot)
+    red[1][c] = fmaxf(d - a * m, 0.f);
   }
   __syncthreads();
   const int cg = C / G;
   for (int g = threadIdx.x; g < G; g += 256) {
-    float a = 0.f, d = 0.f;
-    for (int k = 0; k < cg; ++k) { a += red[0][g * cg + k]; d += red[1][g * cg + k]; }
-    part[(((int64_t)b * tiles + tile) * G + g) * 2] = a;
-    part[(((int64_t)b * tiles + tile) * G + g) * 2 + 1] = d;
+    float mg = 0.f;
+    for (int k = 0; k < cg; ++k) mg += red[0][g * cg + k];
+    mg /= (float)cg;
+    float m2 = 0.f;
+    for (int k = 0; k < cg; ++k) {
+      const float dm = red[0][g * cg + k] - mg;
+      m2 += red[1][g * cg + k] + nt * dm * dm;
+    }
+    part[(((int64_t)b * tiles + tile) * G + g) * 2] = mg;
+    part[(((int64_t)b * tiles + tile) * G + g) * 2 + 1] = m2;
   }
 }
 
@@ -139,25 +160,29 @@ __global__ __launch_bounds__(256) void k_gn_partial(const bf16_t* __restrict__ x
 // t, t + 64, ...), then a butterfly over the wave.  (A thread per (image, group) walking the
 // tiles serially was latency-bound: 8.8 us per call, 52 calls per DPT-Hybrid step.)
 __global__ __launch_bounds__(256) void k_gn_finalize(const float* __restrict__ part, int B, int G, int tiles,
-                                                     double inv_n, float eps, float* __restrict__ stats) {
+                                                     int HW, int PIX, int cg, float eps, float* __restrict__ stats) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= B * G) return;
   const int b = i / G, g = i - (i / G) * G;
-  double a = 0.0, d = 0.0;
+  // Chan: (n, mean, M2) of two parts -> the union's
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  auto merge = [&](double nb, double mb, double m2b) {
+    if (nb == 0.0) return;
+    const double nn = n + nb, dlt = mb - mean;
+    mean += dlt * (nb / nn);
+    m2 += m2b + dlt * dlt * (n * nb / nn);
+    n = nn;
+  };
   for (int t = lane; t < tiles; t += 64) {
     const float2 pr = *reinterpret_cast<const float2*>(part + (((int64_t)b * tiles + t) * G + g) * 2);
-    a += pr.x;
-    d += pr.y;
+    merge((double)(min(PIX, HW - t * PIX) * cg), pr.x, pr.y);
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    a += __shfl_xor(a, o);
-    d += __shfl_xor(d, o);
-  }
+  for (int o = 32; o > 0; o >>= 1)
+    merge(__shfl_xor(n, o), __shfl_xor(mean, o), __shfl_xor(m2, o));
   if (lane == 0) {
-    const double mean = a * inv_n;
-    const double var = fmax(d * inv_n - mean * mean, 0.0);
+    const double var = fmax(m2 / n, 0.0);
     stats[2 * i] = (float)mean;
     stats[2 * i + 1] = 1.0f / sqrtf((float)var + eps);
   }
@@ -407,8 +432,8 @@ extern "C" int i2pc_groupnorm_stats(const void* x, int batch, int hw, int c, int
   hipLaunchKernelGGL(k_gn_partial, dim3(batch * tiles), dim3(256), 0, s, static_cast<const bf16_t*>(x), hw, c, groups,
                      tiles, pix, part);
   const int n = batch * groups;
-  hipLaunchKernelGGL(k_gn_finalize, dim3((n + 3) / 4), dim3(256), 0, s, part, batch, groups, tiles,
-                     1.0 / ((double)hw * (c / groups)), eps, stats);
+  hipLaunchKernelGGL(k_gn_finalize, dim3((n + 3) / 4), dim3(256), 0, s, part, batch, groups, tiles, hw, pix,
+                     c / groups, eps, stats);
   return check_launch("groupnorm_stats");
 }
 

@@ -44,7 +44,7 @@ constexpr int kBins = 2048;
 constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
 constexpr int kSlowBlock = 1024;
-constexpr int kRangeChunks = 32;
+constexpr int kRangeChunks = 32;         // k_prepare workgroups per image, at least (range_chunks)
 constexpr int kSampleChunks = 8;          // k_model_hist workgroups (partial sample histograms) per image, at least
 constexpr int kMaxSampleChunks = 128;     // ... at most (large images: up to ~1 M samples, 8 K per workgroup)
 constexpr int kHistBlock = 1024;          // k_model_hist: threads per (image, chunk) workgroup (~8 samples each)
@@ -173,6 +173,10 @@ static SamplePlan sample_plan(int H, int W) {
   return sp;
 }
 
+// k_prepare's workgroups per image (the model map's key-range partials): 32, more for small
+// batches so a single large image still spreads over the chip
+static int range_chunks(int B) { return std::min(256, std::max(kRangeChunks, 256 / std::max(B, 1))); }
+
 static Layout layout(int B, int H, int W, int smooth, int nranks = 0) {
   Layout L{};
   size_t off = 0;
@@ -180,12 +184,12 @@ static Layout layout(int B, int H, int W, int smooth, int nranks = 0) {
   L.state = off; off = align_up(off + sizeof(SelState) * (size_t)B, 256);
   L.hist = off;  off = align_up(off + sizeof(uint32_t) * kSlots * kBins * (size_t)B, 256);
   L.cand = off;  off = align_up(off + sizeof(uint32_t) * kSlots * (size_t)L.cap * B, 256);
-  L.rpart = off; off = align_up(off + sizeof(uint32_t) * 2 * kRangeChunks * (size_t)B, 256);
+  L.rpart = off; off = align_up(off + sizeof(uint32_t) * 2 * range_chunks(B) * (size_t)B, 256);
   L.xtab = off;  off = align_up(off + sizeof(Tap) * (size_t)W, 256);
   L.ytab = off;  off = align_up(off + sizeof(Tap) * (size_t)H, 256);
   L.trig = off;  off = align_up(off + sizeof(double) * 2 * ((size_t)W + H), 256);
   L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)std::max(B, kBandEx), 256);
-  L.mhist = off; off = align_up(off + sizeof(uint32_t) * sample_plan(H, W).nch * kBins * (size_t)B, 256);
+  L.mhist = off; off = align_up(off + sizeof(uint32_t) * kBins * (size_t)B, 256);
   L.gsend = off; off = align_up(off + (nranks > 0 ? sizeof(uint32_t) * kBandWords : 0), 256);
   L.grecv = off; off = align_up(off + sizeof(uint32_t) * kBandWords * (size_t)std::max(nranks, 0), 256);
   L.field = off;
@@ -380,7 +384,8 @@ __device__ __forceinline__ bool key_nonfinite(uint32_t k) { return k >= kKeyPosI
 // as per-chunk partials (k_model_hist reduces them).
 __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, int m, int n, SelState* st,
                                                     uint32_t* hist, uint32_t* rpart, Tap* xt, Tap* yt, int dh, int dw,
-                                                    int H, int W, double sx, double sy, double* trig) {
+                                                    int H, int W, double sx, double sy, double* trig, uint32_t* mhist,
+                                                    int nrc) {
   __shared__ uint32_t red[2][kBlock / 64];
   const int gtid = blockIdx.x * kBlock + threadIdx.x;
   const int nthr = gridDim.x * kBlock;
@@ -411,6 +416,8 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
   }
   if (hist)        // (the level histograms: band path only)
     for (size_t i = gtid; i < (size_t)B * kSlots * kBins; i += nthr) hist[i] = 0;
+  if (mhist)       // the sample histograms k_model_hist adds into
+    for (size_t i = gtid; i < (size_t)B * kBins; i += nthr) mhist[i] = 0;
   if (trig) {       // equirectangular ray tables (the oracle evaluates the same expressions)
     const double pi = 3.141592653589793;
     for (int i = gtid; i < W + H; i += nthr) {
@@ -432,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
   };
   if ((m & 3) == 0) {
     const int m4 = m >> 2;
-    const int per = (m4 + kRangeChunks - 1) / kRangeChunks;
+    const int per = (m4 + nrc - 1) / nrc;
     const int i1 = min(m4, (c + 1) * per);
     const float4* D4 = reinterpret_cast<const float4*>(D);
     for (int i = c * per + threadIdx.x; i < i1; i += kBlock) {
@@ -440,7 +447,7 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
       take(v.x); take(v.y); take(v.z); take(v.w);
     }
   } else {
-    const int per = (m + kRangeChunks - 1) / kRangeChunks;
+    const int per = (m + nrc - 1) / nrc;
     const int i1 = min(m, (c + 1) * per);
     for (int i = c * per + threadIdx.x; i < i1; i += kBlock) take(D[i]);
   }
@@ -450,17 +457,17 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < kBlock / 64; ++w) { lo = min(lo, red[0][w]); hi = max(hi, red[1][w]); }
-    rpart[((size_t)b * kRangeChunks + c) * 2] = lo;
-    rpart[((size_t)b * kRangeChunks + c) * 2 + 1] = hi;
+    rpart[((size_t)b * nrc + c) * 2] = lo;
+    rpart[((size_t)b * nrc + c) * 2 + 1] = hi;
   }
 }
 
 // Level-0 histogram of a sample of each full-resolution map (finite values, the level-0 binning):
-// one partial histogram per (image, chunk) in `mhist` [B][kSampleChunks][kBins], summed by k_window
-// (no global atomics: every chunk's workgroup sees most bins of its image).  The estimate k_window
+// every (image, chunk) workgroup adds its LDS histogram's non-empty bins into `mhist` [B][kBins]
+// (zeroed by k_prepare) with global atomics.  The estimate k_window
 // predicts the target bins from.
 __global__ __launch_bounds__(kHistBlock) void k_model_hist(Geo g, int B, SelState* st, uint32_t* mhist,
-                                                       const uint32_t* rpart, int stride, int nch) {
+                                                       const uint32_t* rpart, int stride, int nch, int nrc) {
   __shared__ __attribute__((aligned(16))) uint32_t lh[kBins];
   __shared__ uint32_t rr[2];
   const int b = blockIdx.x % B, c = blockIdx.x / B;
@@ -468,9 +475,9 @@ __global__ __launch_bounds__(kHistBlock) void k_model_hist(Geo g, int B, SelStat
   for (int i = threadIdx.x; i < kBins; i += kHistBlock) lh[i] = 0;
   if (threadIdx.x < 64) {     // the image's key range from k_prepare's partials
     uint32_t lo = 0xffffffffu, hi = 0u;
-    if (threadIdx.x < kRangeChunks) {
-      lo = rpart[((size_t)b * kRangeChunks + threadIdx.x) * 2];
-      hi = rpart[((size_t)b * kRangeChunks + threadIdx.x) * 2 + 1];
+    for (int i = threadIdx.x; i < nrc; i += 64) {
+      lo = min(lo, rpart[((size_t)b * nrc + i) * 2]);
+      hi = max(hi, rpart[((size_t)b * nrc + i) * 2 + 1]);
     }
     lo = wave_min_u32(lo);
     hi = wave_max_u32(hi);
@@ -550,9 +557,9 @@ __global__ __launch_bounds__(kHistBlock) void k_model_hist(Geo g, int B, SelStat
   }
   if (run >= 0) atomicAdd(&lh[run], cnt);
   __syncthreads();
-  uint4* gh = reinterpret_cast<uint4*>(mhist + ((size_t)b * nch + c) * kBins);
-  const uint4* l4 = reinterpret_cast<const uint4*>(lh);
-  for (int i = threadIdx.x; i < kBins / 4; i += kHistBlock) gh[i] = l4[i];
+  uint32_t* gh = mhist + (size_t)b * kBins;       // (zeroed by k_prepare)
+  for (int i = threadIdx.x; i < kBins; i += kHistBlock)
+    if (lh[i]) atomicAdd(&gh[i], lh[i]);
 }
 
 // Block histogram in LDS as packed 16-bit counts (bin pairs share a word; a sweep workgroup
@@ -1318,18 +1325,12 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
   const int b = blockIdx.x;
   if (b >= B) return;
   SelState* S = st + b;
-  // the sample histogram: k_model_hist's per-chunk partials summed (8 bins per thread, all loads in flight)
+  // the sample histogram (8 bins per thread)
   uint32_t local = 0;
   {
     static_assert(kBins == 8 * kBlock, "k_window: 8 bins per thread");
-    const uint4* src = reinterpret_cast<const uint4*>(mhist + (size_t)b * nch * kBins) + 2 * threadIdx.x;
-    uint4 acc0 = make_uint4(0, 0, 0, 0), acc1 = make_uint4(0, 0, 0, 0);
-#pragma unroll 8
-    for (int c = 0; c < nch; ++c) {
-      const uint4 x = src[c * (kBins / 4)], y = src[c * (kBins / 4) + 1];
-      acc0.x += x.x; acc0.y += x.y; acc0.z += x.z; acc0.w += x.w;
-      acc1.x += y.x; acc1.y += y.y; acc1.z += y.z; acc1.w += y.w;
-    }
+    const uint4* src = reinterpret_cast<const uint4*>(mhist + (size_t)b * kBins) + 2 * threadIdx.x;
+    const uint4 acc0 = src[0], acc1 = src[1];
     reinterpret_cast<uint4*>(mh)[2 * threadIdx.x] = acc0;
     reinterpret_cast<uint4*>(mh)[2 * threadIdx.x + 1] = acc1;
     local = acc0.x + acc0.y + acc0.z + acc0.w + acc1.x + acc1.y + acc1.z + acc1.w;
@@ -3096,6 +3097,29 @@ __global__ __launch_bounds__(kBlock) void k_bandw_final(SelState* st, const uint
     __syncthreads();
     if (bad) return;
     if (ng == 0) continue;
+    if (tot <= (uint32_t)kBins) {
+      // the usual case (tens of keys per fine bin and band): the bin's keys in LDS, each key's
+      // rank range counted against all of them
+      for (int r = 0; r < nranks; ++r) {
+        const uint32_t o = offs[r], n = offs[r + 1] - o;
+        const uint32_t* src = recv + (size_t)r * kBandWords + (size_t)t0 * kPickWords + 3;
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock) lh[o + i] = src[i];
+      }
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < tot; i += kBlock) {
+        const uint32_t k = lh[i];
+        uint32_t less = 0, leq = 0;
+        for (uint32_t q = 0; q < tot; ++q) {
+          const uint32_t v = lh[q];
+          less += v < k ? 1u : 0u;
+          leq += v <= k ? 1u : 0u;
+        }
+        for (int q = 0; q < ng; ++q)
+          if (less <= ranks[q] && ranks[q] < leq) S->tlo[who[q]] = S->thi[who[q]] = k;   // (equal keys: same value)
+      }
+      __syncthreads();
+      continue;
+    }
     uint32_t* keys = scratch + base;
     for (int r = 0; r < nranks; ++r) {
       const uint32_t o = offs[r], n = offs[r + 1] - o;
@@ -3186,12 +3210,14 @@ static thread_local int g_sel_rows = [] {
 
 static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, const uint32_t* rpart,
                          uint32_t* mhist, uint32_t cap, int B, const Sweep& sw, hipStream_t s,
-                         const Exchange* x = nullptr) {
+                         const Exchange* x = nullptr, int nrc = 0) {
+  if (nrc <= 0) nrc = range_chunks(B);
   // full-resolution sample of ~64 K points per image for the level-0 estimate
   const SamplePlan sp = sample_plan(g.H, g.W);
   // windows: the batch path, and band runs that can all-gather their candidate lists
   const bool win = x ? x->gather != nullptr : g_sel_windows != 0;
-  hipLaunchKernelGGL(k_model_hist, dim3(B * sp.nch), dim3(kHistBlock), 0, s, g, B, st, mhist, rpart, sp.stride, sp.nch);
+  hipLaunchKernelGGL(k_model_hist, dim3(B * sp.nch), dim3(kHistBlock), 0, s, g, B, st, mhist, rpart, sp.stride, sp.nch,
+                     nrc);
   hipLaunchKernelGGL(k_window, dim3(B), dim3(kBlock), 0, s, st, mhist, cap, B, win ? 1 : 0, sp.ns, sp.nch);
   if (win) {
     // batch path: one window-only sweep + resolve; k_sel_slow finishes (or, for the rare image
@@ -3277,6 +3303,40 @@ extern "C" size_t i2pc_unproject_workspace_bytes(int batch, int img_h, int img_w
   return layout(batch, img_h, img_w, smooth).total;
 }
 
+// Forked selection chains (batch path): per host thread and device, side streams and the
+// fork / join events (thread-local, so concurrent callers on other threads never share them).
+// "sel_parts" (I2PC_SEL_PARTS): sub-batches of the selection chain; 0 = automatic = 1.
+// Measured r03 (B = 32 x 1024^2, whole call): 1 part 254 us, 2 parts 271, 3 parts 289, 4 parts
+// 311 -- the halves' launches do not overlap enough to pay for the split sweeps, so it stays off.
+constexpr int kMaxParts = 4;
+struct AuxStreams {
+  bool ok = false;
+  int dev = -1;
+  hipStream_t s[kMaxParts - 1] = {};
+  hipEvent_t fork = nullptr, join[kMaxParts - 1] = {};
+};
+static thread_local int g_sel_parts = [] { const char* e = getenv("I2PC_SEL_PARTS"); return e ? atoi(e) : 0; }();
+static int select_parts(int batch) {
+  if (!g_sel_windows) return 1;
+  const int p = g_sel_parts > 0 ? std::min(g_sel_parts, kMaxParts) : 1;
+  return std::max(1, std::min(p, batch));
+}
+static AuxStreams& aux_streams(int need) {
+  static thread_local AuxStreams ax[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) { static thread_local AuxStreams bad; return bad; }
+  AuxStreams& a = ax[dev];
+  if (!a.ok) {
+    a.ok = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < kMaxParts - 1 && a.ok; ++i)
+      a.ok = hipStreamCreateWithFlags(&a.s[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&a.join[i], hipEventDisableTiming) == hipSuccess;
+    a.dev = dev;
+  }
+  (void)need;
+  return a;
+}
+
 // Band [row0, row1) of the image rows (the whole image when row0 = 0, row1 = img_h);
 // `image`, `xyz`, `rgb` address the full image (band runs pass offset pointers).
 static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t* image, int channels,
@@ -3308,8 +3368,10 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   const int n = img_h * img_w;
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
   double* trig = params->projection == 1 ? reinterpret_cast<double*>(ws + L.trig) : nullptr;
-  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n, st,
-                     (xch || !g_sel_windows) ? hist : nullptr, rpart, xt, yt, dep_h, dep_w, img_h, img_w, cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig);
+  hipLaunchKernelGGL(k_prepare, dim3(batch * range_chunks(batch)), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n,
+                     st, (xch || !g_sel_windows) ? hist : nullptr, rpart, xt, yt, dep_h, dep_w, img_h, img_w,
+                     cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig, reinterpret_cast<uint32_t*>(ws + L.mhist),
+                     range_chunks(batch));
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
@@ -3322,9 +3384,34 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   xb.send = reinterpret_cast<uint32_t*>(ws + L.gsend);
   xb.recv = reinterpret_cast<uint32_t*>(ws + L.grecv);
   uint32_t* cand = reinterpret_cast<uint32_t*>(ws + L.cand);
-  int rc = launch_select(g, st, hist, cand, rpart, reinterpret_cast<uint32_t*>(ws + L.mhist), L.cap, batch, ssel, s,
-                         xch ? &xb : nullptr);
-  if (rc) return rc;
+  uint32_t* mhist = reinterpret_cast<uint32_t*>(ws + L.mhist);
+  const int nrc = range_chunks(batch);
+  int rc;
+  const int parts = xch ? 1 : select_parts(batch);
+  if (parts > 1) {
+    // the selection chain is mostly latency-bound small launches: run it as `parts` sub-batches
+    // on forked streams so their launches overlap, then join for one unprojection launch
+    AuxStreams& ax = aux_streams(parts - 1);
+    if (!ax.ok) return set_error(I2PC_ELAUNCH, "cannot create the selection side streams");
+    if (hipEventRecord(ax.fork, s) != hipSuccess) return set_error(I2PC_ELAUNCH, "hipEventRecord failed");
+    for (int q = 0; q < parts; ++q) {
+      const int b0 = batch * q / parts, b1 = batch * (q + 1) / parts;
+      hipStream_t sq = q == 0 ? s : ax.s[q - 1];
+      if (q > 0 && hipStreamWaitEvent(sq, ax.fork, 0) != hipSuccess) return set_error(I2PC_ELAUNCH, "hipStreamWaitEvent failed");
+      Geo gq = g;
+      gq.depth = g.depth + (size_t)b0 * dep_h * dep_w;
+      rc = launch_select(gq, st + b0, hist + (size_t)b0 * kSlots * kBins, cand + (size_t)b0 * kSlots * L.cap,
+                         rpart + (size_t)b0 * nrc * 2, mhist + (size_t)b0 * kBins, L.cap, b1 - b0, ssel, sq, nullptr, nrc);
+      if (rc) return rc;
+      if (q > 0) {
+        if (hipEventRecord(ax.join[q - 1], sq) != hipSuccess || hipStreamWaitEvent(s, ax.join[q - 1], 0) != hipSuccess)
+          return set_error(I2PC_ELAUNCH, "stream join failed");
+      }
+    }
+  } else {
+    rc = launch_select(g, st, hist, cand, rpart, mhist, L.cap, batch, ssel, s, xch ? &xb : nullptr, nrc);
+    if (rc) return rc;
+  }
 
   Cam cam;
   cam.cx = img_w / 2.0;
@@ -3504,8 +3591,9 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
   Tap* yt = reinterpret_cast<Tap*>(ws + L.ytab);
   const int n = h * w;
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
-  hipLaunchKernelGGL(k_prepare, dim3(batch * kRangeChunks), dim3(kBlock), 0, s, depth, batch, n, n, st,
-                     g_sel_windows ? nullptr : hist, rpart, xt, yt, h, w, h, w, 1.0, 1.0, nullptr);
+  hipLaunchKernelGGL(k_prepare, dim3(batch * range_chunks(batch)), dim3(kBlock), 0, s, depth, batch, n, n, st,
+                     g_sel_windows ? nullptr : hist, rpart, xt, yt, h, w, h, w, 1.0, 1.0, nullptr,
+                     reinterpret_cast<uint32_t*>(ws + L.mhist), range_chunks(batch));
   Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
   const Sweep ssel = plan_select(h, w, h, w, true, 0, h);
   int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart,
@@ -3523,6 +3611,7 @@ bool i2pc_unproject_tune(const char* name, int value) {
   if (std::strcmp(name, "unp_nt") == 0) { i2pc::unproj::g_unp_nt = value; return true; }
   if (std::strcmp(name, "unp_rpt") == 0) { i2pc::unproj::g_unp_rpt = value; return true; }
   if (std::strcmp(name, "sel_windows") == 0) { i2pc::unproj::g_sel_windows = value; return true; }
+  if (std::strcmp(name, "sel_parts") == 0) { g_sel_parts = value; return true; }
   if (std::strcmp(name, "sel_rows") == 0) {
     i2pc::unproj::g_sel_rows = value > 0 && value <= i2pc::unproj::kMaxSelRows ? value : 16;
     return true;

@@ -129,10 +129,15 @@ def band_exchange(group=None):
     def _exchange(hist, counters):
         if not dist.is_initialized():       # one rank: the sums / min / max are its own values
             return
+        host = dist.get_backend(group) == "gloo"    # gloo: reduce host copies (ranks may share a GPU)
         if hist is not None:                # (None: the window mode's counters-only exchange)
-            dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+            h = hist.cpu() if host else hist
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            if host:
+                hist.copy_(h)
         if counters is not None:
-            sums, kmin, kmax = counters[:2].contiguous(), counters[2].contiguous(), counters[3].contiguous()
+            c = counters.cpu() if host else counters
+            sums, kmin, kmax = c[:2].contiguous(), c[2].contiguous(), c[3].contiguous()
             dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
             dist.all_reduce(kmin, op=dist.ReduceOp.MIN, group=group)
             dist.all_reduce(kmax, op=dist.ReduceOp.MAX, group=group)
@@ -145,20 +150,28 @@ def band_exchange(group=None):
 def band_gather(group=None):
     """The all-gather of the window-selection band mode (i2pc_unproject_band_w): every rank's
     candidate words into recv [nranks, words]."""
+    import torch
     import torch.distributed as dist
 
     def _gather(send, recv):
         if not dist.is_initialized():
             recv[0].copy_(send)
             return
-        dist.all_gather(list(recv.unbind(0)), send, group=group)
+        if dist.get_backend(group) == "gloo":
+            r = torch.empty(recv.shape, dtype=recv.dtype)
+            dist.all_gather(list(r.unbind(0)), send.cpu(), group=group)
+            recv.copy_(r)
+        else:
+            dist.all_gather(list(recv.unbind(0)), send, group=group)
     return _gather
 
 
 def reduce_bbox(bbox, group=None):
     """Global bounds from per-band bboxes [6] (min x, max x, min y, max y, min z, max z)."""
     import torch.distributed as dist
-    mins, maxs = bbox[0::2].contiguous(), bbox[1::2].contiguous()
+    host = dist.get_backend(group) == "gloo"
+    b = bbox.cpu() if host else bbox
+    mins, maxs = b[0::2].contiguous(), b[1::2].contiguous()
     dist.all_reduce(mins, op=dist.ReduceOp.MIN, group=group)
     dist.all_reduce(maxs, op=dist.ReduceOp.MAX, group=group)
     out = bbox.clone()

@@ -362,6 +362,10 @@ int i2pc_gemm_set_engine(int mode);
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
  *   "sel_windows" 1 = the window-only p2 / p98 selection of i2pc_unproject (one sweep), 0 = the
  *                 histogram levels (the band path's)
+ *   "sel_parts"   sub-batches of i2pc_unproject's selection chain, run on forked side streams so
+ *                 their small launches overlap (joined before the unprojection launch; graph
+ *                 capture follows the fork); 0 = automatic = 1 (2-4 measured slower, r03)
+ *   "sel_rows"    output rows per selection-sweep workgroup, 1..64 (default 16)
  *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _UNP_ROWS / _UNP_NT / _UNP_RPT /

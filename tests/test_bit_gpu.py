@@ -31,6 +31,26 @@ def test_group_norm_modes(B, H, W, C):
         assert err <= 2e-2 * exp.abs().max().item(), (shortcut is None, relu, err)
 
 
+@pytest.mark.parametrize("C", [64, 256, 1024])
+def test_group_norm_large_offset(C):
+    """Activations whose mean is ~200x their spread (BiT after a residual can drift there): the
+    statistics come from shifted sums merged by Chan's formula, so the variance does not cancel
+    away as E[x^2] - mean^2 in fp32 would.  The reference is fp64 group_norm of the
+    same bf16 values."""
+    from image_to_pointcloud_amd import ops
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(C)
+    B, H, W = 2, 48, 40
+    x = (torch.randn(B, H, W, C, generator=g) * 0.05 + 10.0).to(torch.bfloat16).to(dev)
+    gm, bt = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    ref = F.group_norm(_nchw(x).double(), 32, gm.double(), bt.double(), 1e-5)
+    got = _nchw(ops.group_norm(x, gm, bt, relu=False)).double()
+    err = (got - ref).abs().max().item()
+    # bf16 output of unit-variance values: ~4e-3 relative; a cancelled variance would be off by O(1)
+    assert err <= 3e-2, err
+    print("parity", {"case": f"groupnorm offset C={C}", "max_abs_err": err})
+
+
 @pytest.mark.parametrize("H,W", [(192, 192), (97, 64), (5, 6)])
 def test_maxpool_same_padding(H, W):
     from image_to_pointcloud_amd import ops

@@ -100,3 +100,21 @@ def test_bench_gpus_2_launches_two_ranks():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
                        text=True, timeout=120, cwd=ROOT, env=env)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.parametrize("extra", [[], ["--smooth", "--ksize", "9"], ["--levels"]])
+def test_c4_two_ranks_window_bands_bit_exact(extra):
+    """C4 with two real ranks (gloo, sharing cuda:0, host-staged exchange): each rank unprojects its
+    band of a 600 x 1000 panorama with the window selection across bands (or the histogram levels),
+    optionally smoothed; --check compares every band with the whole-image unprojection."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tools", "c4_panorama.py"),
+           "--height", "600", "--width", "1000", "--steps", "2", "--warmup", "1", "--check"] + extra
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_ranks"] == 2 and rec["bit_exact_vs_whole_image"] is True, rec
+    assert ("histogram levels" in rec["exchange"]) == ("--levels" in extra)

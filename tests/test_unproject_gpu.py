@@ -526,3 +526,48 @@ def test_window_selection_matches_histogram_levels_and_oracle(size):
             ep, _ = ref.depth_to_point_cloud(imgs[i], deps[i], density="high", invert=True, depth_scale=10.0,
                                              loop=False)
         assert _same_bits(outs[0][0][i], ep), (k, _first_diff(outs[0][0][i], ep))
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3, 4])
+def test_forked_selection_parts_bit_identical(parts):
+    """i2pc_unproject's selection chain as 1-4 sub-batches on forked side streams (knob sel_parts),
+    joined before one unprojection launch: bit-identical to one chain and to the oracle, and the
+    same under HIP graph capture (the fork is captured through its events)."""
+    from image_to_pointcloud_amd import ops
+    g = _geom()
+    dev = torch.device("cuda")
+    B, h, w, H, W = 17, 48, 64, 96, 128
+    deps = np.stack([_smooth_depth(h, w, 500 + i) for i in range(B)])
+    deps[5, 2, 3] = np.nan
+    imgs = np.stack([_rgb(H, W, 600 + i) for i in range(B)])
+    tdep, timg = torch.from_numpy(deps).to(dev), torch.from_numpy(imgs).to(dev)
+    ws = torch.empty(g.workspace_bytes(B, H, W), dtype=torch.uint8, device=dev)
+    try:
+        ops.set_tuning("sel_parts", 1)
+        one = g.unproject_batch(tdep, timg, density="high", workspace=ws)
+        torch.cuda.synchronize()
+        ref_xyz, ref_stats = one.xyz.cpu().numpy(), one.stats.cpu().numpy()
+        ops.set_tuning("sel_parts", parts)
+        got = g.unproject_batch(tdep, timg, density="high", workspace=ws)
+        torch.cuda.synchronize()
+        assert _same_bits(got.xyz.cpu().numpy(), ref_xyz)
+        assert _same_bits(got.stats.cpu().numpy(), ref_stats)
+        out = g.PointBatch(torch.zeros_like(got.xyz), torch.zeros_like(got.rgb), torch.zeros_like(got.bbox),
+                           torch.zeros_like(got.stats))
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g.unproject_batch(tdep, timg, density="high", workspace=ws, out=out)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g.unproject_batch(tdep, timg, density="high", workspace=ws, out=out)
+        out.xyz.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert _same_bits(out.xyz.cpu().numpy(), ref_xyz)
+    finally:
+        ops.set_tuning("sel_parts", 0)
+    for i in (0, 5, 16):
+        ep, _ = ref.depth_to_point_cloud(imgs[i], deps[i], density="high", loop=False)
+        assert _same_bits(ref_xyz[i], ep), i

@@ -95,7 +95,12 @@ def main():
                 if world > 1:
                     if k == rank:
                         deps[k].copy_(own)
-                    dist.broadcast(deps[k], k)
+                    if backend == "nccl":
+                        dist.broadcast(deps[k], k)
+                    else:                               # gloo: through host memory
+                        hk = deps[k].cpu()
+                        dist.broadcast(hk, k)
+                        deps[k].copy_(hk)
                 else:
                     deps[k].copy_(own)
         infer()
@@ -167,7 +172,7 @@ def main():
                   and torch.equal(whole.stats[0].view(torch.int64), res[3].view(torch.int64))   # NaN-aware
                   and torch.equal(whole.bbox[0], bbox))
         if world > 1:
-            t = torch.tensor([int(ok)], device=dev)
+            t = torch.tensor([int(ok)], device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             ok = bool(t.item())
     n = ((H + step - 1) // step) * ((W + step - 1) // step)

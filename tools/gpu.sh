@@ -162,5 +162,10 @@ case "$TASK" in
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/t -o t --output-format csv -- \
       python tools/c4_panorama.py --steps 10 "$@" > $D/run.txt 2>&1 || { tail -5 $D/run.txt; exit 1; }
     grep -o '"ms_per_image": [0-9.]*' $D/run.txt; stats $D/t unproj ;;
+  parts)      # whole unprojection call by selection sub-batches (I2PC_SEL_PARTS), then the kernel trace at the default
+    for P in 1 2 3 4; do
+      I2PC_SEL_PARTS=$P timeout -k 10 120 python tools/bench_unproject.py 32 high > gpurun_out/v.txt 2>&1 || exit 1
+      echo "parts $P: $(grep -h 'B=' gpurun_out/v.txt | sed 's/algorithmic.*//' | tr '\n' ' ')"
+    done ;;
   *) echo "unknown task '$TASK' (see the header of tools/gpu.sh)"; exit 2 ;;
 esac

@@ -15,7 +15,7 @@ import re
 import sys
 from collections import defaultdict
 
-EPI = {"0": "plain", "1": "res_f32", "2": "res_bf16", "3": "res2", "4": "convT", "5": "q8"}
+EPI = {"0": "plain", "1": "res_f32", "2": "res_bf16", "3": "res2", "4": "convT", "5": "q8", "6": "ln_fold"}
 
 
 def label(name: str) -> str:
