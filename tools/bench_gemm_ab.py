@@ -11,6 +11,10 @@ dev = torch.device("cuda")
 M = 32 * 577
 shapes = [("qkv", M, 3072, 1024, None), ("fc1", M, 4096, 1024, "gelu"), ("o", M, 1024, 1024, None),
           ("fc2", M, 1024, 4096, None), ("big", 8192, 8192, 4096, None)]
+if os.environ.get("AB_SHAPES") == "hybrid":        # DPT-Hybrid (C5, batch 64) bf16 linears
+    MH = 64 * 577
+    shapes = [("hqkv", MH, 2304, 768, None), ("hfc2", MH, 768, 3072, None), ("ho", MH, 768, 768, None),
+              ("hfc1", MH, 3072, 768, "gelu")]
 modes = [int(m) for m in os.environ.get("AB_MODES", "0,3").split(",")]
 g = torch.Generator(device="cpu").manual_seed(0)
 
