@@ -1791,7 +1791,13 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
     // the ping-pong engine (k_gemm_8p): dense A, plain / fp32-residual epilogues, K >= 128
     const bool can8 = !conv && !relu && (epi == pers::EPI_PLAIN || epi == pers::EPI_RESF32) && p.K >= 128;
     if (pforce == 4 && can8) return Plan{2, 256, 256, epi};
-    if (pforce == 2 || pforce == 4 || tiles >= 3 * ncu) {
+    // one to three rounds: persistent when its last round is at least 80 % full (DPT-Hybrid's
+    // bf16 FC2 / O, M = 36928, N = 768: 435 tiles = 0.85 of 2 rounds; 180 vs 203 us and 56 vs
+    // 68 us against the 128 x 128 tile kernel, tools/gpu.sh ab-hyb); DPT-Large's N = 1024 calls
+    // (292 tiles = 0.57 of 2 rounds) keep the one-round 320 x 256 tile kernel
+    const int64_t rounds = (tiles + ncu - 1) / ncu;
+    const bool full_rounds = tiles >= ncu && tiles * 10 >= rounds * ncu * 8;
+    if (pforce == 2 || pforce == 4 || tiles >= 3 * ncu || full_rounds) {
       // the single-stage engine by default: in the DPT-Large step the ping-pong engine measured
       // 1.6 % slower end to end (tools/ab_pipeline.py), though equal or faster in isolation
       pl = Plan{pforce == 3 && can8 ? 2 : 1, best, 256, epi};
