@@ -65,6 +65,10 @@ constexpr int kPick = 1024;
 constexpr int kPickWords = 3 + kPick;
 constexpr int kBandWords = kMaxTgt * kPickWords;
 constexpr int kBandEx = 8;               // row length of the window exchange's int64 [4][8] counters
+// k_sweep_w's per-workgroup "finite keys below window w" counts go to kBelowSlots slots per image
+// (workgroup i -> slot i % kBelowSlots) instead of one counter: a single large image (C4) had
+// its 2048 workgroups' atomics on the same three words
+constexpr int kBelowSlots = 64;
 constexpr int kMaxBandRanks = 256;
 
 // PH_INIT: level-0 sweep pending; PH_SEL: targets being narrowed; PH_SLOW: handed to
@@ -144,7 +148,7 @@ struct Geo {
 inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
-  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, mhist, gsend, grecv, field, tmp, total;
+  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, mhist, gsend, grecv, wpart, field, tmp, total;
   uint32_t cap;   // candidate keys per slot and image (compaction sweeps)
 };
 
@@ -192,6 +196,7 @@ static Layout layout(int B, int H, int W, int smooth, int nranks = 0) {
   L.mhist = off; off = align_up(off + sizeof(uint32_t) * kBins * (size_t)B, 256);
   L.gsend = off; off = align_up(off + (nranks > 0 ? sizeof(uint32_t) * kBandWords : 0), 256);
   L.grecv = off; off = align_up(off + sizeof(uint32_t) * kBandWords * (size_t)std::max(nranks, 0), 256);
+  L.wpart = off; off = align_up(off + sizeof(uint32_t) * kBelowSlots * 4 * (size_t)B, 256);
   L.field = off;
   if (smooth) {
     off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
@@ -385,7 +390,7 @@ __device__ __forceinline__ bool key_nonfinite(uint32_t k) { return k >= kKeyPosI
 __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, int m, int n, SelState* st,
                                                     uint32_t* hist, uint32_t* rpart, Tap* xt, Tap* yt, int dh, int dw,
                                                     int H, int W, double sx, double sy, double* trig, uint32_t* mhist,
-                                                    int nrc) {
+                                                    int nrc, uint32_t* wpart) {
   __shared__ uint32_t red[2][kBlock / 64];
   const int gtid = blockIdx.x * kBlock + threadIdx.x;
   const int nthr = gridDim.x * kBlock;
@@ -418,6 +423,8 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
     for (size_t i = gtid; i < (size_t)B * kSlots * kBins; i += nthr) hist[i] = 0;
   if (mhist)       // the sample histograms k_model_hist adds into
     for (size_t i = gtid; i < (size_t)B * kBins; i += nthr) mhist[i] = 0;
+  if (wpart)       // k_sweep_w's below-window slots
+    for (size_t i = gtid; i < (size_t)B * kBelowSlots * 4; i += nthr) wpart[i] = 0;
   if (trig) {       // equirectangular ray tables (the oracle evaluates the same expressions)
     const double pi = 3.141592653589793;
     for (int i = gtid; i < W + H; i += nthr) {
@@ -1033,7 +1040,7 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
 
 template <bool SAME>
 __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_t* cand, uint32_t cap, int B,
-                                                    Sweep sw) {
+                                                    Sweep sw, uint32_t* wpart) {
   // thread = 4 columns c0 + j * kBlock + tid of a kTileW-column tile, walking down the block's
   // R output rows.  The horizontal cv2 pass of a model row is a thread's own business (its 4
   // columns), so it stays in registers.
@@ -1080,7 +1087,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
     for (int q = 0; q < nwin; ++q) {
       uint32_t bw = 0;
       for (int w = 0; w < kBlock / 64; ++w) bw += red[w][4 + q];
-      if (bw) atomicAdd(&S->wbelow[q], bw);
+      if (bw) atomicAdd(&wpart[((size_t)b * kBelowSlots + (blockIdx.x % kBelowSlots)) * 4 + q], bw);
       const uint32_t nq = min(lcnt[q], (uint32_t)kStageW);
       gbase[q] = nq ? atomicAdd(&S->ccount[q], nq) : 0u;
       if (spk[q]) {
@@ -1725,7 +1732,19 @@ __global__ __launch_bounds__(kBlock) void k_resolve(SelState* st, uint32_t* hist
 // Anything else (a rank outside every window, a multi-key spike, an overflowed candidate list)
 // sets the image's err flag: k_sel_slow then selects it from scratch.  Window 0's workgroup
 // also stores the target bookkeeping k_sel_slow's finish needs.
-__global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32_t* cand, uint32_t cap, int B) {
+// wave 0: the image's kBelowSlots below-window partial counts of k_sweep_w summed into dst[3]
+__device__ __forceinline__ void sum_below(const uint32_t* wpart, int b, uint32_t* dst) {
+  if (threadIdx.x < 64) {
+    const uint4 v = threadIdx.x < kBelowSlots
+                        ? *reinterpret_cast<const uint4*>(wpart + ((size_t)b * kBelowSlots + threadIdx.x) * 4)
+                        : make_uint4(0, 0, 0, 0);
+    const uint32_t a = wave_sum_u32(v.x), c = wave_sum_u32(v.y), d = wave_sum_u32(v.z);
+    if (threadIdx.x == 0) { dst[0] = a; dst[1] = c; dst[2] = d; }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32_t* cand, uint32_t cap, int B,
+                                                      const uint32_t* wpart) {
   __shared__ uint32_t lh[kBins];
   __shared__ uint32_t ck[kLdsCand];
   __shared__ uint32_t wsum[kBlock / 64];
@@ -1737,6 +1756,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32
   if (b >= B) return;
   auto body = [&]() {
   if (threadIdx.x == 0) s = st[b];
+  __syncthreads();
+  sum_below(wpart, b, s.wbelow);
   __syncthreads();
   if (s.phase != PH_INIT) return;
   if (w > 0 && w >= (int)s.nwin) return;
@@ -2854,15 +2875,20 @@ __device__ __forceinline__ void window_keys(const SelState& s, int w, uint32_t& 
 constexpr int kBandSplit = 32;   // workgroups per window of the band histogram / compaction passes
 
 __global__ __launch_bounds__(kBlock) void k_bandw_hist(const SelState* st, const uint32_t* cand, uint32_t cap,
-                                                       uint32_t* hist, int64_t* ex) {
+                                                       uint32_t* hist, int64_t* ex, const uint32_t* wpart) {
   __shared__ uint32_t lh[kBins];
+  __shared__ uint32_t below[3];
   const int w = blockIdx.x % 3, j = blockIdx.x / 3;
   const SelState& s = st[0];
+  if (blockIdx.x == 0) {
+    sum_below(wpart, 0, below);
+    __syncthreads();
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     int64_t* e = ex;
     e[0] = s.nonfinite_count; e[1] = s.nan_count; e[2] = s.ninf_neg; e[3] = s.ninf_pos;
     for (int q = 0; q < 3; ++q) {
-      e[4 + q] = s.wbelow[q];
+      e[4 + q] = below[q];
       e[8 + q] = s.wcntF[q];
       e[11 + q] = s.wcntL[q];
       e[16 + q] = s.wminF[q];
@@ -3209,7 +3235,7 @@ static thread_local int g_sel_rows = [] {
 }();
 
 static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, const uint32_t* rpart,
-                         uint32_t* mhist, uint32_t cap, int B, const Sweep& sw, hipStream_t s,
+                         uint32_t* mhist, uint32_t* wpart, uint32_t cap, int B, const Sweep& sw, hipStream_t s,
                          const Exchange* x = nullptr, int nrc = 0) {
   if (nrc <= 0) nrc = range_chunks(B);
   // full-resolution sample of ~64 K points per image for the level-0 estimate
@@ -3231,13 +3257,13 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
     sww.ntiles = (g.W + kTileW - 1) / kTileW;
     const dim3 grid(B * sww.nrb * sww.ntiles), block(kBlock);
     if (g.same)
-      hipLaunchKernelGGL((k_sweep_w<true>), grid, block, 0, s, g, st, cand, cap, B, sww);
+      hipLaunchKernelGGL((k_sweep_w<true>), grid, block, 0, s, g, st, cand, cap, B, sww, wpart);
     else
-      hipLaunchKernelGGL((k_sweep_w<false>), grid, block, 0, s, g, st, cand, cap, B, sww);
+      hipLaunchKernelGGL((k_sweep_w<false>), grid, block, 0, s, g, st, cand, cap, B, sww, wpart);
     if (x) {
       // band run (B = 1): fine histograms + counters all-reduced, each target's bin keys
       // all-gathered, every rank selects the same keys (2 collectives, ~40 KB per rank)
-      hipLaunchKernelGGL(k_bandw_hist, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex);
+      hipLaunchKernelGGL(k_bandw_hist, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex, wpart);
       if (x->fn(x->user, hist, 3 * kBins, x->ex, kBandEx, s) != 0)
         return set_error(I2PC_ELAUNCH, "exchange callback failed (window histograms)");
       hipLaunchKernelGGL(k_bandw_pick, dim3(3), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex, x->send);
@@ -3248,7 +3274,7 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
       hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
       return check_launch("select");
     }
-    hipLaunchKernelGGL(k_resolve_w, dim3(B * 3), dim3(kBlock), 0, s, st, cand, cap, B);
+    hipLaunchKernelGGL(k_resolve_w, dim3(B * 3), dim3(kBlock), 0, s, st, cand, cap, B, wpart);
     hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
     return check_launch("select");
   }
@@ -3371,7 +3397,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   hipLaunchKernelGGL(k_prepare, dim3(batch * range_chunks(batch)), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n,
                      st, (xch || !g_sel_windows) ? hist : nullptr, rpart, xt, yt, dep_h, dep_w, img_h, img_w,
                      cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig, reinterpret_cast<uint32_t*>(ws + L.mhist),
-                     range_chunks(batch));
+                     range_chunks(batch), reinterpret_cast<uint32_t*>(ws + L.wpart));
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
@@ -3385,6 +3411,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   xb.recv = reinterpret_cast<uint32_t*>(ws + L.grecv);
   uint32_t* cand = reinterpret_cast<uint32_t*>(ws + L.cand);
   uint32_t* mhist = reinterpret_cast<uint32_t*>(ws + L.mhist);
+  uint32_t* wpart = reinterpret_cast<uint32_t*>(ws + L.wpart);
   const int nrc = range_chunks(batch);
   int rc;
   const int parts = xch ? 1 : select_parts(batch);
@@ -3401,7 +3428,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
       Geo gq = g;
       gq.depth = g.depth + (size_t)b0 * dep_h * dep_w;
       rc = launch_select(gq, st + b0, hist + (size_t)b0 * kSlots * kBins, cand + (size_t)b0 * kSlots * L.cap,
-                         rpart + (size_t)b0 * nrc * 2, mhist + (size_t)b0 * kBins, L.cap, b1 - b0, ssel, sq, nullptr, nrc);
+                         rpart + (size_t)b0 * nrc * 2, mhist + (size_t)b0 * kBins, wpart + (size_t)b0 * kBelowSlots * 4,
+                         L.cap, b1 - b0, ssel, sq, nullptr, nrc);
       if (rc) return rc;
       if (q > 0) {
         if (hipEventRecord(ax.join[q - 1], sq) != hipSuccess || hipStreamWaitEvent(s, ax.join[q - 1], 0) != hipSuccess)
@@ -3409,7 +3437,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
       }
     }
   } else {
-    rc = launch_select(g, st, hist, cand, rpart, mhist, L.cap, batch, ssel, s, xch ? &xb : nullptr, nrc);
+    rc = launch_select(g, st, hist, cand, rpart, mhist, wpart, L.cap, batch, ssel, s, xch ? &xb : nullptr, nrc);
     if (rc) return rc;
   }
 
@@ -3593,11 +3621,12 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
   hipLaunchKernelGGL(k_prepare, dim3(batch * range_chunks(batch)), dim3(kBlock), 0, s, depth, batch, n, n, st,
                      g_sel_windows ? nullptr : hist, rpart, xt, yt, h, w, h, w, 1.0, 1.0, nullptr,
-                     reinterpret_cast<uint32_t*>(ws + L.mhist), range_chunks(batch));
+                     reinterpret_cast<uint32_t*>(ws + L.mhist), range_chunks(batch), reinterpret_cast<uint32_t*>(ws + L.wpart));
   Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
   const Sweep ssel = plan_select(h, w, h, w, true, 0, h);
   int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart,
-                         reinterpret_cast<uint32_t*>(ws + L.mhist), L.cap, batch, ssel, s);
+                         reinterpret_cast<uint32_t*>(ws + L.mhist), reinterpret_cast<uint32_t*>(ws + L.wpart), L.cap,
+                         batch, ssel, s);
   if (rc) return rc;
   const int64_t total = (int64_t)batch * n;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
