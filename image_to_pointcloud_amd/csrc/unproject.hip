@@ -57,6 +57,7 @@ constexpr int kTileW = 1024;     // selection sweep column tile (4 columns per t
 constexpr int kSlotWords = kBins / 2;   // sweep LDS per slot: 2048 packed 16-bit counts or 1024 staged keys
 constexpr int kHrowBudget = 40 * 1024;   // LDS bytes of staged + horizontally interpolated model rows
 constexpr int kStageW = 1024;            // k_sweep_w: window keys a workgroup stages in LDS per window
+constexpr int kWaveBuf = kStageW / 4;     // ... per wave (4 waves)
 constexpr int kMaxSelRows = 64;          // k_sweep_w: output rows per workgroup at most
 // window-selection band runs (C4): after the window sweep each band bins its window keys into
 // kBins fine bins per window (all-reduced), then hands over only the keys of each target's fine
@@ -861,7 +862,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
 template <bool SAME, int NW>
 __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t* cand, uint32_t cap, int b,
                                              int v0, int v1, int cw, int c0, const Tap* tys,
-                                             uint32_t (*sh)[kStageW], uint32_t (*red)[24], uint32_t* lcnt,
+                                             uint32_t (*sh)[kStageW], uint32_t (*red)[28],
                                              const float* vlo, const float* vhi, const float* vF,
                                              const float* vL, const uint32_t* spk) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -916,8 +917,13 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
   uint32_t nf = 0, nnan = 0, nneg = 0, npos = 0;
   uint32_t below[NW], cF[NW], cL[NW];
   uint32_t mnF[NW], mxF[NW], mnL[NW], mxL[NW];
+  uint32_t wc[NW];                 // keys in this wave's LDS buffer of window w (wave-uniform)
+  uint32_t* wbuf = &sh[0][0] + wid * kWaveBuf;      // + w * kStageW
+  uint32_t* cw_dst[NW];
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
+    wc[w] = 0u;
+    cw_dst[w] = cand + ((size_t)b * kSlots + w) * cap;
     below[w] = cF[w] = cL[w] = 0u;
     mnF[w] = mnL[w] = 0xffffffffu;
     mxF[w] = mxL[w] = 0u;
@@ -991,27 +997,31 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
           m &= ~(fm | lm);
           if (!m) continue;
         }
-        const int leader = __ffsll((unsigned long long)m) - 1;
+        // the wave's own LDS buffer (kWaveBuf keys per window); a full buffer leaves as one
+        // reservation of kWaveBuf candidate slots and four contiguous 256-B stores, so a
+        // spatially dense window (a smooth map puts a quantile's pixels in a few blocks; one
+        // large image has them all) costs one global atomic per kWaveBuf keys
         const uint32_t cnt = (uint32_t)__popcll(m);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&lcnt[w], cnt);
-        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-        // ranks below `room` fill the LDS stage; the rest of the wave's keys (a spatially dense
-        // window: a smooth map puts a quantile's pixels in a few blocks) go straight to the
-        // candidate list with ONE global reservation per wave
-        const uint32_t room = base < (uint32_t)kStageW ? (uint32_t)kStageW - base : 0u;
-        const uint32_t over = cnt > room ? cnt - room : 0u;
-        uint32_t gb = 0;
-        if (over && lane == leader) gb = atomicAdd(&S->ccount[w], over);
-        gb = (uint32_t)__builtin_amdgcn_readlane((int)gb, leader);
-        if ((m >> lane) & 1ull) {
-          const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          if (r < room) {
-            sh[w][base + r] = key;
-          } else {
-            const uint32_t gpos = gb + (r - room);
-            if (gpos < cap) cand[((size_t)b * kSlots + w) * cap + gpos] = key;
-          }
+        const bool mine = (m >> lane) & 1ull;
+        const uint32_t pos = wc[w] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        uint32_t* buf = wbuf + w * kStageW;
+        if (mine && pos < (uint32_t)kWaveBuf) buf[pos] = key;
+        if (wc[w] + cnt >= (uint32_t)kWaveBuf) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's buffer writes, then its reads
+          uint32_t gb = 0;
+          if (lane == 0) gb = atomicAdd(&S->ccount[w], (uint32_t)kWaveBuf);
+          gb = (uint32_t)__builtin_amdgcn_readfirstlane((int)gb);
+          uint32_t kk[kWaveBuf / 64];
+#pragma unroll
+          for (int i = 0; i < kWaveBuf / 64; ++i) kk[i] = buf[i * 64 + lane];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < kWaveBuf / 64; ++i)
+            if (gb + i * 64 + lane < cap) cw_dst[w][gb + i * 64 + lane] = kk[i];
+          if (mine && pos >= (uint32_t)kWaveBuf) buf[pos - kWaveBuf] = key;
+          wc[w] = wc[w] + cnt - (uint32_t)kWaveBuf;
+        } else {
+          wc[w] += cnt;
         }
       }
     }
@@ -1023,7 +1033,7 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
   if (lane == 0) {
     red[wid][0] = nf; red[wid][1] = nnan; red[wid][2] = nneg; red[wid][3] = npos;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) red[wid][4 + w] = below[w];
+    for (int w = 0; w < NW; ++w) { red[wid][4 + w] = below[w]; red[wid][24 + w] = wc[w]; }
   }
   if (any_spike) {
 #pragma unroll
@@ -1044,9 +1054,9 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
   // thread = 4 columns c0 + j * kBlock + tid of a kTileW-column tile, walking down the block's
   // R output rows.  The horizontal cv2 pass of a model row is a thread's own business (its 4
   // columns), so it stays in registers.
-  __shared__ uint32_t sh[3][kStageW];               // staged window keys
-  __shared__ uint32_t red[kBlock / 64][24];
-  __shared__ uint32_t lcnt[3], gbase[3];
+  __shared__ uint32_t sh[3][kStageW];               // per window: the waves' key buffers (kWaveBuf each)
+  __shared__ uint32_t red[kBlock / 64][28];
+  __shared__ uint32_t gbase[3];
   __shared__ Tap tys[kMaxSelRows];                  // the block's row taps (no global load in the row loop)
   int b, chunk;
   map_block(blockIdx.x, B, sw.nrb * sw.ntiles, b, chunk);
@@ -1065,13 +1075,12 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
   }
   const int v0 = sw.row0 + rb * sw.R;
   const int v1 = min(sw.row_end, v0 + sw.R);
-  if (threadIdx.x < 3) lcnt[threadIdx.x] = 0;
   if (!SAME && (int)threadIdx.x < v1 - v0) tys[threadIdx.x] = g.yt[v0 + threadIdx.x];
   __syncthreads();
   switch (nwin) {
-    case 1: sweep_w_rows<SAME, 1>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, lcnt, vlo, vhi, vF, vL, spk); break;
-    case 2: sweep_w_rows<SAME, 2>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, lcnt, vlo, vhi, vF, vL, spk); break;
-    default: sweep_w_rows<SAME, 3>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, lcnt, vlo, vhi, vF, vL, spk); break;
+    case 1: sweep_w_rows<SAME, 1>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, vlo, vhi, vF, vL, spk); break;
+    case 2: sweep_w_rows<SAME, 2>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, vlo, vhi, vF, vL, spk); break;
+    default: sweep_w_rows<SAME, 3>(g, S, cand, cap, b, v0, v1, cw, c0, tys, sh, red, vlo, vhi, vF, vL, spk); break;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1088,7 +1097,8 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
       uint32_t bw = 0;
       for (int w = 0; w < kBlock / 64; ++w) bw += red[w][4 + q];
       if (bw) atomicAdd(&wpart[((size_t)b * kBelowSlots + (blockIdx.x % kBelowSlots)) * 4 + q], bw);
-      const uint32_t nq = min(lcnt[q], (uint32_t)kStageW);
+      uint32_t nq = 0;                 // the waves' leftover keys: one reservation per window
+      for (int w = 0; w < kBlock / 64; ++w) nq += red[w][24 + q];
       gbase[q] = nq ? atomicAdd(&S->ccount[q], nq) : 0u;
       if (spk[q]) {
         uint32_t a = 0, cmn = 0xffffffffu, dmx = 0, e = 0, fmn = 0xffffffffu, hmx = 0;
@@ -1102,11 +1112,14 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
     }
   }
   __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int q = 0; q < nwin; ++q) {
-    const uint32_t nq = min(lcnt[q], (uint32_t)kStageW);
+    uint32_t off = gbase[q];
+    for (int w = 0; w < wid; ++w) off += red[w][24 + q];
+    const uint32_t nq = red[wid][24 + q];
     uint32_t* dst = cand + ((size_t)b * kSlots + q) * cap;
-    for (uint32_t i = threadIdx.x; i < nq; i += kBlock)
-      if (gbase[q] + i < cap) dst[gbase[q] + i] = sh[q][i];
+    for (uint32_t i = lane; i < nq; i += 64)
+      if (off + i < cap) dst[off + i] = sh[q][wid * kWaveBuf + i];
   }
 }
 

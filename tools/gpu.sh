@@ -170,5 +170,16 @@ case "$TASK" in
       I2PC_SEL_PARTS=$P timeout -k 10 120 python tools/bench_unproject.py 32 high > gpurun_out/v.txt 2>&1 || exit 1
       echo "parts $P: $(grep -h 'B=' gpurun_out/v.txt | sed 's/algorithmic.*//' | tr '\n' ' ')"
     done ;;
+  pmc-sweep)  # SQ counters of k_sweep_w: the C2 batch call and the one-rank C4 band call
+    D=gpurun_out/pmc_sweep; rm -rf $D; mkdir -p $D
+    P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM"
+    P2="SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA"
+    i=0
+    for P in "$P1" "$P2"; do
+      i=$((i + 1))
+      timeout -k 10 120 rocprofv3 --pmc $P --kernel-trace -d $D/u$i -o u --output-format csv -- python tools/bench_unproject.py 32 > $D/u$i.txt 2>&1 || exit 1
+      timeout -k 10 120 rocprofv3 --pmc $P --kernel-trace -d $D/c$i -o c --output-format csv -- python tools/c4_panorama.py --steps 2 --warmup 1 > $D/c$i.txt 2>&1 || exit 1
+    done
+    for i in 1 2; do echo "== C2 pass $i"; python tools/pmc_summary.py $D/u$i k_sweep_w; echo "== C4 pass $i"; python tools/pmc_summary.py $D/c$i k_sweep_w; done ;;
   *) echo "unknown task '$TASK' (see the header of tools/gpu.sh)"; exit 2 ;;
 esac
