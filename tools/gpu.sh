@@ -116,6 +116,8 @@ case "$TASK" in
   ab-hyb)     # engine modes 0 (automatic) / 2 (persistent wherever it applies) on the DPT-Hybrid bf16 linears
     AB_SHAPES=hybrid AB_MODES=0,2 timeout -k 10 300 python -u tools/bench_gemm_ab.py > gpurun_out/ab.log 2>&1; rc=$?
     cat gpurun_out/ab.log; exit $rc ;;
+  epi)        # epilogue cost of the tile GEMM on the O-projection / FC2 shapes
+    timeout -k 10 300 python -u tools/epi_cost.py > gpurun_out/epi.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/epi.log; exit $rc ;;
   ab-gemm)
     timeout -k 10 300 python -u -m pytest tests/test_gemm_engines_gpu.py -x -q --timeout 120 --timeout-method thread \
       > gpurun_out/eng.log 2>&1 || { tail -15 gpurun_out/eng.log; exit 1; }
