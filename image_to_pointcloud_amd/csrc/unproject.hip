@@ -46,7 +46,10 @@ constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefe
 constexpr int kSlowBlock = 1024;
 constexpr int kRangeChunks = 32;         // k_prepare workgroups per image, at least (range_chunks)
 constexpr int kSampleChunks = 8;          // k_model_hist workgroups (partial sample histograms) per image, at least
-constexpr int kMaxSampleChunks = 128;     // ... at most (large images: up to ~1 M samples, 8 K per workgroup)
+constexpr int kMaxSampleChunks = 256;     // ... at most (large images: up to ~1 M samples, 4 K per workgroup)
+constexpr int kSamplesPerChunk = 8192;    // ~8 per thread: one batch of loads in flight, then the LDS adds
+// (4096 when the batch has too few images to fill the chip: the C4 panorama 25 -> 19.5 us;
+// with 32 images the extra workgroups' histogram atomics cost more than they hide, 17 -> 27 us)
 constexpr int kHistBlock = 1024;          // k_model_hist: threads per (image, chunk) workgroup (~8 samples each)
 // Level 0 bins values (one bin ~ up to 2^31 keys near 0); levels 1-3 bin keys 2048 ways each:
 // 2^31 -> 2^20 -> 2^9 -> 1 key, so the last level always resolves.
@@ -168,13 +171,15 @@ static uint32_t cand_cap(int64_t n) {
 struct SamplePlan {
   int stride, ns, nch;
 };
-static SamplePlan sample_plan(int H, int W) {
+static SamplePlan sample_plan(int H, int W, int B) {
   const double n = (double)H * W;
   const double target = std::min(1048576.0, std::max(65536.0, n / 32.0));
   SamplePlan sp;
   sp.stride = std::max(1, (int)std::sqrt(n / target));
   sp.ns = ((H + sp.stride - 1) / sp.stride) * ((W + sp.stride - 1) / sp.stride);
-  sp.nch = std::min(kMaxSampleChunks, std::max(kSampleChunks, (sp.ns + 8191) / 8192));
+  const int spc = (int64_t)B * ((sp.ns + kSamplesPerChunk - 1) / kSamplesPerChunk) >= 256 ? kSamplesPerChunk
+                                                                                        : kSamplesPerChunk / 2;
+  sp.nch = std::min(kMaxSampleChunks, std::max(kSampleChunks, (sp.ns + spc - 1) / spc));
   return sp;
 }
 
@@ -2872,7 +2877,7 @@ __global__ void k_band_import(SelState* st, int B, const int64_t* ex) {
 // counts.  1) k_bandw_hist: per window a kBins-bin histogram of the local keys over the
 // window's key range (the same range on every rank: the windows come from the whole image's
 // sample) and the counters as int64 [4][kBandEx] (rows 0-1 SUM, row 2 MIN, row 3 MAX) -> one
-// all-reduce.  2) k_bandw_pick: from the SUMMED counts every rank derives the same targets and,
+// all-reduce.  2) k_bandw_pickc: from the SUMMED counts every rank derives the same targets and,
 // for a target in a window's compacted part, its fine bin and its rank inside the bin; the local
 // keys of that bin (count, min, max, up to kPick keys) go to the target's slot -> one all-gather.
 // 3) k_bandw_final: each target's bin keys of every band merged, the exact key selected.
@@ -2888,7 +2893,8 @@ __device__ __forceinline__ void window_keys(const SelState& s, int w, uint32_t& 
 constexpr int kBandSplit = 32;   // workgroups per window of the band histogram / compaction passes
 
 __global__ __launch_bounds__(kBlock) void k_bandw_hist(const SelState* st, const uint32_t* cand, uint32_t cap,
-                                                       uint32_t* hist, int64_t* ex, const uint32_t* wpart) {
+                                                       uint32_t* hist, int64_t* ex, const uint32_t* wpart,
+                                                       uint32_t* send) {
   __shared__ uint32_t lh[kBins];
   __shared__ uint32_t below[3];
   const int w = blockIdx.x % 3, j = blockIdx.x / 3;
@@ -2909,9 +2915,18 @@ __global__ __launch_bounds__(kBlock) void k_bandw_hist(const SelState* st, const
       e[24 + q] = s.wmaxF[q];
       e[27 + q] = s.wmaxL[q];
     }
-    e[7] = e[14] = e[15] = 0;
+    // the bands' compacted counts (SUM) and whether any band's list overflowed (MAX): every rank
+    // must take the same decision
+    e[7] = s.ccount[0]; e[14] = s.ccount[1]; e[15] = s.ccount[2];
     e[22] = e[23] = 0xffffffffll;
-    e[30] = e[31] = 0;
+    e[30] = (s.ccount[0] > cap || s.ccount[1] > cap || s.ccount[2] > cap) ? 1 : 0;
+    e[31] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < kMaxTgt) {   // target slot headers for k_bandw_pickc's atomics
+    uint32_t* h = send + (size_t)threadIdx.x * kPickWords;
+    h[0] = 0u;
+    h[1] = 0xffffffffu;
+    h[2] = 0u;
   }
   if (w >= (int)s.nwin) return;
   const uint32_t c = min(s.ccount[w], cap);
@@ -2929,17 +2944,22 @@ __global__ __launch_bounds__(kBlock) void k_bandw_hist(const SelState* st, const
     if (lh[i]) atomicAdd(&hist[(size_t)w * kBins + i], lh[i]);
 }
 
-__global__ __launch_bounds__(kBlock) void k_bandw_pick(SelState* st, const uint32_t* cand, uint32_t cap,
-                                                       const uint32_t* hist, const int64_t* ex, uint32_t* send) {
+// k_bandw_pickc: kBandSplit workgroups per window w.  Each places the targets from the summed
+// counts (the same on every workgroup and rank) and finds its window's target fine bins; the
+// first workgroup of the window records them in the state, and every workgroup appends the
+// keys of those bins from its slice of the band's window keys to the target slots.
+__global__ __launch_bounds__(kBlock) void k_bandw_pickc(SelState* st, const uint32_t* cand, uint32_t cap,
+                                                        const uint32_t* hist, const int64_t* ex, uint32_t* send) {
   __shared__ SelState s;
   __shared__ uint32_t qr[kMaxTgt], rbin[kMaxTgt], rrem[kMaxTgt], wsum[kBlock / 64];
   __shared__ uint32_t sl[kMaxTgt], sz[kMaxTgt];
   __shared__ int tq[kMaxTgt], slot[kMaxTgt], nc, fail, nslot;
-  const int w = blockIdx.x;
+  __shared__ uint32_t ctot[3];
+  const int w = blockIdx.x % 3, jw = blockIdx.x / 3;
+  const bool rec = jw == 0;                // this workgroup records the window's targets
   SelState* S = st;
   if (threadIdx.x == 0) {
     s = st[0];
-    const uint32_t local = s.ccount[w];
     const int64_t* e = ex;
     s.nonfinite_count = (uint32_t)e[0]; s.nan_count = (uint32_t)e[1];
     s.ninf_neg = (uint32_t)e[2]; s.ninf_pos = (uint32_t)e[3];
@@ -2952,31 +2972,20 @@ __global__ __launch_bounds__(kBlock) void k_bandw_pick(SelState* st, const uint3
       s.wmaxF[q] = (uint32_t)e[24 + q];
       s.wmaxL[q] = (uint32_t)e[27 + q];
     }
-    fail = local > cap ? 1 : 0;          // this band's list overflowed: its histogram is short
+    ctot[0] = (uint32_t)e[7]; ctot[1] = (uint32_t)e[14]; ctot[2] = (uint32_t)e[15];
+    fail = e[30] ? 1 : 0;                // some band's list overflowed: its histogram is short
     nc = 0;
     nslot = 0;
   }
   __syncthreads();
-  // summed compacted count of every window (each workgroup needs all of them to place targets)
-  __shared__ uint32_t ctot[3];
-  if (threadIdx.x < 64) {
-    for (int q = 0; q < 3; ++q) {
-      uint32_t a = 0;
-      if (q < (int)s.nwin)
-        for (int i = threadIdx.x; i < kBins; i += 64) a += hist[(size_t)q * kBins + i];
-      a = wave_sum_u32(a);
-      if (threadIdx.x == 0) ctot[q] = a;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && !fail) {
     bool done = false;
     if (s.nonfinite_count == 0) {
       pct_ranks(s.n, s.rank);
       s.ntgt = 4;
       for (int t = 0; t < 4; ++t) { s.tlo[t] = 0; s.thi[t] = 0xffffffffu; }
     } else if (s.nan_count == s.n) {     // all-NaN: nanmedian is NaN, every value stays NaN
-      if (w == 0) {
+      if (w == 0 && rec) {
         S->has_med = 1;
         S->mode = 2;
         S->p2 = S->p98 = (double)__uint_as_float(0x7fc00000u);
@@ -2987,7 +2996,7 @@ __global__ __launch_bounds__(kBlock) void k_bandw_pick(SelState* st, const uint3
       fill_targets(s);
     }
     if (!done) {
-      if (w == 0) {
+      if (w == 0 && rec) {
         S->ntgt = s.ntgt;
         S->fill = s.fill;
         S->med_ranks = s.med_ranks;
@@ -3012,19 +3021,24 @@ __global__ __launch_bounds__(kBlock) void k_bandw_pick(SelState* st, const uint3
         const uint32_t cF = (s.wspike[w] & 1u) ? s.wcntF[w] : 0u;
         const uint64_t rp = r - s.wbelow[w];
         if (rp < cF) {
-          if (s.wminF[w] == s.wmaxF[w]) { S->tlo[t] = S->thi[t] = s.wminF[w]; S->tslot[t] = kNoSlot; } else fail = 1;
+          if (s.wminF[w] != s.wmaxF[w]) fail = 1;
+          else if (rec) { S->tlo[t] = S->thi[t] = s.wminF[w]; S->tslot[t] = kNoSlot; }
         } else if (rp < (uint64_t)cF + ctot[w]) {
           qr[nc] = (uint32_t)(rp - cF);
           tq[nc++] = t;
         } else {
-          if (s.wminL[w] == s.wmaxL[w]) { S->tlo[t] = S->thi[t] = s.wminL[w]; S->tslot[t] = kNoSlot; } else fail = 1;
+          if (s.wminL[w] != s.wmaxL[w]) fail = 1;
+          else if (rec) { S->tlo[t] = S->thi[t] = s.wminL[w]; S->tslot[t] = kNoSlot; }
         }
       }
     }
   }
   __syncthreads();
-  if (fail) atomicOr(&S->err, 1u);
-  if (nc == 0 || fail) return;
+  if (fail) {
+    if (rec && threadIdx.x == 0) atomicOr(&S->err, 1u);
+    return;
+  }
+  if (nc == 0) return;
   find_bins(hist + (size_t)w * kBins, kBins, qr, nc, wsum, rbin, rrem);
   if (threadIdx.x == 0) {
     uint32_t k0, k1;
@@ -3041,42 +3055,21 @@ __global__ __launch_bounds__(kBlock) void k_bandw_pick(SelState* st, const uint3
         sl[own] = a; sz[own] = z;
         slot[own] = tq[j];
       }
-      const int t = tq[j];
-      S->tlo[t] = a;
-      S->thi[t] = z;
-      S->rank[t] = rrem[j];              // rank inside the fine bin
-      S->tslot[t] = (uint32_t)slot[own];
-      S->twin[t] = (uint32_t)w;
+      if (rec) {
+        const int t = tq[j];
+        S->tlo[t] = a;
+        S->thi[t] = z;
+        S->rank[t] = rrem[j];            // rank inside the fine bin
+        S->tslot[t] = (uint32_t)slot[own];
+        S->twin[t] = (uint32_t)w;
+      }
     }
-    for (int q = 0; q < nslot; ++q) {    // the slot's header: count, min key, max key (k_bandw_compact)
-      uint32_t* h = send + (size_t)slot[q] * kPickWords;
-      h[0] = 0u;
-      h[1] = 0xffffffffu;
-      h[2] = 0u;
-    }
-  }
-}
-
-// The band's keys of every target slot (count, min, max, up to kPick keys): kBandSplit
-// workgroups per window, each over a slice of the band's window keys.
-__global__ __launch_bounds__(kBlock) void k_bandw_compact(const SelState* st, const uint32_t* cand, uint32_t cap,
-                                                          uint32_t* send) {
-  __shared__ uint32_t sl[kMaxTgt], sz[kMaxTgt];
-  __shared__ int slot[kMaxTgt], nslot;
-  const int w = blockIdx.x % 3, j = blockIdx.x / 3;
-  const SelState* S = st;
-  if (S->err || S->phase != PH_INIT) return;
-  if (threadIdx.x == 0) {
-    int n = 0;
-    for (int t = 0; t < (int)S->ntgt; ++t)
-      if (S->tslot[t] == (uint32_t)t && S->twin[t] == (uint32_t)w) { sl[n] = S->tlo[t]; sz[n] = S->thi[t]; slot[n++] = t; }
-    nslot = n;
   }
   __syncthreads();
+  // this workgroup's slice of the band's window keys -> the slots (headers zeroed by k_bandw_hist)
   const int ns = nslot;
-  if (ns == 0) return;
-  const uint32_t c = min(S->ccount[w], cap);
-  const uint32_t i0 = (uint32_t)((uint64_t)c * j / kBandSplit), i1 = (uint32_t)((uint64_t)c * (j + 1) / kBandSplit);
+  const uint32_t c = min(s.ccount[w], cap);
+  const uint32_t i0 = (uint32_t)((uint64_t)c * jw / kBandSplit), i1 = (uint32_t)((uint64_t)c * (jw + 1) / kBandSplit);
   const uint32_t* keys = cand + (size_t)w * cap;
   for (uint32_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
     const uint32_t k = keys[i];
@@ -3092,8 +3085,8 @@ __global__ __launch_bounds__(kBlock) void k_bandw_compact(const SelState* st, co
   }
 }
 
-// Every band's keys of each target slot merged (into `scratch`), then the exact key of each
-// target sharing the slot (rank inside the bin) selected: one workgroup.
+// Every band's keys of each target slot merged (in LDS, or `scratch` past kBins keys), then the
+// exact key of each target sharing the slot (rank inside the bin) selected: a workgroup per slot.
 __global__ __launch_bounds__(kBlock) void k_bandw_final(SelState* st, const uint32_t* recv, int nranks,
                                                         uint32_t* scratch, uint32_t scratch_cap) {
   __shared__ uint32_t lh[kBins];
@@ -3105,9 +3098,12 @@ __global__ __launch_bounds__(kBlock) void k_bandw_final(SelState* st, const uint
   SelState* S = st;
   if (S->phase != PH_INIT || S->err) return;
   const int ntgt = (int)S->ntgt;
-  uint32_t base = 0;                     // each slot's keys in their own scratch range
-  for (int t0 = 0; t0 < ntgt; ++t0) {
-    if (S->tslot[t0] != (uint32_t)t0) continue;      // not a slot owner (or resolved)
+  // one workgroup per target slot (slot t0 = the first target of its fine bin)
+  const int t0 = blockIdx.x;
+  if (t0 >= ntgt || S->tslot[t0] != (uint32_t)t0) return;      // not a slot owner (or resolved)
+  const uint32_t per = scratch_cap / kMaxTgt;                  // each slot's keys in their own scratch range
+  const uint32_t base = per * (uint32_t)t0;
+  {
     if (threadIdx.x == 0) {
       ng = 0;
       for (int t = t0; t < ntgt; ++t)
@@ -3130,12 +3126,12 @@ __global__ __launch_bounds__(kBlock) void k_bandw_final(SelState* st, const uint
         ng = 0;
         bad = 0;
       }
-      if (!bad && ng > 0 && base + acc > scratch_cap) bad = 1;
+      if (!bad && ng > 0 && acc > (uint32_t)kBins && acc > per) bad = 1;
       if (bad) S->err = 1u;
     }
     __syncthreads();
     if (bad) return;
-    if (ng == 0) continue;
+    if (ng == 0) return;
     if (tot <= (uint32_t)kBins) {
       // the usual case (tens of keys per fine bin and band): the bin's keys in LDS, each key's
       // rank range counted against all of them
@@ -3156,8 +3152,7 @@ __global__ __launch_bounds__(kBlock) void k_bandw_final(SelState* st, const uint
         for (int q = 0; q < ng; ++q)
           if (less <= ranks[q] && ranks[q] < leq) S->tlo[who[q]] = S->thi[who[q]] = k;   // (equal keys: same value)
       }
-      __syncthreads();
-      continue;
+      return;
     }
     uint32_t* keys = scratch + base;
     for (int r = 0; r < nranks; ++r) {
@@ -3168,8 +3163,6 @@ __global__ __launch_bounds__(kBlock) void k_bandw_final(SelState* st, const uint
     __syncthreads();
     cand_select(keys, tot, gmn, gmx < gmn ? gmn : gmx, ranks, ng, out, lh, wsum, rbin, rrem, tl, tz, tr);
     if (threadIdx.x < ng) S->tlo[who[threadIdx.x]] = S->thi[who[threadIdx.x]] = out[threadIdx.x];
-    base += tot;
-    __syncthreads();
   }
 }
 
@@ -3252,7 +3245,7 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
                          const Exchange* x = nullptr, int nrc = 0) {
   if (nrc <= 0) nrc = range_chunks(B);
   // full-resolution sample of ~64 K points per image for the level-0 estimate
-  const SamplePlan sp = sample_plan(g.H, g.W);
+  const SamplePlan sp = sample_plan(g.H, g.W, B);
   // windows: the batch path, and band runs that can all-gather their candidate lists
   const bool win = x ? x->gather != nullptr : g_sel_windows != 0;
   hipLaunchKernelGGL(k_model_hist, dim3(B * sp.nch), dim3(kHistBlock), 0, s, g, B, st, mhist, rpart, sp.stride, sp.nch,
@@ -3276,14 +3269,14 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
     if (x) {
       // band run (B = 1): fine histograms + counters all-reduced, each target's bin keys
       // all-gathered, every rank selects the same keys (2 collectives, ~40 KB per rank)
-      hipLaunchKernelGGL(k_bandw_hist, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex, wpart);
+      hipLaunchKernelGGL(k_bandw_hist, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex, wpart,
+                         x->send);
       if (x->fn(x->user, hist, 3 * kBins, x->ex, kBandEx, s) != 0)
         return set_error(I2PC_ELAUNCH, "exchange callback failed (window histograms)");
-      hipLaunchKernelGGL(k_bandw_pick, dim3(3), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex, x->send);
-      hipLaunchKernelGGL(k_bandw_compact, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, x->send);
+      hipLaunchKernelGGL(k_bandw_pickc, dim3(3 * kBandSplit), dim3(kBlock), 0, s, st, cand, cap, hist, x->ex, x->send);
       if (x->gather(x->user, x->send, x->recv, kBandWords, s) != 0)
         return set_error(I2PC_ELAUNCH, "gather callback failed (target bins)");
-      hipLaunchKernelGGL(k_bandw_final, dim3(1), dim3(kBlock), 0, s, st, x->recv, x->nranks, cand, kSlots * cap);
+      hipLaunchKernelGGL(k_bandw_final, dim3(kMaxTgt), dim3(kBlock), 0, s, st, x->recv, x->nranks, cand, kSlots * cap);
       hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
       return check_launch("select");
     }
