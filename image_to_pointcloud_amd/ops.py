@@ -169,6 +169,45 @@ def gemm(desc: GemmDesc) -> None:
         _lib.call("i2pc_gemm_ws", ctypes.byref(desc), _p(ws), nb, _stream())
 
 
+def _ceil(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+def _pad_cols(t, cols: int):
+    """A copy of the 2-D device tensor t [R, c] zero-padded to [R, cols] (same dtype)."""
+    torch = _torch()
+    o = torch.zeros((t.shape[0], cols), dtype=t.dtype, device=t.device)
+    o[:, :t.shape[1]] = t
+    return o
+
+
+def _linear_padded(x, w, bias, act, res, res2, out, out_f32, rows):
+    """linear() for widths the GEMM engines do not take (K % 64, N % 32): the operands are
+    zero-padded to K' = ceil64(K), N' = ceil32(N) (zero weights and bias add nothing), the HIP
+    GEMM runs on the padded shapes and the first N columns are copied to `out`.  For checkpoints
+    whose widths differ from the shipped models'; the shipped networks never take this path."""
+    torch = _torch()
+    M = rows if rows is not None else x.shape[0]
+    N, K = w.shape
+    Kp, Np = _ceil(K, 64), _ceil(N, 32)
+    xp = _pad_cols(x[:M].reshape(M, -1)[:, :K], Kp) if Kp != K else x
+    wp = torch.zeros((Np, Kp), dtype=w.dtype, device=w.device)
+    wp[:N, :K] = w
+    bp = None
+    if bias is not None:
+        bp = torch.zeros(Np, dtype=bias.dtype, device=bias.device)
+        bp[:N] = bias
+    rp = _pad_cols(res[:M], Np) if res is not None else None
+    r2p = _pad_cols(res2[:M], Np) if res2 is not None else None
+    dt = out.dtype if out is not None else (torch.float32 if out_f32 else torch.bfloat16)
+    op = torch.empty((M, Np), dtype=dt, device=x.device)
+    linear(xp, wp, bias=bp, act=act, res=rp, res2=r2p, out=op, rows=M)
+    if out is None:
+        return op[:, :N].contiguous()
+    out[:M, :N].copy_(op[:, :N])
+    return out
+
+
 def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=False,
            a_map=(0, 0, 0), out_map=(0, 0, 0), rows=None, row_bias=None, row_bias_group=1,
            table=None, table_rows=1, ldc=None, ln_rows=None, col_sum=None, ln_part=None, out_bf16=None,
@@ -186,6 +225,12 @@ def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=Fal
     _check(w, torch.bfloat16, "w")
     M = rows if rows is not None else x.shape[0]
     N, K = w.shape
+    if K % 64 or N % 32:
+        plain = (a_map == (0, 0, 0) and out_map == (0, 0, 0) and row_bias is None and table is None and ldc is None
+                 and ln_rows is None and ln_part is None)
+        if not plain:
+            raise _lib.I2PCError(f"linear: K={K} (% 64) / N={N} (% 32) are padded for plain calls only")
+        return _linear_padded(x, w, bias, act, res, res2, out, out_f32, rows)
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
     d = GemmDesc()
@@ -261,6 +306,27 @@ def conv2d(x, w, bias=None, k=3, stride=1, pad=1, relu_in=False, act=None, res=N
     OW = (W + 2 * pad - k) // stride + 1
     if out_hw is not None:
         OH, OW = out_hw
+    if C % 64 or Co % 32:
+        # widths the engines do not take: zero-pad the input channels to ceil64(C) (the weights'
+        # k*k*C axis with them) and the output channels to ceil32(Co), run the HIP conv, keep Co
+        Cp, Cop = _ceil(C, 64), _ceil(Co, 32)
+        xp = x
+        if Cp != C:
+            xp = torch.zeros((B, H, W, Cp), dtype=x.dtype, device=x.device)
+            xp[..., :C] = x
+        wp = torch.zeros((Cop, k * k, Cp), dtype=w.dtype, device=w.device)
+        wp[:Co, :, :C] = w.reshape(Co, k * k, C)
+        bp = None
+        if bias is not None:
+            bp = torch.zeros(Cop, dtype=bias.dtype, device=bias.device)
+            bp[:Co] = bias
+        pad4 = lambda t: None if t is None else torch.nn.functional.pad(t, (0, Cop - Co))   # noqa: E731 (a copy)
+        op = conv2d(xp, wp.reshape(Cop, k * k * Cp), bias=bp, k=k, stride=stride, pad=pad, relu_in=relu_in, act=act,
+                    res=pad4(res), res2=pad4(res2), out_hw=(OH, OW))
+        if out is None:
+            return op[..., :Co].contiguous()
+        out.copy_(op[..., :Co])
+        return out
     if out is None:
         out = torch.empty((B, OH, OW, Co), dtype=torch.bfloat16, device=x.device)
     d = GemmDesc()

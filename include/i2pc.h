@@ -219,7 +219,10 @@ int i2pc_sor(const float* xyz, const uint8_t* rgb, int64_t n, int nb_neighbors, 
  *    (row stride ldc), or, with convt_s > 0, the ConvTranspose(kernel = stride = s)
  *    pixel shuffle: m = (b, iy, ix) over convt_h x convt_w, n = (dy*s + dx)*convt_c + co
  *    -> NHWC [b][iy*s+dy][ix*s+dx][co].
- * Requires k % 64 == 0, n % 32 == 0, conv_c % 64 == 0. */
+ * Requires k % 64 == 0, n % 32 == 0, conv_c % 64 == 0.  Other widths: zero-pad K (A's columns
+ * and W's, or a conv's input channels) to a multiple of 64 and N (W's rows, bias, residuals) to a
+ * multiple of 32, call on the padded shapes and keep the first n columns -- what the Python layer
+ * (ops.linear / ops.conv2d) does for such checkpoints. */
 typedef struct i2pc_gemm_desc {
   const void* a; int64_t lda; int32_t m, n, k;
   int32_t a_group, a_group_stride, a_offset;
