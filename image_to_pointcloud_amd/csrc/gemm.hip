@@ -86,10 +86,11 @@ struct Args {
   uint32_t as_bytes, ws_bytes;
   int kspan;   // split-K (tile kernel): K-steps per blockIdx.y slice, 0 = the whole K
   // LayerNorm fold (i2pc.h): consumer row scales float2 [M] + column sums [N]; producer chunk
-  // partials float2 [M][N / 64] + the bf16 copy of the fp32 output
+  // partials float2 [M][N / lnc] (lnc = 64 or 32 columns per chunk) + the bf16 copy of the fp32 output
   const float* lnr; const float* csum;
   float* lnp; bf16_t* cbf; int64_t ldcb;
   const float* lnsh;
+  int lnc;
 };
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
@@ -266,10 +267,10 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       float* c = static_cast<float*>(p.C) + off;
       *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      if constexpr (LPR % 8 == 0) {
+      if constexpr (LPR % 4 == 0) {
         if (p.lnp) {
           // LayerNorm producer: the bf16 copy of out - shift[m], and (mean, M2) of each 64-column
-          // chunk (= 8 lanes) of it
+          // chunk (= 8 lanes) of it, or of each 32-column chunk (4 lanes; lnc = 32)
           const float shf = p.lnsh ? p.lnsh[m] : 0.f;
           float u[8];
 #pragma unroll
@@ -283,16 +284,19 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
           float sm = ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
           sm += __shfl_xor(sm, 1);
           sm += __shfl_xor(sm, 2);
-          sm += __shfl_xor(sm, 4);
-          const float mean = sm * (1.0f / 64.0f);
+          const bool c64 = LPR % 8 == 0 && p.lnc == 64;   // the host allows 64 only where LPR % 8 == 0
+          if (c64) sm += __shfl_xor(sm, 4);
+          const float mean = sm * (c64 ? 1.0f / 64.0f : 1.0f / 32.0f);
           float q = 0.f;
 #pragma unroll
           for (int t = 0; t < 8; ++t) q = __builtin_fmaf(u[t] - mean, u[t] - mean, q);
           q += __shfl_xor(q, 1);
           q += __shfl_xor(q, 2);
-          q += __shfl_xor(q, 4);
-          if ((c8 & 7) == 0)
-            *reinterpret_cast<float2*>(p.lnp + ((int64_t)m * (p.N / 64) + n / 64) * 2) = make_float2(mean, q);
+          if (c64) q += __shfl_xor(q, 4);
+          if ((c8 & (c64 ? 7 : 3)) == 0) {
+            const int cs = c64 ? 6 : 5;
+            *reinterpret_cast<float2*>(p.lnp + ((int64_t)m * (p.N >> cs) + (n >> cs)) * 2) = make_float2(mean, q);
+          }
         }
       }
     } else {
@@ -1830,7 +1834,7 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
     // LayerNorm-fold producer: the tile epilogue's row layout must give whole 64-column chunks
     // to 8-lane groups (wave tile a multiple of 64 columns)
     const int wn = pl.bn == 256 ? 4 : pl.bn == 32 || pl.bn == 192 ? (pl.bn == 192 ? 2 : 1) : 2;
-    if ((pl.bn / wn) % 64 != 0) pl = p.N % 128 == 0 ? Plan{0, 128, 128, 64} : Plan{-2, 0, 0, 0};
+    if ((pl.bn / wn) % p.lnc != 0) pl = p.N % 128 == 0 ? Plan{0, 128, 128, 64} : Plan{-2, 0, 0, 0};
   }
   return pl;
 }
@@ -2142,10 +2146,12 @@ static int make_args(const i2pc_gemm_desc* d, gemm::Args& p) {
   p.lnr = d->ln_rows; p.csum = d->col_sum;
   p.lnp = d->ln_part; p.cbf = static_cast<gemm::bf16_t*>(d->c_bf16); p.ldcb = d->ldc_bf16;
   p.lnsh = d->ln_part ? d->ln_shift : nullptr;
+  p.lnc = d->ln_chunk ? d->ln_chunk : 64;
   if (d->ln_rows) I2PC_REQUIRE(d->col_sum, "gemm: ln_rows needs col_sum");
   if (d->ln_part) {
-    I2PC_REQUIRE(d->c_bf16 && d->c_f32 && d->n % 64 == 0 && d->ldc_bf16 % 8 == 0 && d->ldc_bf16 >= d->n,
-                 "gemm: ln_part needs c_bf16 (ldc_bf16 %% 8, >= n), an fp32 output and n %% 64 == 0");
+    I2PC_REQUIRE(p.lnc == 32 || p.lnc == 64, "gemm: ln_chunk=%d must be 0, 32 or 64", d->ln_chunk);
+    I2PC_REQUIRE(d->c_bf16 && d->c_f32 && d->n % p.lnc == 0 && d->ldc_bf16 % 8 == 0 && d->ldc_bf16 >= d->n,
+                 "gemm: ln_part needs c_bf16 (ldc_bf16 %% 8, >= n), an fp32 output and n %% ln_chunk == 0");
     I2PC_REQUIRE(d->out_group == 0 && d->out_offset == 0 && d->convt_s == 0, "gemm: ln_part needs a linear output row map");
     I2PC_REQUIRE(!d->ln_rows, "gemm: ln_part and ln_rows in one call");
   }

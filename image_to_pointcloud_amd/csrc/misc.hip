@@ -231,12 +231,12 @@ __global__ __launch_bounds__(256) void k_head_out(const bf16_t* __restrict__ x, 
   }
 }
 
-// LayerNorm row statistics from the 64-column chunk partials an i2pc_gemm producer epilogue
-// wrote ((mean, M2) per chunk of out - shift): Chan's combination for equal chunk counts,
-// mean = avg(mean_c), M2 = sum M2_c + 64 sum (mean_c - mean)^2, var = M2 / (64 P) (biased, as
+// LayerNorm row statistics from the cw-column chunk partials (cw = 64 or 32) an i2pc_gemm producer
+// epilogue wrote ((mean, M2) per chunk of out - shift): Chan's combination for equal chunk counts,
+// mean = avg(mean_c), M2 = sum M2_c + cw sum (mean_c - mean)^2, var = M2 / (cw P) (biased, as
 // nn.LayerNorm), out = (rstd, -rstd * mean), shift_out = shift_in + mean.  16 lanes per row (coalesced 8-byte
 // partials, partial c on lane c % 16), 16 rows per 256-thread block.
-__global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ part, int rows, int P, float eps,
+__global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ part, int rows, int P, float cw, float eps,
                                                      float2* __restrict__ out, const float* shift_in,
                                                      float* shift_out) {
   const int r = blockIdx.x * 16 + (threadIdx.x >> 4);
@@ -259,14 +259,14 @@ __global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ 
   for (int j = 0; j < 4; ++j)
     if (l + 16 * j < P) {
       const float d = v[j].x - mean;
-      m2 += v[j].y + 64.0f * d * d;
+      m2 += v[j].y + cw * d * d;
     }
   m2 += __shfl_xor(m2, 1);
   m2 += __shfl_xor(m2, 2);
   m2 += __shfl_xor(m2, 4);
   m2 += __shfl_xor(m2, 8);
   if (ok && l == 0) {
-    const float rstd = 1.0f / sqrtf(m2 / (float)(64 * P) + eps);
+    const float rstd = 1.0f / sqrtf(m2 / (cw * (float)P) + eps);
     out[r] = make_float2(rstd, -rstd * mean);
     if (shift_out) shift_out[r] = (shift_in ? shift_in[r] : 0.f) + mean;
   }
@@ -289,15 +289,21 @@ bool i2pc_misc_tune(const char* name, int value) {
   return false;
 }
 
-extern "C" int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out,
-                                const float* shift_in, float* shift_out, void* stream) {
+extern "C" int i2pc_ln_rowstats_w(const float* part, int rows, int parts, int chunk_cols, float eps, float* rows_out,
+                                  const float* shift_in, float* shift_out, void* stream) {
   clear_error();
   I2PC_REQUIRE(part && rows_out, "NULL pointer");
   I2PC_REQUIRE(rows > 0 && parts >= 1 && parts <= 64, "ln_rowstats: parts=%d must be 1..64", parts);
+  I2PC_REQUIRE(chunk_cols == 32 || chunk_cols == 64, "ln_rowstats: chunk_cols=%d must be 32 or 64", chunk_cols);
   hipLaunchKernelGGL(k_ln_rowstats, dim3((rows + 15) / 16), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<const float2*>(part), rows, parts, eps, reinterpret_cast<float2*>(rows_out), shift_in,
-                     shift_out);
+                     reinterpret_cast<const float2*>(part), rows, parts, (float)chunk_cols, eps,
+                     reinterpret_cast<float2*>(rows_out), shift_in, shift_out);
   return check_launch("ln_rowstats");
+}
+
+extern "C" int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out,
+                                const float* shift_in, float* shift_out, void* stream) {
+  return i2pc_ln_rowstats_w(part, rows, parts, 64, eps, rows_out, shift_in, shift_out, stream);
 }
 
 static int layernorm_impl(const float* x, int64_t ldx, const float* gamma, const float* beta, float eps, int rows,

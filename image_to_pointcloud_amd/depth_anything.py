@@ -15,6 +15,9 @@ kernels of libi2pc.so: bf16 operands, fp32 accumulation, fp32 residual stream.
   encoder x L  LN -> QKV -> attention -> O -> +res -> LN -> FC1+GELU -> FC2 -> +res.
                LayerScale is folded into the O / FC2 weight rows and biases
                (lambda * (W x + b) = (lambda W) x + lambda b)          modeling_dinov2.py Dinov2Layer
+               With dpt.LN_FOLD the two LNs are folded through QKV / FC1: O and FC2
+               write the residual's bf16 copy and 32-column row partials in their
+               epilogue, QKV / FC1 apply (rstd, -rstd*mean) in theirs (_encoder_folded)
   features     backbone LayerNorm of the hidden states after layers out_indices
   reassemble   drop CLS (GEMM row remap) -> 1x1 projection -> ConvT(4)/ConvT(2)/
                id/3x3 s2 conv                                       modeling_depth_anything.py:31-93
@@ -37,6 +40,9 @@ from dataclasses import dataclass
 from . import dpt, ops
 from .dpt import _pack_conv
 from .preprocess import patch_pitch
+
+# LayerNorm-fold partial width (columns per (mean, M2) chunk; dpt.LN_FOLD switches the fold)
+LN_CHUNK = 32
 
 
 @dataclass(frozen=True)
@@ -233,7 +239,7 @@ class DepthAnythingModel:
             qb = [sd[p + f"attention.attention.{n}.bias"] for n in ("query", "key", "value")]
             l1 = sd[p + "layer_scale1.lambda1"]
             l2 = sd[p + "layer_scale2.lambda1"]
-            self.layers.append(dict(
+            L = dict(
                 ln1_g=f32(sd[p + "norm1.weight"]), ln1_b=f32(sd[p + "norm1.bias"]),
                 w_qkv=bf(torch.cat(q, 0)), b_qkv=f32(torch.cat(qb, 0)),
                 w_o=bf(sd[p + "attention.output.dense.weight"] * l1[:, None]),
@@ -241,7 +247,15 @@ class DepthAnythingModel:
                 ln2_g=f32(sd[p + "norm2.weight"]), ln2_b=f32(sd[p + "norm2.bias"]),
                 w_1=bf(sd[p + "mlp.fc1.weight"]), b_1=f32(sd[p + "mlp.fc1.bias"]),
                 w_2=bf(sd[p + "mlp.fc2.weight"] * l2[:, None]), b_2=f32(sd[p + "mlp.fc2.bias"] * l2),
-            ))
+            )
+            # the LN-folded forms of QKV (norm1) and FC1 (norm2), as in dpt.py
+            wf, cs, bfold = ops.ln_fold_weights(torch.cat(q, 0), torch.cat(qb, 0), sd[p + "norm1.weight"],
+                                                sd[p + "norm1.bias"])
+            L.update(w_qkv_f=wf.to(dev), s_qkv=cs.to(dev), b_qkv_f=bfold.to(dev))
+            wf, cs, bfold = ops.ln_fold_weights(sd[p + "mlp.fc1.weight"], sd[p + "mlp.fc1.bias"], sd[p + "norm2.weight"],
+                                                sd[p + "norm2.bias"])
+            L.update(w_1_f=wf.to(dev), s_1=cs.to(dev), b_1_f=bfold.to(dev))
+            self.layers.append(L)
         self.ln_g = f32(sd["backbone.layernorm.weight"])
         self.ln_b = f32(sd["backbone.layernorm.bias"])
         F = spec.fusion
@@ -322,9 +336,33 @@ class DepthAnythingModel:
         M = B * (gh * gw + 1)
         e = lambda shape, dt=torch.bfloat16: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
         b = dict(x=e((M, D), torch.float32), ln=e((M, D)), qkv=e((M, 3 * D)), att=e((M, D)), mlp=e((M, s.mlp)),
-                 hs=[e((M, D)) for _ in s.out_indices])
+                 hs=[e((M, D)) for _ in s.out_indices],
+                 part=e((M, D // LN_CHUNK, 2), torch.float32), rs=e((M, 2), torch.float32), shift=e((M,), torch.float32))
+        b["ln_fold"] = dpt.LN_FOLD and D % LN_CHUNK == 0 and self._ln_fold_ok(b, M)
         self._bufs[key] = b
         return b
+
+    def _ln_fold_ok(self, b, M) -> bool:
+        """Whether libi2pc.so takes the LN-folded calls at this size (i2pc_gemm_kernel_name is
+        "invalid" for a descriptor i2pc_gemm would reject)."""
+        L, D = self.layers[0], self.spec.hidden
+
+        def name(x, w, out, **kw):
+            d = ops.GemmDesc()
+            d.a, d.lda, d.m, d.n, d.k = x.data_ptr(), x.stride(0), M, w.shape[0], w.shape[1]
+            d.w, d.ldw, d.c, d.ldc = w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0)
+            d.c_f32 = int(out.element_size() == 4)
+            for k, v in kw.items():
+                setattr(d, k, v)
+            return ops.gemm_kernel_label(d)
+        consumer = dict(ln_rows=b["rs"].data_ptr(), col_sum=L["s_qkv"].data_ptr(), bias=L["b_qkv_f"].data_ptr())
+        producer = dict(res=b["x"].data_ptr(), res_f32=1, ldr=D, ln_part=b["part"].data_ptr(), ln_chunk=LN_CHUNK,
+                        c_bf16=b["ln"].data_ptr(), ldc_bf16=D, ln_shift=b["shift"].data_ptr())
+        names = [name(b["ln"], L["w_qkv_f"], b["qkv"], **consumer),
+                 name(b["ln"], L["w_1_f"], b["mlp"], **dict(consumer, col_sum=L["s_1"].data_ptr(), act=1)),
+                 name(b["att"], L["w_o"], b["x"], **producer),
+                 name(b["mlp"], L["w_2"], b["x"], **producer)]
+        return "invalid" not in names
 
     # ------------------------------------------------------------------ forward
     def forward(self, patches, B: int, gh: int = None, gw: int = None):
@@ -340,7 +378,9 @@ class DepthAnythingModel:
         ops.cls_pos(self.cls, self.pos0, x, B, T, D)
         scale = 1.0 / math.sqrt(D // s.heads)
         hs_i = 0
-        for i, L in enumerate(self.layers):
+        if buf["ln_fold"]:
+            self._encoder_folded(buf, B, T, scale)
+        for i, L in enumerate(self.layers if not buf["ln_fold"] else ()):
             ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
             qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
             att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
@@ -366,6 +406,45 @@ class DepthAnythingModel:
         return ops.head_out(t2, self.w_h3, self.b_h3)
 
     __call__ = forward
+
+    def _encoder_folded(self, buf, B, T, scale):
+        """The encoder with norm1 / norm2 folded through QKV / FC1 (include/i2pc.h "LayerNorm
+        fold"): attention-out and FC2 write the residual's bf16 copy (minus the previous LayerNorm's
+        row mean) and 32-column (mean, M2) partials in their epilogue (the 384-column outputs run on
+        384 x 192 tiles whose 96-column wave tiles hold no whole 64-column chunk); ln_rowstats turns
+        them into (rstd, -rstd * mean) rows the next QKV / FC1 epilogue applies.  The backbone
+        LayerNorm of the kept hidden states stays a LayerNorm kernel on the fp32 rows."""
+        s = self.spec
+        x = buf["x"]
+        nl = len(self.layers)
+        hs_i = 0
+        a_in = None
+        for i, L in enumerate(self.layers):
+            if a_in is None:      # layer 0: norm1 of the embeddings (its row means: the first shift)
+                ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"], mean_out=buf["shift"])
+                qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
+            else:
+                qkv = ops.linear(a_in, L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
+                                 out=buf["qkv"])
+            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x, ln_part=buf["part"], out_bf16=buf["ln"],
+                       ln_shift=buf["shift"], ln_chunk=LN_CHUNK)
+            ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=buf["shift"], shift_out=buf["shift"],
+                            chunk=LN_CHUNK)
+            h = ops.linear(buf["ln"], L["w_1_f"], bias=L["b_1_f"], act="gelu", ln_rows=buf["rs"], col_sum=L["s_1"],
+                           out=buf["mlp"])
+            if i + 1 < nl:
+                # FC2 + residual; its shifted bf16 copy and partials feed the next layer's QKV
+                ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x, ln_part=buf["part"], out_bf16=buf["ln"],
+                           ln_shift=buf["shift"], ln_chunk=LN_CHUNK)
+                ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=buf["shift"], shift_out=buf["shift"],
+                                chunk=LN_CHUNK)
+                a_in = buf["ln"]
+            else:
+                ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x)
+            if (i + 1) in s.out_indices:
+                ops.layernorm(x, self.ln_g, self.ln_b, s.eps, out=buf["hs"][hs_i])    # backbone LayerNorm
+                hs_i += 1
 
     def _reassemble(self, j, hs, B, gh, gw):
         st = self.stages[j]

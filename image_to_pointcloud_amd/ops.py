@@ -35,7 +35,7 @@ class GemmDesc(ctypes.Structure):
         ("out_group", c_int32), ("out_group_stride", c_int32), ("out_offset", c_int32),
         ("convt_s", c_int32), ("convt_h", c_int32), ("convt_w", c_int32), ("convt_c", c_int32),
         ("ln_rows", c_void_p), ("col_sum", c_void_p), ("ln_part", c_void_p), ("c_bf16", c_void_p),
-        ("ldc_bf16", c_int64), ("ln_shift", c_void_p),
+        ("ldc_bf16", c_int64), ("ln_shift", c_void_p), ("ln_chunk", c_int32),
     ]
 
 
@@ -47,6 +47,8 @@ _lib.register("i2pc_gemm_set_engine", ctypes.c_int, [ctypes.c_int])
 _lib.register("i2pc_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
 _lib.register("i2pc_ln_rowstats", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, c_void_p,
                                                  c_void_p, c_void_p, c_void_p])
+_lib.register("i2pc_ln_rowstats_w", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                                   c_void_p, c_void_p, c_void_p, c_void_p])
 _lib.register("i2pc_layernorm_stats", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
                                                      ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p, c_void_p])
 _lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
@@ -151,7 +153,7 @@ def gemm_bytes(d: GemmDesc, esz: float = 2.0, c_esz: float = None) -> float:
     if d.res2:
         b += M * N * 2.0
     if d.ln_part:          # LN-fold producer: the bf16 copy + chunk partials
-        b += M * N * 2.0 + M * (N // 64) * 8.0
+        b += M * N * 2.0 + M * (N // (d.ln_chunk or 64)) * 8.0
     if d.ln_rows:          # LN-fold consumer: row scales + column sums
         b += M * 8.0 + N * 4.0
     return b
@@ -211,14 +213,15 @@ def _linear_padded(x, w, bias, act, res, res2, out, out_f32, rows):
 def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=False,
            a_map=(0, 0, 0), out_map=(0, 0, 0), rows=None, row_bias=None, row_bias_group=1,
            table=None, table_rows=1, ldc=None, ln_rows=None, col_sum=None, ln_part=None, out_bf16=None,
-           ln_shift=None):
+           ln_shift=None, ln_chunk=64):
     """out = act(x @ w.T + bias + row_bias + table) + res + res2.
 
     x: bf16 [*, K] (row stride x.stride(0)); w: bf16 [N, K]; rows = M (defaults to x rows).
     a_map / out_map = (group, group_stride, offset) row remaps (see i2pc.h).
     LayerNorm fold (i2pc.h): ln_rows fp32 [M, 2] (ln_rowstats) + col_sum fp32 [N] make this the
-    consumer (out = act(rs.x * acc + rs.y * col_sum + bias)); ln_part fp32 [M, N / 64, 2] +
-    out_bf16 bf16 [M, N] make an fp32-output call the producer (of out - ln_shift[row] when given).
+    consumer (out = act(rs.x * acc + rs.y * col_sum + bias)); ln_part fp32 [M, N / ln_chunk, 2] +
+    out_bf16 bf16 [M, N] make an fp32-output call the producer (of out - ln_shift[row] when given;
+    ln_chunk 64 or 32 columns per partial).
     """
     torch = _torch()
     _check(x, torch.bfloat16, "x")
@@ -255,9 +258,12 @@ def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=Fal
     if ln_part is not None:
         _check(ln_part, torch.float32, "ln_part")
         _check(out_bf16, torch.bfloat16, "out_bf16")
-        if ln_part.numel() < 2 * M * (N // 64) or out_bf16.shape[0] < M or out_bf16.shape[-1] < N:
+        if ln_chunk not in (32, 64):
+            raise ValueError(f"ln_chunk={ln_chunk} must be 32 or 64")
+        if ln_part.numel() < 2 * M * (N // ln_chunk) or out_bf16.shape[0] < M or out_bf16.shape[-1] < N:
             raise ValueError("ln_part / out_bf16 too small for the call")
         d.ln_part, d.c_bf16, d.ldc_bf16 = _p(ln_part), _p(out_bf16), out_bf16.stride(0)
+        d.ln_chunk = ln_chunk
         if ln_shift is not None:
             _check(ln_shift, torch.float32, "ln_shift")
             d.ln_shift = _p(ln_shift)
@@ -265,10 +271,10 @@ def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=Fal
     return out
 
 
-def ln_rowstats(part, eps, out=None, shift_in=None, shift_out=None):
-    """LayerNorm row statistics from producer partials: part fp32 [M, P, 2] -> out fp32 [M, 2] =
-    (rstd, -rstd * mean) (i2pc_ln_rowstats); shift_in: the producer's ln_shift (None = 0);
-    shift_out fp32 [M] receives the rows' true means (may be shift_in)."""
+def ln_rowstats(part, eps, out=None, shift_in=None, shift_out=None, chunk=64):
+    """LayerNorm row statistics from producer partials: part fp32 [M, P, 2] of `chunk`-column
+    chunks -> out fp32 [M, 2] = (rstd, -rstd * mean) (i2pc_ln_rowstats_w); shift_in: the
+    producer's ln_shift (None = 0); shift_out fp32 [M] receives the rows' true means (may be shift_in)."""
     torch = _torch()
     _check(part, torch.float32, "part")
     _check(shift_in, torch.float32, "shift_in")
@@ -278,7 +284,8 @@ def ln_rowstats(part, eps, out=None, shift_in=None, shift_out=None):
         out = torch.empty((M, 2), dtype=torch.float32, device=part.device)
     nb = M * (P * 8.0 + 8.0 + (4.0 if shift_in is not None else 0.0) + (4.0 if shift_out is not None else 0.0))
     with _Timed("k_ln_rowstats", 0.0, nb):
-        _lib.call("i2pc_ln_rowstats", _p(part), M, P, float(eps), _p(out), _p(shift_in), _p(shift_out), _stream())
+        _lib.call("i2pc_ln_rowstats_w", _p(part), M, P, int(chunk), float(eps), _p(out), _p(shift_in), _p(shift_out),
+                  _stream())
     return out
 
 

@@ -240,12 +240,14 @@ typedef struct i2pc_gemm_desc {
   /* LayerNorm folded through the GEMM (nn.LayerNorm before a linear layer, modeling_dpt.py:233-234,
    * 376-381; NULL = off).
    * Producer (fp32 output rows, e.g. the residual-add epilogue of attention-out / FC2): with
-   *   ln_part set it also writes c_bf16 [m][ldc_bf16] = bf16(out) and, per output row and 64-column
-   *   chunk, ln_part float2 [m][n / 64] = (mean, sum of squared deviations from it) of that chunk of
-   *   out.  With ln_shift (fp32 [m], e.g. the row means of the previous LayerNorm) both are taken
-   *   of out - ln_shift[row] instead (the bf16 copy then keeps its precision for rows whose mean is
-   *   large against their spread).  Needs n % 64 == 0, c_f32, no row remap / ConvTranspose store
-   *   (EUNSUPPORTED where the chosen kernel cannot: i2pc_gemm_kernel_name says "invalid").
+   *   ln_part set it also writes c_bf16 [m][ldc_bf16] = bf16(out) and, per output row and C-column
+   *   chunk (C = ln_chunk: 0 or 64 -> 64, or 32), ln_part float2 [m][n / C] = (mean, sum of squared
+   *   deviations from it) of that chunk of out.  With ln_shift (fp32 [m], e.g. the row means of the
+   *   previous LayerNorm) both are taken of out - ln_shift[row] instead (the bf16 copy then keeps its
+   *   precision for rows whose mean is large against their spread).  Needs n % C == 0, c_f32, no row
+   *   remap / ConvTranspose store (EUNSUPPORTED where the chosen kernel cannot: i2pc_gemm_kernel_name
+   *   says "invalid").  32-column chunks let narrow-tile plans produce (e.g. n = 384 on 384 x 192
+   *   tiles, whose 96-column wave tiles hold no whole 64-column chunk).
    * Consumer (A = the producer's c_bf16, W = W * gamma[k] in bf16): with ln_rows set the epilogue
    *   computes act(rs.x * acc + rs.y * col_sum[n] + bias[n]) with rs = ln_rows float2 [m] =
    *   (rstd, -rstd * mean) (i2pc_ln_rowstats), col_sum fp32 [n] = sum_k of W's bf16 row, bias =
@@ -254,6 +256,7 @@ typedef struct i2pc_gemm_desc {
   const float* ln_rows; const float* col_sum;
   float* ln_part; void* c_bf16; int64_t ldc_bf16;
   const float* ln_shift;
+  int32_t ln_chunk;
 } i2pc_gemm_desc;
 
 /* LayerNorm row statistics from i2pc_gemm's producer partials: rows_out float2 [rows] =
@@ -264,6 +267,9 @@ typedef struct i2pc_gemm_desc {
  * means, shift_in + mean (the next producer's shift; may alias shift_in).  parts <= 64. */
 int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out, const float* shift_in,
                      float* shift_out, void* stream);
+/* The same for chunk_cols-column chunks (32 or 64; i2pc_ln_rowstats = chunk_cols 64). */
+int i2pc_ln_rowstats_w(const float* part, int rows, int parts, int chunk_cols, float eps, float* rows_out,
+                       const float* shift_in, float* shift_out, void* stream);
 
 int i2pc_gemm(const i2pc_gemm_desc* desc, void* stream);
 

@@ -74,3 +74,23 @@ def test_kernel_selection_knobs_are_per_thread():
     assert seen["other"] == default
     assert seen["mine"] != default and seen["mine"].startswith("k_gemm<")
     assert ops.gemm_kernel_label(d) == default
+
+
+def test_ln_fold_producer_plans():
+    """The LN-fold producer plans (i2pc_gemm_kernel_name, no device work): 64-column partials need
+    wave tiles of whole 64-column chunks, so Depth-Anything-V2-Small's 384-wide attention-out / FC2
+    (M = 43840) falls back to 128 x 128 tiles with them and keeps its 384 x 192 tiles with 32-column
+    partials (ln_chunk = 32); ln_chunk other than 0 / 32 / 64 is rejected."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libi2pc.so not built")
+    from image_to_pointcloud_amd import ops
+
+    def label(chunk):
+        d = ops.GemmDesc()
+        d.m, d.n, d.k, d.lda, d.ldw, d.ldc = 43840, 384, 1536, 1536, 1536, 384
+        d.a = d.w = d.c = d.res = d.ln_part = d.c_bf16 = 16
+        d.res_f32, d.ldr, d.c_f32, d.ldc_bf16, d.ln_chunk = 1, 384, 1, 384, chunk
+        return ops.gemm_kernel_label(d)
+    assert label(0).startswith("k_gemm<128, 128") and label(64) == label(0)
+    assert label(32).startswith("k_gemm<384, 192")
+    assert label(48) == "invalid"

@@ -30,8 +30,10 @@ def _rand(shape, g, scale=1.0):
     return ((torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1) * scale)
 
 
-@pytest.mark.parametrize("M,N,K", [(18464, 1024, 1024), (18464, 1024, 4096), (1000, 1024, 1024)])
-def test_producer_outputs(M, N, K):
+@pytest.mark.parametrize("M,N,K,C", [(18464, 1024, 1024, 64), (18464, 1024, 4096, 64), (1000, 1024, 1024, 64),
+                                     (43840, 384, 1536, 32), (43840, 384, 384, 32), (1000, 384, 384, 32)])
+def test_producer_outputs(M, N, K, C):
+    """C = columns per partial chunk (32: Depth-Anything-V2-Small's 384-wide outputs on 384 x 192 tiles)."""
     ops = _ops()
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(M + K)
@@ -42,14 +44,14 @@ def test_producer_outputs(M, N, K):
     y_ref = x0.clone()
     ops.linear(a, w, bias=b, res=y_ref, out=y_ref)
     y = x0.clone()
-    part = torch.empty((M, N // 64, 2), dtype=torch.float32, device=dev)
+    part = torch.empty((M, N // C, 2), dtype=torch.float32, device=dev)
     yb = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
     shift = (_rand((M,), g) * 3).to(torch.float32).to(dev)
-    ops.linear(a, w, bias=b, res=y, out=y, ln_part=part, out_bf16=yb, ln_shift=shift)
+    ops.linear(a, w, bias=b, res=y, out=y, ln_part=part, out_bf16=yb, ln_shift=shift, ln_chunk=C)
     torch.cuda.synchronize()
     assert torch.equal(y, y_ref), "fp32 output changed by the LN-fold producer"
     assert torch.equal(yb, (y - shift[:, None]).to(torch.bfloat16)), "bf16 copy is not bf16(out - shift)"
-    yc = (y - shift[:, None]).double().view(M, N // 64, 64)
+    yc = (y - shift[:, None]).double().view(M, N // C, C)
     mean = yc.mean(-1)
     m2 = ((yc - mean[..., None]) ** 2).sum(-1)
     p = part.double()
@@ -57,19 +59,20 @@ def test_producer_outputs(M, N, K):
     assert torch.allclose(p[..., 1], m2, rtol=1e-4, atol=1e-5)
 
 
-def test_rowstats_match_layernorm_statistics():
+@pytest.mark.parametrize("N,C", [(1024, 64), (384, 32), (1024, 32)])
+def test_rowstats_match_layernorm_statistics(N, C):
     ops = _ops()
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(5)
-    M, N = 4096, 1024
+    M = 4096
     x = (_rand((M, N), g) * torch.linspace(0.1, 3.0, M, dtype=torch.float64)[:, None]
          + torch.linspace(-20, 20, M, dtype=torch.float64)[:, None])
-    xc = x.view(M, N // 64, 64)
+    xc = x.view(M, N // C, C)
     mean_c = xc.mean(-1)
     part = torch.stack([mean_c, ((xc - mean_c[..., None]) ** 2).sum(-1)], -1).to(torch.float32).to(dev)
     s_in = torch.linspace(-5, 5, M, dtype=torch.float32, device=dev)
     s_out = torch.empty(M, dtype=torch.float32, device=dev)
-    rs = ops.ln_rowstats(part, 1e-12, shift_in=s_in, shift_out=s_out)
+    rs = ops.ln_rowstats(part, 1e-12, shift_in=s_in, shift_out=s_out, chunk=C)
     torch.cuda.synchronize()
     mean = x.mean(1)
     rstd = 1.0 / torch.sqrt(x.var(1, unbiased=False) + 1e-12)
@@ -147,4 +150,35 @@ def test_dpt_large_ln_fold_matches_unfused_forward():
     from test_dpt_gpu import _report
     _report("dpt-large ln-fold vs LN kernels", rel_l2=rel)
     # two bf16 paths, each ~1e-2 from transformers fp32 (test_dpt_gpu.py) on this random network
+    assert rel <= 2e-2, rel
+
+
+def test_depth_anything_ln_fold_matches_unfused_forward():
+    """Depth-Anything-V2-Small's encoder with and without the fold (32-column partials from the
+    384 x 192 producer tiles) on the same input: depth within the bf16 noise of each other (both are
+    checked against transformers fp32 in test_depth_anything_gpu.py)."""
+    from image_to_pointcloud_amd import dpt, ops
+    from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL, DepthAnythingModel, synthetic_state_dict
+    dev = torch.device("cuda")
+    model = DepthAnythingModel(DA_V2_SMALL, synthetic_state_dict(DA_V2_SMALL, 0), dev)
+    B, gh, gw = 2, 37, 37
+    g = torch.Generator().manual_seed(4)
+    patches = torch.randn((B * gh * gw, 640), generator=g).to(torch.bfloat16).to(dev)
+    old = dpt.LN_FOLD
+    try:
+        dpt.LN_FOLD = True
+        model._bufs.clear()
+        d1 = model(patches, B, gh, gw).clone()
+        buf = model.buffers(B, gh, gw)
+        assert buf["ln_fold"], "LN fold not taken at Depth-Anything-V2-Small"
+        dpt.LN_FOLD = False
+        model._bufs.clear()
+        d0 = model(patches, B, gh, gw).clone()
+    finally:
+        dpt.LN_FOLD = old
+        model._bufs.clear()
+    torch.cuda.synchronize()
+    rel = ((d1 - d0).norm() / d0.norm()).item()
+    from test_dpt_gpu import _report
+    _report("depth-anything-v2 ln-fold vs LN kernels", rel_l2=rel)
     assert rel <= 2e-2, rel
