@@ -74,14 +74,22 @@ def test_quant_row_remap_skips_cls(dev):
 @pytest.mark.parametrize("dim", [768, 1024])
 def test_layernorm_fp8(dev, dim):
     from image_to_pointcloud_amd import ops
-    x = torch.randn(1000, dim, device=dev) * 3 + 0.5
-    gm = 1 + 0.1 * torch.randn(dim, device=dev)
-    bt = 0.1 * torch.randn(dim, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(dim)
+    x = (torch.randn(1000, dim, generator=g) * 3 + 0.5).to(dev)
+    gm = (1 + 0.1 * torch.randn(dim, generator=g)).to(dev)
+    bt = (0.1 * torch.randn(dim, generator=g)).to(dev)
     got = ops.layernorm_fp8(x, gm, bt, 1e-12)
     ref = ops.quantize_mx(torch.nn.functional.layer_norm(x, (dim,), gm, bt, 1e-12))
-    # fp32 LN rounding may move a value across an e4m3 rounding boundary: allow rare +-1 codes
-    assert torch.equal(got.scale, ref.scale) or (got.scale != ref.scale).float().mean() < 1e-3
-    diff = (got.data.to(torch.int16) - ref.data.to(torch.int16)).abs()
+    # fp32 LN rounding may move a value across an e4m3 rounding boundary (rare +-1 codes) or move a
+    # block's maximum across a power of two (rare scale steps; that block's codes then all differ,
+    # so they are compared only where the scales agree)
+    same = got.scale == ref.scale
+    assert same.float().mean() > 1 - 1e-3
+    def order(codes):                  # e4m3 sign-magnitude codes -> monotone integers (+0 == -0)
+        c = codes.to(torch.int16)
+        return torch.where(c >= 128, 128 - c, c)
+    diff = (order(got.data) - order(ref.data)).abs()
+    diff = diff * same.repeat_interleave(32, dim=1)[:, :dim]
     assert (diff > 1).sum() == 0 and (diff > 0).float().mean() < 1e-3
 
 
