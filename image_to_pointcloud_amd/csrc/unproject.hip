@@ -200,7 +200,8 @@ static Layout layout(int B, int H, int W, int smooth, int nranks = 0) {
   L.trig = off;  off = align_up(off + sizeof(double) * 2 * ((size_t)W + H), 256);
   L.ex = off;    off = align_up(off + sizeof(int64_t) * 4 * (size_t)std::max(B, kBandEx), 256);
   L.mhist = off; off = align_up(off + sizeof(uint32_t) * kBins * (size_t)B, 256);
-  L.gsend = off; off = align_up(off + (nranks > 0 ? sizeof(uint32_t) * kBandWords : 0), 256);
+  // (B = 1: also the single-image path's local band chain, run_unproject)
+  L.gsend = off; off = align_up(off + (nranks > 0 || B == 1 ? sizeof(uint32_t) * kBandWords : 0), 256);
   L.grecv = off; off = align_up(off + sizeof(uint32_t) * kBandWords * (size_t)std::max(nranks, 0), 256);
   L.wpart = off; off = align_up(off + sizeof(uint32_t) * kBelowSlots * 4 * (size_t)B, 256);
   L.field = off;
@@ -3348,6 +3349,16 @@ struct AuxStreams {
   hipEvent_t fork = nullptr, join[kMaxParts - 1] = {};
 };
 static thread_local int g_sel_parts = [] { const char* e = getenv("I2PC_SEL_PARTS"); return e ? atoi(e) : 0; }();
+// "sel_lband" (I2PC_SEL_LBAND): a single image resolves its windows through the band kernels with a
+// local (identity) exchange -- fine histogram and target-bin compaction spread over 3 x kBandSplit
+// workgroups -- instead of k_resolve_w's one workgroup per window, whose key lists grow with the
+// image (the window half-width follows the sample's rank noise).  -1 = automatic (from
+// kLocalBandPixels pixels: measured equal at 1024^2, 120 -> 102 us at 2048^2, 301 -> 248 us at
+// 8192 x 4096), 0 = off, 1 = always (B = 1).
+static thread_local int g_sel_lband = [] { const char* e = getenv("I2PC_SEL_LBAND"); return e ? atoi(e) : -1; }();
+constexpr int64_t kLocalBandPixels = 2 << 20;
+static int local_exchange(void*, uint32_t*, int64_t, int64_t*, int, void*) { return 0; }   // one band: sums in place
+static int local_gather(void*, const uint32_t*, uint32_t*, int64_t, void*) { return 0; }    // recv aliases send
 static int select_parts(int batch) {
   if (!g_sel_windows) return 1;
   const int p = g_sel_parts > 0 ? std::min(g_sel_parts, kMaxParts) : 1;
@@ -3389,6 +3400,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
     I2PC_REQUIRE(blur_k <= kMaxBlur, "smooth_ksize -> kernel %d: at most %d taps", blur_k, kMaxBlur);
   const int granks = xch && xch->gather ? xch->nranks : 0;
   const Layout L = layout(batch, img_h, img_w, params->smooth, granks);
+  const bool lband = !xch && batch == 1 && g_sel_windows &&
+                     (g_sel_lband > 0 || (g_sel_lband < 0 && (int64_t)img_h * img_w >= kLocalBandPixels));
   if (workspace_bytes < L.total) return set_error(I2PC_EWORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
   hipStream_t s = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
@@ -3401,7 +3414,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
   double* trig = params->projection == 1 ? reinterpret_cast<double*>(ws + L.trig) : nullptr;
   hipLaunchKernelGGL(k_prepare, dim3(batch * range_chunks(batch)), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n,
-                     st, (xch || !g_sel_windows) ? hist : nullptr, rpart, xt, yt, dep_h, dep_w, img_h, img_w,
+                     st, (xch || lband || !g_sel_windows) ? hist : nullptr, rpart, xt, yt, dep_h, dep_w, img_h, img_w,
                      cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig, reinterpret_cast<uint32_t*>(ws + L.mhist),
                      range_chunks(batch), reinterpret_cast<uint32_t*>(ws + L.wpart));
 
@@ -3415,6 +3428,12 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   xb.ex = reinterpret_cast<int64_t*>(ws + L.ex);
   xb.send = reinterpret_cast<uint32_t*>(ws + L.gsend);
   xb.recv = reinterpret_cast<uint32_t*>(ws + L.grecv);
+  if (lband) {
+    xb.fn = local_exchange;
+    xb.gather = local_gather;
+    xb.nranks = 1;
+    xb.recv = xb.send;
+  }
   uint32_t* cand = reinterpret_cast<uint32_t*>(ws + L.cand);
   uint32_t* mhist = reinterpret_cast<uint32_t*>(ws + L.mhist);
   uint32_t* wpart = reinterpret_cast<uint32_t*>(ws + L.wpart);
@@ -3443,7 +3462,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
       }
     }
   } else {
-    rc = launch_select(g, st, hist, cand, rpart, mhist, wpart, L.cap, batch, ssel, s, xch ? &xb : nullptr, nrc);
+    rc = launch_select(g, st, hist, cand, rpart, mhist, wpart, L.cap, batch, ssel, s, (xch || lband) ? &xb : nullptr, nrc);
     if (rc) return rc;
   }
 
@@ -3647,6 +3666,7 @@ bool i2pc_unproject_tune(const char* name, int value) {
   if (std::strcmp(name, "unp_rpt") == 0) { i2pc::unproj::g_unp_rpt = value; return true; }
   if (std::strcmp(name, "sel_windows") == 0) { i2pc::unproj::g_sel_windows = value; return true; }
   if (std::strcmp(name, "sel_parts") == 0) { g_sel_parts = value; return true; }
+  if (std::strcmp(name, "sel_lband") == 0) { g_sel_lband = value; return true; }
   if (std::strcmp(name, "sel_rows") == 0) {
     i2pc::unproj::g_sel_rows = value > 0 && value <= i2pc::unproj::kMaxSelRows ? value : 16;
     return true;

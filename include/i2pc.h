@@ -375,6 +375,9 @@ int i2pc_gemm_set_engine(int mode);
  *                 their small launches overlap (joined before the unprojection launch; graph
  *                 capture follows the fork); 0 = automatic = 1 (2-4 measured slower, r03)
  *   "sel_rows"    output rows per selection-sweep workgroup, 1..64 (default 16)
+ *   "sel_lband"   a single image's windows resolved by the band kernels with a local exchange
+ *                 (fine histogram and target-bin compaction over 96 workgroups) instead of one
+ *                 workgroup per window: -1 = automatic (from 2 M pixels; default), 0 = off, 1 = on
  *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _UNP_ROWS / _UNP_NT / _UNP_RPT /

@@ -571,3 +571,54 @@ def test_forked_selection_parts_bit_identical(parts):
     for i in (0, 5, 16):
         ep, _ = ref.depth_to_point_cloud(imgs[i], deps[i], density="high", loop=False)
         assert _same_bits(ref_xyz[i], ep), i
+
+
+@pytest.mark.parametrize("size", [(300, 400), (96, 128)])
+def test_single_image_local_band_chain_matches_resolve_and_oracle(size):
+    """A single image's windows resolved through the band kernels with a local exchange (knob
+    sel_lband 1; automatic from 4 M pixels) against k_resolve_w (sel_lband 0) and the oracle, bit for
+    bit, on the maps built to make windows miss (spikes, NaN / Inf, constant, all-NaN)."""
+    from image_to_pointcloud_amd import ops
+    g = _geom()
+    dev = torch.device("cuda")
+    H, W = size
+    cases = _sel_cases()
+    try:
+        for i, (k, dep) in enumerate(cases.items()):
+            img = _rgb(H, W, 90 + i)
+            td, ti = torch.from_numpy(dep[None]).to(dev), torch.from_numpy(img[None]).to(dev)
+            outs = []
+            for lb in (1, 0):
+                ops.set_tuning("sel_lband", lb)
+                pb = g.unproject_batch(td, ti, density="high", invert=True, depth_scale=10.0)
+                outs.append((pb.xyz.cpu().numpy()[0], pb.stats.cpu().numpy()[0]))
+            assert _same_bits(outs[0][1], outs[1][1]), (k, outs[0][1], outs[1][1])
+            assert _same_bits(outs[0][0], outs[1][0]), (k, _first_diff(outs[0][0], outs[1][0]))
+            with np.errstate(all="ignore"):
+                ep, _ = ref.depth_to_point_cloud(img, dep, density="high", invert=True, depth_scale=10.0, loop=False)
+            assert _same_bits(outs[0][0], ep), (k, _first_diff(outs[0][0], ep))
+    finally:
+        ops.set_tuning("sel_lband", -1)
+
+
+def test_single_large_image_local_band_chain_bit_identical():
+    """A 2048 x 4096 image (above the automatic threshold) with a NaN patch: the local band chain,
+    k_resolve_w and numpy's percentiles agree."""
+    from image_to_pointcloud_amd import ops
+    g = _geom()
+    dev = torch.device("cuda")
+    H, W, h, w = 2048, 4096, 518, 1036
+    dep = _smooth_depth(h, w, 77)
+    dep[100:120, 200:260] = np.nan
+    img = _rgb(H, W, 78)
+    td, ti = torch.from_numpy(dep[None]).to(dev), torch.from_numpy(img[None]).to(dev)
+    outs = []
+    try:
+        for lb in (-1, 0):
+            ops.set_tuning("sel_lband", lb)
+            pb = g.unproject_batch(td, ti, density="high")
+            outs.append((pb.xyz.cpu().numpy()[0], pb.stats.cpu().numpy()[0]))
+    finally:
+        ops.set_tuning("sel_lband", -1)
+    assert _same_bits(outs[0][1], outs[1][1]), (outs[0][1], outs[1][1])
+    assert _same_bits(outs[0][0], outs[1][0]), _first_diff(outs[0][0], outs[1][0])

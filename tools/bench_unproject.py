@@ -1,4 +1,5 @@
-"""Geometry-stage microbenchmark: B x 384^2 depth -> 1024^2 points (density high)."""
+"""Geometry-stage microbenchmark: B x 384^2 depth -> 1024^2 points (density high).
+Usage: bench_unproject.py [B] [density] [H W h w] (image H x W from an h x w depth map)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
@@ -7,6 +8,8 @@ dev = torch.device("cuda")
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 dens = sys.argv[2] if len(sys.argv) > 2 else "high"
 h = w = 384; H = W = 1024
+if len(sys.argv) > 6:
+    H, W, h, w = (int(x) for x in sys.argv[3:7])
 v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
 rng = np.random.default_rng(0)
 dep = np.stack([(0.5 + 4.5 * (0.5 + 0.5 * np.sin(6 * np.pi * u / w + i) * np.cos(4 * np.pi * v / h)) + rng.normal(0, 0.05, (h, w))).astype(np.float32) for i in range(B)])

@@ -14,7 +14,8 @@
 #   gm                         census of the C2 network per GEMM tile-order GROUP_M (2, 4, 8, 16)
 #   ab-gemm                    GEMM engine tests + tools/bench_gemm_ab.py (engine modes, interleaved)
 #   unp                        geometry parity tests, unprojection microbench (warm / cold) per kernel variant
-#   trace-unp [B] [density]    kernel durations of the unprojection microbench (kernel trace only)
+#   trace-unp [B] [density] [H W h w]  kernel durations of the unprojection microbench (kernel trace
+#                              only; TAG=<suffix> names the output directory)
 #   pmc-unp                    SQ counters of the unprojection microbench
 #   c4                         tools/c4_panorama.py on one rank: window / levels / smooth / equirect / network stream
 set -o pipefail
@@ -134,9 +135,9 @@ case "$TASK" in
       echo "$v: $(grep -h 'B=' gpurun_out/v.txt | sed 's/algorithmic.*//' | tr '\n' ' ')"
     done ;;
   trace-unp)
-    D=gpurun_out/trace_unp; rm -rf $D; mkdir -p $D
+    D=gpurun_out/trace_unp${TAG}; rm -rf $D; mkdir -p $D
     timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D/t -o t --output-format csv -- \
-      python tools/bench_unproject.py ${1:-32} ${2:-high} > $D/bench.txt 2>&1 || { tail -5 $D/bench.txt; exit 1; }
+      python tools/bench_unproject.py ${1:-32} ${2:-high} "${@:3}" > $D/bench.txt 2>&1 || { tail -5 $D/bench.txt; exit 1; }
     grep 'B=' $D/bench.txt; stats $D/t unproj ;;
   sel-rows)   # k_sweep_w duration by output rows per workgroup (kernel trace only), then its SQ counters
     for R in 8 16 32 64; do
