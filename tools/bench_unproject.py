@@ -13,6 +13,8 @@ if len(sys.argv) > 6:
 v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
 rng = np.random.default_rng(0)
 dep = np.stack([(0.5 + 4.5 * (0.5 + 0.5 * np.sin(6 * np.pi * u / w + i) * np.cos(4 * np.pi * v / h)) + rng.normal(0, 0.05, (h, w))).astype(np.float32) for i in range(B)])
+if os.environ.get("NAN1"):            # one NaN model pixel per map (the C4 tool's synthetic panorama)
+    dep[:, 7, 11] = np.nan
 img = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev)
 d = torch.from_numpy(dep).to(dev)
 out = geometry.unproject_batch(d, img, density=dens)
