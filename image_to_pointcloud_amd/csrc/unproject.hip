@@ -454,16 +454,11 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
   if ((m & 3) == 0) {
     const int m4 = m >> 2;
     const int per = (m4 + nrc - 1) / nrc;
-    const int i0 = c * per, i1 = min(m4, (c + 1) * per);
+    const int i1 = min(m4, (c + 1) * per);
     const float4* D4 = reinterpret_cast<const float4*>(D);
-    // four float4 per thread and pass, all in flight (clamped, counted once: duplicates of the
-    // slice's last element leave min / max unchanged)
-    for (int i = i0 + threadIdx.x; i < i1; i += 4 * kBlock) {
-      float4 v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = D4[min(i + k * kBlock, i1 - 1)];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) { take(v[k].x); take(v[k].y); take(v[k].z); take(v[k].w); }
+    for (int i = c * per + threadIdx.x; i < i1; i += kBlock) {
+      const float4 v = D4[i];
+      take(v.x); take(v.y); take(v.z); take(v.w);
     }
   } else {
     const int per = (m + nrc - 1) / nrc;
