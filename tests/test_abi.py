@@ -94,3 +94,18 @@ def test_ln_fold_producer_plans():
     assert label(0).startswith("k_gemm<128, 128") and label(64) == label(0)
     assert label(32).startswith("k_gemm<384, 192")
     assert label(48) == "invalid"
+
+
+def test_tuning_knob_names():
+    """Every knob include/i2pc.h documents is accepted by i2pc_set_tuning (host-side state only, no
+    device work); an unknown name is an error (I2PCError)."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libi2pc.so not built")
+    from image_to_pointcloud_amd import ops
+    defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "unp_rows": 1, "unp_nt": 1, "unp_rpt": 8,
+                "sel_windows": 1, "sel_parts": 0, "sel_rows": 16, "sel_lband": -1, "attn_lazy": 1,
+                "attn_scalar": 1, "ln_f2": 1}
+    for name, v in defaults.items():
+        ops.set_tuning(name, v)
+    with pytest.raises(_lib.I2PCError):
+        ops.set_tuning("no_such_knob", 1)
