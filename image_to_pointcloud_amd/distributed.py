@@ -166,6 +166,46 @@ def band_gather(group=None):
     return _gather
 
 
+def band_point_counts(img_h: int, img_w: int, world_size: int, step: int = 1) -> list:
+    """Points of every rank's band (geometry.band_rows) of an img_h x img_w image at density step."""
+    from . import geometry
+    wn = (img_w + step - 1) // step
+    return [((r1 + step - 1) // step - r0 // step) * wn for r0, r1 in geometry.band_rows(img_h, world_size, step)]
+
+
+def gather_band_points(xyz, rgb, img_h: int, img_w: int, step: int = 1, group=None, pad=None):
+    """C4's last step: every rank's band points [Nb, 3] -> the whole image's points on
+    every rank, row-major as the single-GPU unprojection writes them.  The bands hold different
+    point counts (the last band can be shorter), so each is padded to the largest one for one RCCL
+    all-gather per tensor (gloo: staged through host memory) and the pads are dropped.
+    pad: optional (xyz, rgb) send buffers of the largest band's size, reused across calls."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return xyz, rgb
+    world = dist.get_world_size(group)
+    counts = band_point_counts(img_h, img_w, world, step)
+    rank = dist.get_rank(group)
+    if xyz.shape[0] != counts[rank] or rgb.shape[0] != counts[rank]:
+        raise ValueError(f"band of rank {rank} holds {xyz.shape[0]} points, the split gives {counts[rank]}")
+    nmax = max(counts)
+    px, pr = pad if pad is not None else (xyz.new_zeros((nmax, 3)), rgb.new_zeros((nmax, 3)))
+    px[:counts[rank]].copy_(xyz)
+    pr[:counts[rank]].copy_(rgb)
+    host = dist.get_backend(group) == "gloo"
+    outs = []
+    for t in (px, pr):
+        if host:
+            g = torch.empty((world * nmax, 3), dtype=t.dtype)
+            dist.all_gather_into_tensor(g, t.cpu(), group=group)
+            g = g.to(t.device)
+        else:
+            g = t.new_empty((world * nmax, 3))
+            dist.all_gather_into_tensor(g, t, group=group)
+        outs.append(torch.cat([g[k * nmax:k * nmax + counts[k]] for k in range(world)]))
+    return outs[0], outs[1]
+
+
 def reduce_bbox(bbox, group=None):
     """Global bounds from per-band bboxes [6] (min x, max x, min y, max y, min z, max z)."""
     import torch.distributed as dist

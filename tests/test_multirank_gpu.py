@@ -102,7 +102,7 @@ def test_bench_gpus_2_launches_two_ranks():
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
 
 
-@pytest.mark.parametrize("extra", [[], ["--smooth", "--ksize", "9"], ["--levels"]])
+@pytest.mark.parametrize("extra", [[], ["--smooth", "--ksize", "9"], ["--levels"], ["--gather", "--density", "medium"]])
 def test_c4_two_ranks_window_bands_bit_exact(extra):
     """C4 with two real ranks (gloo, sharing cuda:0, host-staged exchange): each rank unprojects its
     band of a 600 x 1000 panorama with the window selection across bands (or the histogram levels),
@@ -117,4 +117,6 @@ def test_c4_two_ranks_window_bands_bit_exact(extra):
     assert len(lines) == 1, r.stdout[-2000:]
     rec = json.loads(lines[0])
     assert rec["n_ranks"] == 2 and rec["bit_exact_vs_whole_image"] is True, rec
+    if "--gather" in extra:     # the whole 600 x 1000 panorama at step 2, assembled on every rank
+        assert rec["points_gathered"] == 300 * 500, rec
     assert ("histogram levels" in rec["exchange"]) == ("--levels" in extra)

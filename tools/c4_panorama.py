@@ -20,7 +20,9 @@ unprojects its band of it (ms_per_image = a step / its N panoramas: network / N 
 band call).  --projection equirect back-projects the panorama on the sphere (i2pc.h; the
 reference only has the pinhole model); --smooth applies smooth_depth (the band's blurred field
 with its halo rows, recomputed locally); --levels takes the four histogram levels with a host
-exchange instead of the one-sweep window selection.
+exchange instead of the one-sweep window selection.  --gather then all-gathers every band's points
+onto every rank (the whole panorama's point cloud, row-major), timed apart as
+gather_ms; with --check the assembled cloud must equal the whole-image unprojection bit for bit.
 """
 import argparse
 import json
@@ -51,6 +53,8 @@ def main():
     ap.add_argument("--smooth", action="store_true", help="smooth_depth (GaussianBlur, --ksize)")
     ap.add_argument("--ksize", type=int, default=5)
     ap.add_argument("--levels", action="store_true", help="histogram-level selection, host-callback exchange")
+    ap.add_argument("--gather", action="store_true",
+                    help="then all-gather every band's points onto every rank (SURVEY 8e step 3), timed apart")
     a = ap.parse_args()
     rank, local, world = D.world()
     ngpu = torch.cuda.device_count()
@@ -156,6 +160,22 @@ def main():
         dist.barrier()
     el = D.max_over_ranks(time.perf_counter() - t0, dev) if world > 1 else time.perf_counter() - t0
     bbox = D.reduce_bbox(res[2]) if world > 1 else res[2]
+    gathered, gather_ms = None, None
+    if a.gather:
+        nmax = max(D.band_point_counts(H, W, world, step))
+        pad = (res[0].new_zeros((nmax, 3)), res[1].new_zeros((nmax, 3)))
+        gathered = D.gather_band_points(res[0], res[1], H, W, step, pad=pad)   # (warm-up)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            gathered = D.gather_band_points(res[0], res[1], H, W, step, pad=pad)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        g_el = D.max_over_ranks(time.perf_counter() - t1, dev) if world > 1 else time.perf_counter() - t1
+        gather_ms = round(g_el / a.steps * 1e3, 3)
     ok = None
     if a.check:
         full = np.empty((H, W, 3), np.uint8)
@@ -171,6 +191,8 @@ def main():
                   and torch.equal(whole.rgb[0][p0:p0 + res[1].shape[0]], res[1])
                   and torch.equal(whole.stats[0].view(torch.int64), res[3].view(torch.int64))   # NaN-aware
                   and torch.equal(whole.bbox[0], bbox))
+        if gathered is not None:        # the assembled panorama equals the whole-image call
+            ok = ok and bool(torch.equal(whole.xyz[0], gathered[0]) and torch.equal(whole.rgb[0], gathered[1]))
         if world > 1:
             t = torch.tensor([int(ok)], device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -191,6 +213,8 @@ def main():
                                           "RCCL broadcast from its owner"
                           if a.network else "synthetic smooth field + NaN",
                           "projection": a.projection,
+                          "points_gathered": None if gathered is None else int(gathered[0].shape[0]),
+                          "gather_ms": gather_ms,
                           "bit_exact_vs_whole_image": ok, "stats": res[3].tolist(), "bbox": bbox.tolist()}))
     if comm is not None:
         comm.close()
