@@ -1499,7 +1499,7 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
 // so the filled map's rank-r value is F_(r) if F_(r) < med, else F_(r-k) if F_(r-k) > med,
 // else med: targets t = F_(r_t) and 4 + t = F_(r_t - k) for the four percentile ranks.
 // Ranks outside F are resolved at once to the +-inf keys (they never win those tests).
-__device__ void fill_targets(SelState& s) {
+__device__ void fill_targets(SelState& s, bool drop_unread = false) {
   const uint32_t n = s.n, k = s.nonfinite_count, nfin = n - k, nneg = s.ninf_neg;
   uint32_t r[4];
   pct_ranks(n, r);
@@ -1522,6 +1522,26 @@ __device__ void fill_targets(SelState& s) {
     if (g[i] < nneg) set(8 + i, -1);
     else if (g[i] >= nneg + nfin) set(8 + i, (int64_t)nfin);
     else set(8 + i, (int64_t)(g[i] - nneg));
+  }
+  // Only one of a percentile's pair is ever read (finish_targets: F(r) < med ? F(r) : max(F(r-k),
+  // med)), and which one follows from the ranks alone when the median is finite: below the lower
+  // median rank F(r) <= med, so the value is F(r) (at F(r) == med the twin gives med too); above
+  // the upper one F(r) >= med, so it is max(F(r-k), med).  The other target is marked resolved
+  // with a key that sends finish_targets the right way, so it needs no window: with a few %
+  // non-finite pixels the unused twin sits k ranks away from every window and used to send the
+  // whole image to k_sel_slow's selection from scratch (~5 ms for 32 x 1024^2 at 0.1 % NaN pixels).
+  // Window paths only (drop_unread): the histogram levels group targets by bin and keep them all.
+  if (drop_unread && g[0] >= nneg && g[1] < nneg + nfin) {
+    const int64_t lo = (int64_t)(g[0] - nneg), hi = (int64_t)(g[1] - nneg);
+    for (int t = 0; t < 4; ++t) {
+      if ((int64_t)r[t] < lo && s.tlo[4 + t] != s.thi[4 + t]) {            // the twin is never read
+        s.tlo[4 + t] = s.thi[4 + t] = kKeyNegInf;
+        s.tslot[4 + t] = kNoSlot;
+      } else if ((int64_t)r[t] > hi && s.tlo[t] != s.thi[t]) {             // F(r) only compares >= med
+        s.tlo[t] = s.thi[t] = kKeyPosInf;
+        s.tslot[t] = kNoSlot;
+      }
+    }
   }
   s.ntgt = kMaxTgt;
   s.fill = 1;
@@ -1798,7 +1818,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32
       }
       done = true;
     } else {
-      fill_targets(s);      // (+-inf sentinel targets come back resolved: tlo == thi)
+      fill_targets(s, true);   // (+-inf sentinel and unread targets come back resolved: tlo == thi)
     }
     if (!done) {
       const uint32_t nwin = s.nwin;
@@ -1968,9 +1988,41 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
       if (threadIdx.x == 0) {
         done = finish_targets(s, false) ? 1 : 0;
         if (done) st[b] = s;
+        // every target resolved, only the min / max branch's range is missing (p98 <= p2: a
+        // constant or near-constant map): one pass for the finite range instead of the selection
+        // from scratch below
+        bool resolved = !done;
+        for (int t = 0; t < (int)s.ntgt; ++t) resolved = resolved && s.tlo[t] == s.thi[t];
+        if (resolved) done = 2;
       }
       __syncthreads();
-      if (done) return;
+      if (done == 1) return;
+      if (done == 2) {
+        const int n = g.H * g.W;
+        uint32_t lo = 0xffffffffu, hi = 0u;
+        for (int p = threadIdx.x; p < n; p += kSlowBlock) {
+          const int v = p / g.W, u = p - v * g.W;
+          const float val = sample(g, b, v, u);
+          if (isfinite(val)) {
+            const uint32_t k = f2key(val);
+            lo = min(lo, k);
+            hi = max(hi, k);
+          }
+        }
+        lo = wave_min_u32(lo);
+        hi = wave_max_u32(hi);
+        if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = lo; red[1][threadIdx.x >> 6] = hi; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          for (int w = 0; w < kSlowBlock / 64; ++w) { lo = min(lo, red[0][w]); hi = max(hi, red[1][w]); }
+          s.kmin = min(s.kmin, lo);      // (with a fill, finish_targets already merged the median)
+          s.kmax = max(s.kmax, hi);
+          if (finish_targets(s, true)) st[b] = s;
+          else done = 0;                 // (not expected: the range was the only thing missing)
+        }
+        __syncthreads();
+        if (done == 2) return;
+      }
     }
   } else if (s.phase != PH_SLOW) {
     return;
@@ -2994,7 +3046,7 @@ __global__ __launch_bounds__(kBlock) void k_bandw_pickc(SelState* st, const uint
       }
       done = true;
     } else {
-      fill_targets(s);
+      fill_targets(s, true);
     }
     if (!done) {
       if (w == 0 && rec) {

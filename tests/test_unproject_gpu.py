@@ -489,11 +489,22 @@ def _sel_cases():
     out["nan_inf"] = d
     d = base.copy(); d.ravel()[rng.permutation(d.size)[:d.size * 2 // 5]] = np.nan
     out["nan_40pct"] = d
+    # sparse non-finite pixels (a few % of the resized map): the unread twin of each percentile
+    # pair lies k ranks outside every window and is skipped by rank (fill_targets)
+    d = base.copy(); idx = rng.permutation(d.size)[:d.size // 200]
+    d.ravel()[idx[0::3]] = np.nan; d.ravel()[idx[1::3]] = np.inf; d.ravel()[idx[2::3]] = -np.inf
+    out["sparse_nonfinite"] = d
     # +-inf in the last model column and row: cv2's single-tap border copies them unblended, so the
     # resized map holds +-inf there, not the NaN an inf * 0 weight would make
     d = base.copy(); d[5:40, -1] = np.inf; d[-1, 7:30] = -np.inf
     out["inf_border"] = d
     out["constant"] = np.full_like(base, 2.5)
+    # p2 == p98 with a wider range: the min / max branch (app.py:198-199) from a range-only pass
+    d = np.full_like(base, 1.0)
+    d.ravel()[rng.permutation(d.size)[:d.size // 100]] = rng.uniform(0.5, 3.0, d.size // 100).astype(np.float32)
+    out["near_constant"] = d
+    d = d.copy(); d[4, 9] = np.nan
+    out["near_constant_nan"] = d
     out["all_nan"] = np.full_like(base, np.nan)
     return out
 

@@ -1,5 +1,6 @@
 """Geometry-stage microbenchmark: B x 384^2 depth -> 1024^2 points (density high).
-Usage: bench_unproject.py [B] [density] [H W h w] (image H x W from an h x w depth map)."""
+Usage: bench_unproject.py [B] [density] [H W h w] (image H x W from an h x w depth map);
+DEPTH=const|nan01 for SURVEY 8d's constant-depth and 0.1 %-NaN variants, NAN1=1 for one NaN."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
@@ -15,6 +16,12 @@ rng = np.random.default_rng(0)
 dep = np.stack([(0.5 + 4.5 * (0.5 + 0.5 * np.sin(6 * np.pi * u / w + i) * np.cos(4 * np.pi * v / h)) + rng.normal(0, 0.05, (h, w))).astype(np.float32) for i in range(B)])
 if os.environ.get("NAN1"):            # one NaN model pixel per map (the C4 tool's synthetic panorama)
     dep[:, 7, 11] = np.nan
+kind = os.environ.get("DEPTH", "smooth")   # SURVEY 8d's microbenchmark variants
+if kind == "const":
+    dep[:] = 2.5
+elif kind == "nan01":                    # 0.1 % of the model pixels NaN
+    for i in range(B):
+        dep[i].ravel()[rng.permutation(h * w)[:(h * w) // 1000]] = np.nan
 img = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev)
 d = torch.from_numpy(dep).to(dev)
 out = geometry.unproject_batch(d, img, density=dens)
