@@ -244,6 +244,39 @@ def _launch_ranks(a) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def _multi_gpu_diag(a, pipe, images, og, own_s, world, device):
+    """N > 1: why the whole-job number is what it is, per rank.
+    step_ms -- this rank's own timed-loop time per step (the job's value uses the max over ranks);
+    compute_ms -- the same rank running its step alone, no gather, timed right after the loop;
+    gather_wait_ms -- per step, how long the compute stream waited for the overlapped all-gather
+    (OverlappedGather.gather_wait_ms; host-staged gloo: the whole synchronous staging)."""
+    import torch
+    import torch.distributed as dist
+    wait_ms = og.gather_wait_ms() / a.steps if og is not None else 0.0
+    run = og.runs[0] if og is not None else ((lambda: pipe.run(images)) if a.no_graph else pipe.replay)
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        run()
+    torch.cuda.synchronize()
+    comp_ms = (time.perf_counter() - t0) / a.steps * 1e3
+    mine = torch.tensor([own_s / a.steps * 1e3, comp_ms, wait_ms], dtype=torch.float64)
+    backend = dist.get_backend()
+    if backend != "gloo":
+        mine = mine.to(device)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    per = [{"rank": r, "step_ms": round(float(v[0]), 3), "compute_ms": round(float(v[1]), 3),
+            "gather_wait_ms": round(float(v[2]), 3)} for r, v in enumerate(allv)]
+    return {"world": world, "backend": backend,
+            "rccl_world_size": dist.get_world_size() if backend == "nccl" else None,
+            "all_gather": og is not None,
+            "gathered_bytes_per_step_per_rank": og.recv_bytes_per_step if og is not None else 0,
+            "sent_bytes_per_step_per_rank": og.send_bytes_per_step if og is not None else 0,
+            "per_rank": per}
+
+
 def main():
     a = _args()
     env_world = os.environ.get("WORLD_SIZE")
@@ -307,6 +340,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if gather:
+        og.reset_stats()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
@@ -314,7 +349,9 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = D.max_over_ranks(time.perf_counter() - t0, device)
+    own = time.perf_counter() - t0
+    elapsed = D.max_over_ranks(own, device)
+    multi = _multi_gpu_diag(a, pipe, images, og if gather else None, own, world, device) if world > 1 else None
     points_step = world * B * pipe.points_per_image
     value = points_step * a.steps / elapsed / 1e6
     ms = elapsed / a.steps * 1e3
@@ -427,6 +464,7 @@ def main():
             "roofline": roofline,
             "rooflines": rooflines,
             "cpu_baseline": cpu,
+            "multi_gpu": multi,
             "kernels": kernels,
         }
         print(json.dumps(out))

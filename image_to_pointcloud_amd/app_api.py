@@ -205,10 +205,14 @@ def decode_image(image_data: bytes) -> np.ndarray:
     return np.ascontiguousarray(rgb[:, :, ::-1])
 
 
-def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, model_info: dict) -> dict:
+def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, model_info: dict,
+                  on_progress=None) -> dict:
     """The depth branch of process_image_pipeline (app.py:456-559) as one device pass:
-    depth -> preview -> unprojection + bbox -> outlier removal -> preview subsample -> artefact."""
+    depth -> preview -> unprojection + bbox -> outlier removal -> preview subsample -> artefact.
+    `on_progress(progress, message)` receives the reference's milestones 60 (app.py:465-466,
+    after the depth preview) and 80 (app.py:492-493, after the outlier removal)."""
     import torch
+    report = on_progress if on_progress is not None else (lambda progress, message: None)
     dev = geometry.require_device()
     timg = torch.from_numpy(np.ascontiguousarray(image)).to(dev)
     depth = _depth_device(timg, model_info)
@@ -217,6 +221,7 @@ def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, mo
         depth_url = preview.encode_png_data_url(preview.colored_preview(depth, request.invert_depth).cpu().numpy())
     except Exception as e:
         logger.error(f"Failed to create depth preview: {e}")
+    report(60, "Generating 3D point cloud...")
     pb = geometry.unproject_batch(depth[None], timg[None], density=request.point_density,
                                   invert=request.invert_depth, depth_scale=request.depth_scale,
                                   smooth=request.smooth_depth, smooth_ksize=request.smooth_ksize)
@@ -224,6 +229,7 @@ def run_depth_job(image: np.ndarray, request: ProcessingRequest, job_id: str, mo
     if REFINE_POINT_CLOUD:                                                # app.py:479
         sr = geometry.remove_statistical_outlier(xyz, rgb)
         xyz, rgb, bbox = sr.xyz, sr.rgb, sr.bbox
+    report(80, "Saving point cloud...")
     n = xyz.shape[0]
     prev_pts, prev_cols = geometry.preview_subsample(xyz, rgb, MAX_PREVIEW)
     points = xyz.cpu().numpy()
@@ -256,7 +262,8 @@ def process_image_pipeline(job_id: str, image_data: bytes, request: ProcessingRe
         if model_info.get("type") != "depth":
             raise ValueError(f"model {request.model} has no depth branch in this backend")
         job.update(progress=40, message="Estimating depth with AI...")
-        results = run_depth_job(image, request, job_id, model_info)
+        results = run_depth_job(image, request, job_id, model_info,
+                                on_progress=lambda pr, msg: job.update(progress=pr, message=msg))
         job.update(progress=100, status="completed", message="Processing complete!", results=results)
     except Exception as e:
         logger.error(f"Error in processing pipeline: {str(e)}")

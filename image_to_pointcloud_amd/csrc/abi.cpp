@@ -34,5 +34,9 @@ extern "C" int i2pc_set_tuning(const char* name, int value) {
   if (i2pc_gemm_tune(name, value) || i2pc_unproject_tune(name, value) || i2pc_attention_tune(name, value) ||
       i2pc_misc_tune(name, value))
     return I2PC_OK;
-  return i2pc::set_error(I2PC_EINVAL, "unknown tuning knob '%s' (gemm_tail, gemm_bn128, gemm_splitk, unp_rows, unp_nt, unp_rpt, sel_windows, sel_parts, sel_rows, sel_lband, attn_lazy, attn_scalar, ln_f2: include/i2pc.h)", name);
+  return i2pc::set_error(I2PC_EINVAL,
+                         "unknown tuning knob '%s' (gemm_tail, gemm_bn128, gemm_splitk, gemm_split_tile, gemm_tile192, "
+                         "unp_rows, unp_nt, unp_rpt, sel_windows, sel_parts, sel_rows, sel_lband, attn_lazy, attn_scalar, "
+                         "ln_f2: include/i2pc.h)",
+                         name);
 }

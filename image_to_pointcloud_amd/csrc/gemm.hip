@@ -2252,7 +2252,8 @@ extern "C" int i2pc_gemm_set_engine(int mode) {
   return I2PC_OK;
 }
 
-// process-wide tuning knobs (i2pc_set_tuning): "gemm_tail" (round-quantisation split on/off)
+// per-host-thread tuning knobs (i2pc_set_tuning; thread_local above): gemm_tail, gemm_bn128,
+// gemm_splitk, gemm_split_tile, gemm_tile192
 bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }

@@ -1531,20 +1531,27 @@ __device__ void fill_targets(SelState& s, bool drop_unread = false) {
   // non-finite pixels the unused twin sits k ranks away from every window and used to send the
   // whole image to k_sel_slow's selection from scratch (~5 ms for 32 x 1024^2 at 0.1 % NaN pixels).
   // Window paths only (drop_unread): the histogram levels group targets by bin and keep them all.
+  // The argument needs a FINITE median: np.mean of two middle values near +-FLT_MAX overflows to
+  // +-inf, and then F(r) above the upper rank compares below med after all.  fill = 2 records that
+  // targets were dropped; finish_targets refuses such an image when med is not finite, and it goes
+  // to the selection from scratch.
+  bool dropped = false;
   if (drop_unread && g[0] >= nneg && g[1] < nneg + nfin) {
     const int64_t lo = (int64_t)(g[0] - nneg), hi = (int64_t)(g[1] - nneg);
     for (int t = 0; t < 4; ++t) {
       if ((int64_t)r[t] < lo && s.tlo[4 + t] != s.thi[4 + t]) {            // the twin is never read
         s.tlo[4 + t] = s.thi[4 + t] = kKeyNegInf;
         s.tslot[4 + t] = kNoSlot;
+        dropped = true;
       } else if ((int64_t)r[t] > hi && s.tlo[t] != s.thi[t]) {             // F(r) only compares >= med
         s.tlo[t] = s.thi[t] = kKeyPosInf;
         s.tslot[t] = kNoSlot;
+        dropped = true;
       }
     }
   }
   s.ntgt = kMaxTgt;
-  s.fill = 1;
+  s.fill = dropped ? 2 : 1;
 }
 
 // All targets resolved: p2 / p98 (and their branch) from the target keys (false: the
@@ -1560,6 +1567,10 @@ __device__ bool finish_targets(SelState& s, bool have_mm = true) {
     s.p2 = s.p98 = (double)med;
     s.phase = PH_DONE;
     return true;
+  }
+  if (s.fill == 2 && !isfinite(med)) {   // dropped targets assumed a finite median (fill_targets)
+    s.err = 1;
+    return false;
   }
   const uint32_t mk = f2key(med);
   uint32_t pk[4];
@@ -1991,7 +2002,7 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
         // every target resolved, only the min / max branch's range is missing (p98 <= p2: a
         // constant or near-constant map): one pass for the finite range instead of the selection
         // from scratch below
-        bool resolved = !done;
+        bool resolved = !done && s.err == 0;
         for (int t = 0; t < (int)s.ntgt; ++t) resolved = resolved && s.tlo[t] == s.thi[t];
         if (resolved) done = 2;
       }
@@ -3399,6 +3410,19 @@ struct AuxStreams {
   int dev = -1;
   hipStream_t s[kMaxParts - 1] = {};
   hipEvent_t fork = nullptr, join[kMaxParts - 1] = {};
+  // released when the owning host thread exits (thread_local below; the main thread's run before
+  // the static destructors, so the HIP runtime is still up)
+  ~AuxStreams() {
+    if (dev < 0) return;
+    int cur = -1;
+    const bool swap = hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess;
+    for (int i = 0; i < kMaxParts - 1; ++i) {
+      if (s[i]) (void)hipStreamDestroy(s[i]);
+      if (join[i]) (void)hipEventDestroy(join[i]);
+    }
+    if (fork) (void)hipEventDestroy(fork);
+    if (swap) (void)hipSetDevice(cur);
+  }
 };
 static thread_local int g_sel_parts = [] { const char* e = getenv("I2PC_SEL_PARTS"); return e ? atoi(e) : 0; }();
 // "sel_lband" (I2PC_SEL_LBAND): a single image resolves its windows through the band kernels with a

@@ -66,11 +66,34 @@ class OverlappedGather:
         if len(runs) != 2:
             raise ValueError("OverlappedGather needs two step callables (double-buffered point sets)")
         self.runs, self.group = runs, group
+        self.world = dist.get_world_size(group)
         self.gx = [torch.empty((world * batch, points, 3), dtype=torch.float32, device=device) for _ in range(2)]
         self.gr = [torch.empty((world * batch, points, 3), dtype=torch.uint8, device=device) for _ in range(2)]
         self.host_staged = self.gx[0].is_cuda and dist.get_backend(group) == "gloo"
         self.works = [None, None]
         self.k = 0
+        # diagnostics (bench.py at N > 1): bytes a rank receives per step (xyz f32 + rgb u8 of every
+        # other rank's images), and the time its compute stream waited for gathers
+        self.recv_bytes_per_step = (world - 1) * batch * points * 15
+        self.send_bytes_per_step = batch * points * 15
+        self.reset_stats()
+
+    def reset_stats(self):
+        """Start a new gather-wait measurement (gather_wait_ms)."""
+        self._wait_s = 0.0         # host-side waits (host-staged gloo, CPU tensors)
+        self._events = []          # (before, after) CUDA events around the compute stream's waits
+
+    def gather_wait_ms(self) -> float:
+        """Milliseconds the compute stream (or, host-staged, the host) spent waiting for gathers since
+        reset_stats(): for an async RCCL gather the gap between an event recorded before the stream's
+        wait on the collective and one recorded after it (0 when the gather finished under the next
+        step's compute)."""
+        ms = self._wait_s * 1e3
+        if self._events:
+            import torch
+            torch.cuda.synchronize()
+            ms += sum(a.elapsed_time(b) for a, b in self._events)
+        return ms
 
     def step(self):
         import torch.distributed as dist
@@ -78,10 +101,15 @@ class OverlappedGather:
         self._wait(slot)                      # the gather that read this slot's buffers is done
         out = self.runs[slot]()
         if self.host_staged:
+            import time
+            import torch
+            torch.cuda.current_stream().synchronize()     # the compute is not part of the wait
+            t0 = time.perf_counter()
             for dst, src in ((self.gx[slot], out.xyz), (self.gr[slot], out.rgb)):
                 host = dst.new_empty(dst.shape, device="cpu")
                 dist.all_gather_into_tensor(host, src.cpu(), group=self.group)
                 dst.copy_(host)
+            self._wait_s += time.perf_counter() - t0
         else:
             self.works[slot] = (
                 dist.all_gather_into_tensor(self.gx[slot], out.xyz, group=self.group, async_op=True),
@@ -92,8 +120,20 @@ class OverlappedGather:
     def _wait(self, slot):
         w = self.works[slot]
         if w is not None:
-            for x in w:
-                x.wait()
+            if self.gx[0].is_cuda:
+                import torch
+                before, after = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                before.record()
+                for x in w:
+                    x.wait()
+                after.record()
+                self._events.append((before, after))
+            else:
+                import time
+                t0 = time.perf_counter()
+                for x in w:
+                    x.wait()
+                self._wait_s += time.perf_counter() - t0
             self.works[slot] = None
 
     def finish(self):

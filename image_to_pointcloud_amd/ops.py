@@ -127,10 +127,14 @@ def gemm_kernel_label(desc: GemmDesc) -> str:
     return _lib.load().i2pc_gemm_kernel_name(ctypes.byref(desc)).decode()
 
 
+# every knob i2pc_set_tuning accepts (include/i2pc.h), checked by tests/test_abi.py
+TUNING_KNOBS = ("gemm_tail", "gemm_bn128", "gemm_splitk", "gemm_split_tile", "gemm_tile192", "unp_rows", "unp_nt",
+                "unp_rpt", "sel_windows", "sel_parts", "sel_rows", "sel_lband", "attn_lazy", "attn_scalar", "ln_f2")
+
+
 def set_tuning(name: str, value: int) -> None:
     """Kernel-selection knob (i2pc_set_tuning) for calls made from THIS host thread (thread-local
-    in libi2pc.so): gemm_tail, gemm_bn128, gemm_splitk, unp_rows, unp_nt, unp_rpt, sel_windows,
-    attn_lazy, attn_scalar, ln_f2."""
+    in libi2pc.so); the names are TUNING_KNOBS."""
     _lib.call("i2pc_set_tuning", name.encode(), int(value))
 
 
@@ -183,6 +187,27 @@ def _pad_cols(t, cols: int):
     return o
 
 
+_PAD_CACHE = {}
+
+
+def _padded_param(t, shape, fill_view):
+    """Zero-padded copy of a parameter tensor, made once per (tensor, version) and cached (ADVICE
+    r03: the padded GEMM / conv paths used to rebuild every weight and bias on each call, inside HIP
+    graph captures too).  fill_view(padded) returns the view `t` is copied into."""
+    import weakref
+    torch = _torch()
+    key = (id(t), tuple(shape))
+    hit = _PAD_CACHE.get(key)
+    if hit is not None and hit[0]() is t and hit[1] == t._version:
+        return hit[2]
+    o = torch.zeros(shape, dtype=t.dtype, device=t.device)
+    fill_view(o).copy_(t.reshape(fill_view(o).shape))
+    for k in [k for k, v in _PAD_CACHE.items() if v[0]() is None]:       # drop entries of freed tensors
+        del _PAD_CACHE[k]
+    _PAD_CACHE[key] = (weakref.ref(t), t._version, o)
+    return o
+
+
 def _linear_padded(x, w, bias, act, res, res2, out, out_f32, rows):
     """linear() for widths the GEMM engines do not take (K % 64, N % 32): the operands are
     zero-padded to K' = ceil64(K), N' = ceil32(N) (zero weights and bias add nothing), the HIP
@@ -193,12 +218,8 @@ def _linear_padded(x, w, bias, act, res, res2, out, out_f32, rows):
     N, K = w.shape
     Kp, Np = _ceil(K, 64), _ceil(N, 32)
     xp = _pad_cols(x[:M].reshape(M, -1)[:, :K], Kp) if Kp != K else x
-    wp = torch.zeros((Np, Kp), dtype=w.dtype, device=w.device)
-    wp[:N, :K] = w
-    bp = None
-    if bias is not None:
-        bp = torch.zeros(Np, dtype=bias.dtype, device=bias.device)
-        bp[:N] = bias
+    wp = _padded_param(w, (Np, Kp), lambda o: o[:N, :K])
+    bp = _padded_param(bias, (Np,), lambda o: o[:N]) if bias is not None else None
     rp = _pad_cols(res[:M], Np) if res is not None else None
     r2p = _pad_cols(res2[:M], Np) if res2 is not None else None
     dt = out.dtype if out is not None else (torch.float32 if out_f32 else torch.bfloat16)
@@ -321,12 +342,8 @@ def conv2d(x, w, bias=None, k=3, stride=1, pad=1, relu_in=False, act=None, res=N
         if Cp != C:
             xp = torch.zeros((B, H, W, Cp), dtype=x.dtype, device=x.device)
             xp[..., :C] = x
-        wp = torch.zeros((Cop, k * k, Cp), dtype=w.dtype, device=w.device)
-        wp[:Co, :, :C] = w.reshape(Co, k * k, C)
-        bp = None
-        if bias is not None:
-            bp = torch.zeros(Cop, dtype=bias.dtype, device=bias.device)
-            bp[:Co] = bias
+        wp = _padded_param(w, (Cop, k * k, Cp), lambda o: o[:Co, :, :C])
+        bp = _padded_param(bias, (Cop,), lambda o: o[:Co]) if bias is not None else None
         pad4 = lambda t: None if t is None else torch.nn.functional.pad(t, (0, Cop - Co))   # noqa: E731 (a copy)
         op = conv2d(xp, wp.reshape(Cop, k * k * Cp), bias=bp, k=k, stride=stride, pad=pad, relu_in=relu_in, act=act,
                     res=pad4(res), res2=pad4(res2), out_hw=(OH, OW))

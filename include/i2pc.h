@@ -366,6 +366,8 @@ int i2pc_gemm_set_engine(int mode);
  *   "gemm_splitk" 1 = split-K for few-tile long-K calls given a workspace (i2pc_gemm_ws); the one
  *                 knob that changes results: the fp32 partial sums are added in another order
  *                 (within the network parity tolerance, tests/test_gemm_engines_gpu.py)
+ *   "gemm_split_tile" split-K slice tile: 0 = 256 x 256 x 64 (default), 1 = 128 x 128 x 32
+ *   "gemm_tile192" 1 = 384 x 192 tiles for N % 192 == 0 calls that fit one round
  *   "unp_rows"    1 = the row-sweep unprojection kernel
  *   "unp_nt"      1 = non-temporal point stores
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
@@ -380,9 +382,12 @@ int i2pc_gemm_set_engine(int mode);
  *                 workgroup per window: -1 = automatic (from 2 M pixels; default), 0 = off, 1 = on
  *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
- * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _UNP_ROWS / _UNP_NT / _UNP_RPT /
- * _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR environment variables, else 1, 1, 1, 1, 1, 8, 1, 1, 1.  A
- * HIP graph keeps the kernels it captured: re-capture after changing a knob. */
+ *   "ln_f2"       1 = the register-resident LayerNorm for dim 384 (k_layernorm2)
+ * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _GEMM_SPLIT_TILE / _GEMM_TILE192 /
+ * _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR environment variables, else
+ * 1, 1, 1, 0, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
+ * the kernels it captured: re-capture after changing a knob.  An unknown name fails with I2PC_EINVAL
+ * and an error message listing every knob. */
 int i2pc_set_tuning(const char* name, int value);
 
 /* LayerNorm over the last dim: x fp32 [rows][dim] (row stride ldx) -> y bf16 [rows][dim]

@@ -97,15 +97,23 @@ def test_ln_fold_producer_plans():
 
 
 def test_tuning_knob_names():
-    """Every knob include/i2pc.h documents is accepted by i2pc_set_tuning (host-side state only, no
-    device work); an unknown name is an error (I2PCError)."""
+    """Every knob include/i2pc.h documents (ops.TUNING_KNOBS) is accepted by i2pc_set_tuning
+    (host-side state only, no device work), the header and the unknown-knob error message list the
+    same names, and an unknown name is an error (I2PCError)."""
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libi2pc.so not built")
     from image_to_pointcloud_amd import ops
-    defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "unp_rows": 1, "unp_nt": 1, "unp_rpt": 8,
-                "sel_windows": 1, "sel_parts": 0, "sel_rows": 16, "sel_lband": -1, "attn_lazy": 1,
-                "attn_scalar": 1, "ln_f2": 1}
+    defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "gemm_split_tile": 0, "gemm_tile192": 1,
+                "unp_rows": 1, "unp_nt": 1, "unp_rpt": 8, "sel_windows": 1, "sel_parts": 0, "sel_rows": 16,
+                "sel_lband": -1, "attn_lazy": 1, "attn_scalar": 1, "ln_f2": 1}
+    assert set(defaults) == set(ops.TUNING_KNOBS)
+    header = open(os.path.join(os.path.dirname(__file__), "..", "include", "i2pc.h")).read()
+    for name in ops.TUNING_KNOBS:
+        assert f'"{name}"' in header, name
     for name, v in defaults.items():
         ops.set_tuning(name, v)
-    with pytest.raises(_lib.I2PCError):
+    with pytest.raises(_lib.I2PCError) as ei:
         ops.set_tuning("no_such_knob", 1)
+    msg = str(ei.value)
+    for name in ops.TUNING_KNOBS:
+        assert name in msg, name

@@ -56,6 +56,39 @@ def test_rest_job_matches_reference(pipeline_case, monkeypatch, tmp_path):
     assert hashlib.sha256(dl.content).hexdigest() == exp["xyz_sha256"]
 
 
+class _RecordingJob(dict):
+    """A job record that logs every (progress, message) its pipeline publishes."""
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.log = []
+
+    def update(self, *a, **k):
+        super().update(*a, **k)
+        if "progress" in k or "message" in k:
+            self.log.append((self.get("progress"), self.get("message")))
+
+
+def test_job_progress_sequence_matches_reference(pipeline_case, monkeypatch, tmp_path):
+    """A polling frontend sees the reference's status sequence: 10 / 20 / 40 / 60 / 80 / 100 with the
+    messages of app.py:423-424, 429-430, 457-458, 465-466, 492-493 and 542-544."""
+    from PIL import Image
+    from image_to_pointcloud_amd import app_api
+    monkeypatch.chdir(tmp_path)
+    depth = torch.from_numpy(pipeline_case["depth"]).cuda()
+    monkeypatch.setattr(app_api, "load_model", lambda name: {"type": "depth"})
+    monkeypatch.setattr(app_api, "_depth_device", lambda img, mi: depth)
+    monkeypatch.setattr(app_api, "REFINE_POINT_CLOUD", False)
+    buf = io.BytesIO()
+    Image.fromarray(pipeline_case["image"][:, :, ::-1]).save(buf, format="PNG")
+    job = _RecordingJob(status="pending", progress=0, message="Job queued")
+    req = app_api.ProcessingRequest(point_density="high", output_format="xyz")
+    app_api.process_image_pipeline("job0", buf.getvalue(), req, jobs={"job0": job})
+    assert job["status"] == "completed", job["message"]
+    assert job.log == [(10, "Loading AI model..."), (20, "Processing image..."),
+                       (40, "Estimating depth with AI..."), (60, "Generating 3D point cloud..."),
+                       (80, "Saving point cloud..."), (100, "Processing complete!")]
+
+
 def test_load_model_and_depth_shapes():
     from image_to_pointcloud_amd import app_api
     mi = app_api.load_model("depth-anything-v2")

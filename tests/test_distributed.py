@@ -150,6 +150,11 @@ def _overlap_worker(rank, ws, port, q):
         og.finish()
         gx, gr = og.gathered(4 & 1)
         seen.append((4, gx[:, 0, 0].tolist(), gr[:, 0, 0].tolist()))
+        # bench.py's multi-GPU diagnostics: bytes per step and the measured wait (host clock on CPU)
+        assert og.recv_bytes_per_step == (ws - 1) * B * N * 15 and og.send_bytes_per_step == B * N * 15
+        assert og.world == ws and og.gather_wait_ms() >= 0.0
+        og.reset_stats()
+        assert og.gather_wait_ms() == 0.0
         q.put((rank, seen))
     finally:
         dist.destroy_process_group()

@@ -95,6 +95,16 @@ def test_bench_gpus_2_launches_two_ranks():
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 4
     assert "all-gather" in rec["config"]["workload"]
     assert rec["value"] > 0
+    # the per-rank diagnostics of the multi-GPU line
+    mg = rec["multi_gpu"]
+    assert mg["world"] == 2 and mg["backend"] == "gloo" and mg["rccl_world_size"] is None and mg["all_gather"]
+    pts = 512 * 512
+    assert mg["gathered_bytes_per_step_per_rank"] == 1 * 2 * pts * 15
+    assert mg["sent_bytes_per_step_per_rank"] == 2 * pts * 15
+    assert [r["rank"] for r in mg["per_rank"]] == [0, 1]
+    for r in mg["per_rank"]:
+        assert r["step_ms"] > 0 and r["compute_ms"] > 0 and r["gather_wait_ms"] > 0   # gloo stages synchronously
+        assert r["gather_wait_ms"] < r["step_ms"]
     # a launcher world that disagrees with --gpus is an error, not a silent 1-GPU number
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,

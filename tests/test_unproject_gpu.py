@@ -506,6 +506,12 @@ def _sel_cases():
     d = d.copy(); d[4, 9] = np.nan
     out["near_constant_nan"] = d
     out["all_nan"] = np.full_like(base, np.nan)
+    # the nanmedian's middle pair near FLT_MAX: np.mean of them in float32 overflows to +inf, so the
+    # ranks above the median no longer read max(F(r - k), med) -- the window paths must not drop
+    # F(r) there (fill_targets / finish_targets)
+    d = base.copy(); idx = rng.permutation(d.size)
+    d.ravel()[idx[:d.size * 9 // 10]] = np.float32(3.0e38); d.ravel()[idx[-3:]] = np.nan
+    out["huge_median_nan"] = d
     return out
 
 
