@@ -91,6 +91,8 @@ struct Args {
   float* lnp; bf16_t* cbf; int64_t ldcb;
   const float* lnsh;
   int lnc;
+  int dbg_drop;   // diagnostic (I2PC_GEMM_DROP_STORES=1): the persistent engine's output stores are issued to an
+                  // empty buffer range (dropped), to measure what the stores cost the next tile's K-loop
 };
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
@@ -592,7 +594,7 @@ namespace pers {
 
 using namespace ::i2pc::mx;
 
-enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4, EPI_Q8 = 5, EPI_LNF = 6 };
+enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4, EPI_Q8 = 5, EPI_LNF = 6, EPI_LNP = 7 };
 constexpr int OOB = 0x7FFFFFF0;   // buffer range; offsets >= OOB are dropped / read as 0
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -664,8 +666,9 @@ __device__ __forceinline__ int out_elem(const Args& p, int m, int n, int64_t ld,
   } while (0)
 
 template <int EPI> struct EpiCount {
-  static constexpr int loads = EPI == EPI_RESF32 || EPI == EPI_RESBF16 ? 4 : EPI == EPI_RES2 ? 8 : 0;
-  static constexpr int stores = EPI == EPI_RESF32 ? 4 : EPI == EPI_Q8 ? 5 : 2;
+  static constexpr int loads = EPI == EPI_RESF32 || EPI == EPI_RESBF16 || EPI == EPI_LNP ? 4 : EPI == EPI_RES2 ? 8 : 0;
+  // EPI_LNP: 4 fp32 rows + 2 bf16 (shifted copy) + 1 chunk-partials store per m-subtile
+  static constexpr int stores = EPI == EPI_RESF32 ? 4 : EPI == EPI_Q8 ? 5 : EPI == EPI_LNP ? 7 : 2;
 };
 
 // Register-direct tile epilogue of the persistent engines for one wave: rows mw0 + i*16 + (lane & 15),
@@ -678,6 +681,7 @@ template <int RM, int RN, int EPI, bool F8>
 __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], int mw0, int ncol, const float* bias_lds,
                                            rsrc_t c_rs, rsrc_t r_rs, rsrc_t r2_rs, rsrc_t cs_rs,
                                            const float* csum_lds = nullptr, const float* rows_lds = nullptr) {
+    static_assert(EPI != EPI_LNP || RN == 4, "EPI_LNP: a wave's 64 columns are one LayerNorm chunk (or two of 32)");
     constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
     static_assert(RN == 2 || RN == 4, "RN");
     const int lane = threadIdx.x & 63;
@@ -701,7 +705,7 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int n = ncol + j * 16 + fq * 4;
-        if constexpr (EPI == EPI_RESF32) {
+        if constexpr (EPI == EPI_RESF32 || EPI == EPI_LNP) {
           const int off = m < p.M ? (remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldr + n) * 4 : OOB;
           asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(rf[slot][j]) : "v"(off), "s"(r_rs) : "memory");
         }
@@ -725,7 +729,7 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
       if constexpr (NRL > 0) {
         if constexpr (i + 1 < RM) load_res(i + 1, slot ^ 1);
         constexpr int after = (i + 1 < RM ? NRL * RN / 4 : 0) + (i > 0 ? NS : 0);
-        if constexpr (EPI == EPI_RESF32) {
+        if constexpr (EPI == EPI_RESF32 || EPI == EPI_LNP) {
           if constexpr (RN == 4)
             asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rf[slot][0]), "+v"(rf[slot][1]), "+v"(rf[slot][2]), "+v"(rf[slot][3])
                          : "i"(after) : "memory");
@@ -779,7 +783,7 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[j][e] = act_f<ACT>(t[e]);
-        if constexpr (EPI == EPI_RESF32) {
+        if constexpr (EPI == EPI_RESF32 || EPI == EPI_LNP) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[j][e] += rf[slot][j][e];
         }
@@ -822,6 +826,82 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
         const int soff = (ok && fq == 0) ? remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldcs * 4 + ncol / 32 : OOB;
         if constexpr (NB == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)sbytes, cs_rs, soff, 0, 0);
         else __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sbytes, cs_rs, soff, 0, 0);
+      } else if constexpr (EPI == EPI_LNP) {
+        // LayerNorm-fold producer (the tile kernel's tile_epilogue, same values bit for bit): the fp32
+        // output, a bf16 copy of u = out - shift[m], and per 64 (or 32) columns (mean, M2) of u summed
+        // in the tile kernel's order -- there a lane holds 8 consecutive columns of a row and the chunk
+        // is reduced over lane groups by xor 1, 2, 4; here a lane holds 4 columns of each 16-column
+        // group j, so 8-column group g = 2 j + (fq >> 1) is split over lanes fq = 2 h, 2 h + 1 (lane
+        // xor 16), g ^ 1 is lane xor 32, g ^ 2 is j ^ 1 and g ^ 4 is j ^ 2 (fp32 addition commutes).
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const int off = ok ? out_elem(p, m, ncol + j * 16 + fq * 4, p.ldc, false) * 4 : OOB;
+          const u32x4 d = {__float_as_uint(v[j][0]), __float_as_uint(v[j][1]), __float_as_uint(v[j][2]),
+                           __float_as_uint(v[j][3])};
+          __builtin_amdgcn_raw_buffer_store_b128(d, c_rs, off, 0, 0);
+        }
+        const float sh = rows_lds[i * 16 + frow];
+        float u[RN][4];
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[j][e] = v[j][e] - sh;
+#pragma unroll
+        for (int pp = 0; pp < RN / 2; ++pp) {
+          uint32_t x0 = pack_bf16(u[2 * pp][0], u[2 * pp][1]), x1 = pack_bf16(u[2 * pp][2], u[2 * pp][3]);
+          uint32_t y0 = pack_bf16(u[2 * pp + 1][0], u[2 * pp + 1][1]), y1 = pack_bf16(u[2 * pp + 1][2], u[2 * pp + 1][3]);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+          const int n = ncol + 32 * pp + (fq & 1) * 16 + (fq >> 1) * 8;
+          const int off = ok ? (m * (int)p.ldcb + n) * 2 : OOB;
+          const u32x4 d = {s0[0], s1[0], s0[1], s1[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(d, r2_rs, off, 0, 0);
+        }
+        const bool c64 = p.lnc == 64;
+        float sm[RN], mean[RN], q[RN];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const float a = (u[j][0] + u[j][1]) + (u[j][2] + u[j][3]);
+          sm[j] = a + __shfl_xor(a, 16);             // the 8-column group
+          sm[j] += __shfl_xor(sm[j], 32);            // + group g ^ 1
+        }
+        {
+          float t2[RN];
+#pragma unroll
+          for (int j = 0; j < RN; ++j) t2[j] = sm[j] + sm[j ^ 1];               // + g ^ 2
+#pragma unroll
+          for (int j = 0; j < RN; ++j) mean[j] = c64 ? (t2[j] + t2[j ^ 2]) * (1.0f / 64.0f) : t2[j] * (1.0f / 32.0f);
+        }
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          // the tile kernel's sequential fma chain over the group's 8 columns: the low 4 (lane fq even)
+          // first, continued by the high 4 (lane fq odd) from the low lane's partial
+          float x = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x = __builtin_fmaf(u[j][e] - mean[j], u[j][e] - mean[j], x);
+          float y = __shfl_xor(x, 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y = __builtin_fmaf(u[j][e] - mean[j], u[j][e] - mean[j], y);
+          const float w = __shfl_xor(y, 16);
+          q[j] = (fq & 1) ? y : w;
+          q[j] += __shfl_xor(q[j], 32);
+        }
+        {
+          float t2[RN];
+#pragma unroll
+          for (int j = 0; j < RN; ++j) t2[j] = q[j] + q[j ^ 1];
+#pragma unroll
+          for (int j = 0; j < RN; ++j) q[j] = c64 ? t2[j] + t2[j ^ 2] : t2[j];
+        }
+        if (c64) {
+          const int off = (ok && fq == 0) ? (m * (p.N >> 6) + (ncol >> 6)) * 8 : OOB;
+          const u32x2 d = {__float_as_uint(mean[0]), __float_as_uint(q[0])};
+          __builtin_amdgcn_raw_buffer_store_b64(d, cs_rs, off, 0, 0);
+        } else {
+          const int off = (ok && fq == 0) ? (m * (p.N >> 5) + (ncol >> 5)) * 8 : OOB;
+          const u32x4 d = {__float_as_uint(mean[0]), __float_as_uint(q[0]), __float_as_uint(mean[2]), __float_as_uint(q[2])};
+          __builtin_amdgcn_raw_buffer_store_b128(d, cs_rs, off, 0, 0);
+        }
       } else if constexpr (OUTF) {
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
@@ -871,17 +951,23 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   constexpr int ROWB = 128, RPI = 8;
   constexpr int ESZ = F8 ? 1 : 2;          // operand bytes
   constexpr int KSTEP = ROWB / ESZ;        // k per LDS stage
-  constexpr int A_LOADS = BM / 64, W_LOADS = BN / 64;
+  // A: BM / 8 slabs of 8 rows (one glds wave-instruction each), slab w + 8 j to wave w (BM = 160:
+  // waves 0-3 load three, waves 4-7 two); W: BN / 64 slabs per wave
+  constexpr int A_SLABS = BM / RPI;
+  constexpr int A_LOADS = (A_SLABS + 7) / 8, W_LOADS = BN / 64;
   constexpr int A_BYTES = BM * ROWB, W_BYTES = BN * ROWB;
   constexpr int SC_BYTES = F8 ? (BM + BN) * 4 : 0;
   constexpr int STAGE = A_BYTES + W_BYTES + SC_BYTES;
   constexpr int BIAS_OFF = 2 * STAGE;
   constexpr int CSUM_OFF = BIAS_OFF + 2048;          // EPI_LNF: column sums [2][1 KB], row scales [2][BM * 8]
   constexpr int ROWS_OFF = CSUM_OFF + 2048;
+  constexpr int SHIFT_OFF = BIAS_OFF + 2048;         // EPI_LNP: row shifts [2][1 KB] (BM <= 256 floats)
   constexpr int NRL = EpiCount<EPI>::loads * RN / 4, NS = EpiCount<EPI>::stores;
   constexpr int E_ALL = RM * (NRL + NS);
-  static_assert(BM == 256 || BM == 320, "BM");
-  static_assert(EPI != EPI_LNF || (BM == 256 && !F8 && !CONV), "EPI_LNF: dense bf16 A, BM 256");
+  static_assert(BM == 256 || BM == 320 || BM == 160, "BM");
+  static_assert(BM % 64 == 0 || (!F8 && !CONV), "BM = 160: dense bf16 A");
+  static_assert(EPI != EPI_LNF || ((BM == 256 || BM == 160) && !F8 && !CONV), "EPI_LNF: dense bf16 A, BM 256 or 160");
+  static_assert(EPI != EPI_LNP || (BN == 256 && BM <= 256 && !F8 && !CONV), "EPI_LNP: dense bf16 A, BN 256");
   static_assert(BN == 256 || BN == 128, "BN");
   static_assert(!F8 || BM == 256, "fp8 engine: BM 256 (scale loads: one wave per 64 rows)");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -906,9 +992,9 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   const rsrc_t as_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p.As), 0, F8 ? p.as_bytes : 0, 0x00020000);
   const rsrc_t ws_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p.Ws), 0, F8 ? p.ws_bytes : 0, 0x00020000);
   const int chunk16 = (pchunk ^ lrow) << 4;           // swizzled 16-B chunk (row & 7 == lrow)
-  const int a_row0 = wid * A_LOADS * RPI + lrow;      // + j * RPI
+  const int a_row0 = wid * RPI + lrow;                // + j * 64 (slab wid + 8 j)
   const int w_row0 = wid * W_LOADS * RPI + lrow;
-  const int a_sstep = RPI * (int)p.lda * ESZ, w_sstep = RPI * (int)p.ldw * ESZ;
+  const int a_sstep = 64 * (int)p.lda * ESZ, w_sstep = RPI * (int)p.ldw * ESZ;
   // fp8 scale rows: waves 0..BM/64-1 load A rows 64 w + lane, waves 4..4+BN/64-1 W rows
   const bool sc_a = F8 && wid < BM / 64;
   const bool sc_w = F8 && wid >= 4 && wid < 4 + BN / 64;
@@ -939,7 +1025,7 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
       a_off = (uint32_t)(nm0 + a_row0) * (uint32_t)(p.lda * ESZ) + chunk16;
     } else {
 #pragma unroll
-      for (int j = 0; j < A_LOADS; ++j) conv_row(nm0 + a_row0 + j * RPI, cpix[j], cyx[j]);
+      for (int j = 0; j < A_LOADS; ++j) conv_row(nm0 + a_row0 + j * 64, cpix[j], cyx[j]);
     }
     w_off = (uint32_t)(nn0 + w_row0) * (uint32_t)(p.ldw * ESZ) + chunk16;
     if constexpr (F8) {
@@ -958,6 +1044,8 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
                                                             0x00020000);
   const rsrc_t lr_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.lnr), 0, EPI == EPI_LNF ? p.M * 8 : 0,
                                                          0x00020000);
+  const rsrc_t sh_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.lnsh), 0,
+                                                         EPI == EPI_LNP && p.lnsh ? p.M * 4 : 0, 0x00020000);
   auto stage = [&](int buf, int k0, int bias_par) {
     uint8_t* sA = smem + buf * STAGE;
     uint8_t* sW = sA + A_BYTES;
@@ -970,9 +1058,15 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
       if (bias_par >= 0 && wid == 1 && lane < BN / 4)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(cs_rs_ln, (lds_ptr_t)(smem + CSUM_OFF + bias_par * 1024), 16,
                                                   (nn0 + lane * 4) * 4, 0, 0, 0);
-      if (bias_par >= 0 && (wid == 2 || wid == 3))
+      if (bias_par >= 0 && (wid == 2 || (wid == 3 && lane < (BM - 128) / 2)))
         __builtin_amdgcn_raw_ptr_buffer_load_lds(lr_rs, (lds_ptr_t)(smem + ROWS_OFF + bias_par * BM * 8 + (wid - 2) * 1024),
                                                   16, (nm0 + (wid - 2) * 128 + lane * 2) * 8, 0, 0, 0);
+    }
+    if constexpr (EPI == EPI_LNP) {
+      // the tile's BM row shifts (wave 1; rows past M and a NULL shift read as zero)
+      if (bias_par >= 0 && wid == 1 && lane < BM / 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(sh_rs, (lds_ptr_t)(smem + SHIFT_OFF + bias_par * 1024), 16,
+                                                  (nm0 + lane * 4) * 4, 0, 0, 0);
     }
     int kk = 0, ky = 0, kx = 0, ci0 = 0;
     if constexpr (CONV) {
@@ -984,15 +1078,16 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     if constexpr (!CONV) {
 #pragma unroll
       for (int j = 0; j < A_LOADS; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid * A_LOADS + j) * RPI * ROWB), 16,
-                                                  a_off + j * a_sstep, k0 * ESZ, 0, 0);   // row part in voffset: range-checked
+        if (A_SLABS % 8 == 0 || wid + 8 * j < A_SLABS)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid + 8 * j) * RPI * ROWB), 16,
+                                                    a_off + j * a_sstep, k0 * ESZ, 0, 0);   // row part in voffset: range-checked
     } else {
 #pragma unroll
       for (int j = 0; j < A_LOADS; ++j) {
         const int yi = (cyx[j] >> 16) + ky, xi = ((int)(short)(cyx[j] & 0xffff)) + kx;
         const bool ok = (unsigned)yi < (unsigned)p.ch && (unsigned)xi < (unsigned)p.cw;
         const int off = ok ? ((cpix[j] + yi * p.cw + xi) * p.cc + ci0) * ESZ + chunk16 : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid * A_LOADS + j) * RPI * ROWB), 16, off, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sA + (wid + 8 * j) * RPI * ROWB), 16, off, 0, 0, 0);
       }
     }
 #pragma unroll
@@ -1017,10 +1112,11 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     }
   };
 
-  const rsrc_t c_rs = make_rsrc(p.C);
+  const rsrc_t c_rs = p.dbg_drop ? __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0, 0x00020000) : make_rsrc(p.C);
   const rsrc_t r_rs = make_rsrc(p.res);
-  const rsrc_t r2_rs = make_rsrc(p.res2);
-  const rsrc_t cs_rs = make_rsrc(p.Cs);
+  // EPI_LNP: the bf16 copy and the chunk partials take the second-residual / fp8-scale slots
+  const rsrc_t r2_rs = make_rsrc(EPI == EPI_LNP ? static_cast<const void*>(p.cbf) : static_cast<const void*>(p.res2));
+  const rsrc_t cs_rs = make_rsrc(EPI == EPI_LNP ? static_cast<const void*>(p.lnp) : static_cast<const void*>(p.Cs));
   const int nk = p.K / KSTEP;
 
   setup(t);
@@ -1135,7 +1231,8 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     epilogue_p<RM, RN, EPI, F8>(p, acc, m0 + wm * TM, n0 + wn * (BN / 4),
                                 reinterpret_cast<const float*>(smem + BIAS_OFF + tpar * 1024) + wn * (BN / 4), c_rs, r_rs,
                                 r2_rs, cs_rs, reinterpret_cast<const float*>(smem + CSUM_OFF + tpar * 1024) + wn * (BN / 4),
-                                reinterpret_cast<const float*>(smem + ROWS_OFF + tpar * BM * 8) + wm * TM * 2);
+                                EPI == EPI_LNP ? reinterpret_cast<const float*>(smem + SHIFT_OFF + tpar * 1024) + wm * TM
+                                               : reinterpret_cast<const float*>(smem + ROWS_OFF + tpar * BM * 8) + wm * TM * 2);
     PSTAMP(tord, 3);
     ++tord;
     if (!has_next) break;
@@ -1256,7 +1353,7 @@ __global__ __launch_bounds__(512) void k_gemm_q(Args p) {
     return *reinterpret_cast<const bf16x8*>(base + (((4 * s + fq) ^ (row & 7)) << 4));
   };
 
-  const rsrc_t c_rs = make_rsrc(p.C);
+  const rsrc_t c_rs = p.dbg_drop ? __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0, 0x00020000) : make_rsrc(p.C);
   const rsrc_t r_rs = make_rsrc(p.res);
   const rsrc_t r2_rs = make_rsrc(p.res2);
   const int nk = p.K / BK;
@@ -1490,7 +1587,7 @@ __global__ __launch_bounds__(512) void k_gemm_8p(Args p) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  const rsrc_t c_rs = make_rsrc(p.C);
+  const rsrc_t c_rs = p.dbg_drop ? __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0, 0x00020000) : make_rsrc(p.C);
   const rsrc_t r_rs = make_rsrc(p.res);
   const rsrc_t r2_rs = make_rsrc(p.res2);
   const int nk = p.K / BK;   // >= 2 (plan)
@@ -1636,13 +1733,16 @@ static void launch_p(const Args& p, hipStream_t s) {
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = p.N / BN;
   q.group_m = group_m_for(q.tiles_m);
-  const int smem = 2 * ((BM + BN) * 128 + (F8 ? (BM + BN) * 4 : 0)) + 2048 + (EPI == pers::EPI_LNF ? 2048 + 2 * BM * 8 : 0);
+  const int smem = 2 * ((BM + BN) * 128 + (F8 ? (BM + BN) * 4 : 0)) + 2048 + (EPI == pers::EPI_LNF ? 2048 + 2 * BM * 8 : 0) +
+                   (EPI == pers::EPI_LNP ? 2048 : 0);
   auto kern = pers::k_gemm_p<BM, CONV, RELU_A, EPI, BN, F8>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
+  static const int drop = [] { const char* e = getenv("I2PC_GEMM_DROP_STORES"); return e ? atoi(e) : 0; }();
+  q.dbg_drop = drop;
   const int tiles = q.tiles_m * q.tiles_n;
   const int grid = std::min(tiles, num_cus());
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
@@ -1722,6 +1822,12 @@ static thread_local int g_splitk = [] { const char* e = getenv("I2PC_GEMM_SPLITK
 // 384 x 192 tiles for N % 192 == 0 calls that fit one round (I2PC_GEMM_TILE192 / "gemm_tile192")
 static thread_local int g_tile192 = [] { const char* e = getenv("I2PC_GEMM_TILE192"); return e ? atoi(e) : 1; }();
 static thread_local int g_split_tile = [] { const char* e = getenv("I2PC_GEMM_SPLIT_TILE"); return e ? atoi(e) : 0; }();
+// LayerNorm-fold producers (attention-out / FC2 with an fp32 residual) on the persistent engine's EPI_LNP
+// with 160 x 256 tiles where they fit (I2PC_GEMM_LNP_P / "gemm_lnp_p"; 0 = the tile kernel's epilogue)
+// (measured r04, tools/epi_cost.py: O 70.6 vs 66.6 us, FC2 195.9 vs 173.3 us against the tile kernel's one round of
+// 320 x 256 -- a 160-row K-step costs 0.79 of a 256-row one for 0.625 of its MFMAs, and the register-direct
+// producer epilogue's shuffle tree is slower than the tile kernel's LDS-staged one; off by default)
+static thread_local int g_lnp_p = [] { const char* e = getenv("I2PC_GEMM_LNP_P"); return e ? atoi(e) : 0; }();
 
 static int64_t max_row(const Args& p) {
   const int64_t m = p.M - 1;
@@ -1742,6 +1848,29 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
                     p.a_g == 0 && (int64_t)(p.M + 320) * p.lda * 2 < pers::OOB && (int64_t)p.N * p.ldw * 2 < pers::OOB &&
                     (max_row(p) * p.ldc + p.N) * 2 < pers::OOB;
     return ok ? Plan{1, 256, pbn, pers::EPI_LNF} : Plan{-2, 0, 0, 0};
+  }
+  if (p.lnp && g_lnp_p && force == 0 && pforce != 1) {
+    // LayerNorm-fold producer on the persistent engine (EPI_LNP): a wave's 64 columns are one chunk
+    // (or two of 32), fp32 output with the fp32 residual, linear rows.  160-row tiles where they
+    // take fewer row-rounds than 256 (DPT-Large O / FC2, M 18464, N 1024: 464 tiles = 2 per CU of
+    // 160 rows, the tile kernel's one round of 320 rows, but with the first tile's epilogue and the
+    // second's first stage overlapped)
+    const bool ok = p.N % 256 == 0 && !conv && !relu && !p.rbias && !p.tbl && p.res && p.res_f32 && p.c_f32 && !p.res2 &&
+                    p.ct_s == 0 && p.a_g == 0 && p.o_g == 0 && p.o_o == 0 &&
+                    (int64_t)(p.M + 320) * p.lda * 2 < pers::OOB && (int64_t)p.N * p.ldw * 2 < pers::OOB &&
+                    (max_row(p) * p.ldc + p.N) * 4 < pers::OOB && (max_row(p) * p.ldr + p.N) * 4 < pers::OOB &&
+                    ((int64_t)p.M * p.ldcb + p.N) * 2 < pers::OOB && (int64_t)p.M * (p.N / p.lnc) * 8 < pers::OOB;
+    if (ok) {
+      const int64_t ncu = num_cus();
+      int best = 160;
+      int64_t best_cost = -1;
+      for (int bm : {160, 256}) {
+        const int64_t tiles = (int64_t)((p.M + bm - 1) / bm) * (p.N / 256);
+        const int64_t cost = (tiles + ncu - 1) / ncu * bm;
+        if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = bm; }
+      }
+      return Plan{1, best, 256, pers::EPI_LNP};
+    }
   }
   if (pbn && !p.rbias && !p.tbl && !p.lnp && force == 0 && pforce != 1) {
     const bool ct = p.ct_s > 0;
@@ -1930,6 +2059,11 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
     return set_error(I2PC_EUNSUPPORTED, "gemm: no persistent BN=128 variant with ReLU on A");
   }
   if constexpr (!CONV && !RELU_A) {
+    if (pl.epi == EPI_LNP) {
+      if (pl.bm == 160) launch_p<160, false, false, EPI_LNP>(p, s);
+      else launch_p<256, false, false, EPI_LNP>(p, s);
+      return check_launch("gemm (LN producer)");
+    }
     if (pl.epi == EPI_LNF) launch_p<256, false, false, EPI_LNF>(p, s);
     else if (pl.epi == EPI_PLAIN) launch_p<256, false, false, EPI_PLAIN>(p, s);
     else if (pl.epi == EPI_RESF32) launch_p<256, false, false, EPI_RESF32>(p, s);
@@ -1954,7 +2088,11 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
 // would (same per-output accumulation order).  I2PC_GEMM_TAIL=0 disables it.
 // (Measured and dropped: FC1's remainder, M = 18464, N = 4096, as one round of the tile kernel's
 // 192 x 256 tiles instead of a fifth persistent round -- no gain end to end.)
-// Returns 0 (no split) or 1 (BN = 128 persistent remainder).
+// When 256 x 128 tiles do not fit one round, 160 x 256 tiles may: DPT-Large's FC1 (M 18464, N 4096,
+// 4.56 rounds of 256^2) keeps 4 rounds and runs its last 2080 rows as 13 x 16 = 208 tiles of 160 rows
+// (r04; a 160-row K-step costs ~0.79 of a 256-row one, tools/stamps_p.py) instead of a fifth round.
+// Returns 0 (no split), 1 (BN = 128 persistent remainder) or 2 (BM = 160 remainder).
+static thread_local int g_tail160 = [] { const char* e = getenv("I2PC_GEMM_TAIL160"); return e ? atoi(e) : 1; }();
 static int tail_split(const Args& p, int& ma) {
   if (!g_tail || p.o_g != 0 || p.a_g != 0 || p.ct_s > 0 || p.N % 256 != 0) return 0;
   const int64_t tn = p.N / 256, tm = (p.M + 255) / 256, T = tm * tn, G = num_cus();
@@ -1966,7 +2104,9 @@ static int tail_split(const Args& p, int& ma) {
   if (mt >= tm) return 0;
   ma = (int)(mt * 256);
   const int64_t half_tiles = (tm - mt) * 2 * tn;
-  return half_tiles <= G ? 1 : 0;
+  if (half_tiles <= G) return 1;
+  const int64_t t160 = (p.M - ma + 159) / 160 * tn;
+  return g_tail160 && t160 <= G ? 2 : 0;
 }
 
 template <bool CONV, bool RELU_A>
@@ -1985,12 +2125,14 @@ static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
       if (lnf) {
         pb.lnr = p.lnr + (int64_t)ma * 2;      // row scales follow the rows
         launch_p<256, false, false, pers::EPI_LNF>(pa, s);
-        launch_p<256, false, false, pers::EPI_LNF, 128>(pb, s);
+        if (ts == 2) launch_p<160, false, false, pers::EPI_LNF>(pb, s);
+        else launch_p<256, false, false, pers::EPI_LNF, 128>(pb, s);
         return check_launch("gemm (tail split)");
       }
       if (pl.kind == 2) launch_8p<pers::EPI_PLAIN>(pa, s);
       else launch_p<256, false, false, pers::EPI_PLAIN>(pa, s);
-      launch_p<256, false, false, pers::EPI_PLAIN, 128>(pb, s);
+      if (ts == 2) launch_p<160, false, false, pers::EPI_PLAIN>(pb, s);
+      else launch_p<256, false, false, pers::EPI_PLAIN, 128>(pb, s);
       return check_launch("gemm (tail split)");
     }
   }
@@ -2030,7 +2172,7 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu, const SplitPl
   if (pl.kind == 2) {
     snprintf(buf, sizeof buf, "k_gemm_8p<%s>", pl.epi == pers::EPI_PLAIN ? "plain" : "res_f32");
   } else if (pl.kind == 1) {
-    static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8", "ln_fold"};
+    static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8", "ln_fold", "ln_prod"};
     if (g_quarter && pl.epi != pers::EPI_CT) snprintf(buf, sizeof buf, "k_gemm_q<%s, %s, %s>", c, r, epis[pl.epi]);
     else if (pl.bn == 128) snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s, 128>", pl.bm, c, r, epis[pl.epi]);
     else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
@@ -2253,12 +2395,14 @@ extern "C" int i2pc_gemm_set_engine(int mode) {
 }
 
 // per-host-thread tuning knobs (i2pc_set_tuning; thread_local above): gemm_tail, gemm_bn128,
-// gemm_splitk, gemm_split_tile, gemm_tile192
+// gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_tail160
 bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
   if (std::strcmp(name, "gemm_splitk") == 0) { i2pc::gemm::g_splitk = value; return true; }
   if (std::strcmp(name, "gemm_split_tile") == 0) { i2pc::gemm::g_split_tile = value; return true; }
   if (std::strcmp(name, "gemm_tile192") == 0) { i2pc::gemm::g_tile192 = value; return true; }
+  if (std::strcmp(name, "gemm_lnp_p") == 0) { i2pc::gemm::g_lnp_p = value; return true; }
+  if (std::strcmp(name, "gemm_tail160") == 0) { i2pc::gemm::g_tail160 = value; return true; }
   return false;
 }

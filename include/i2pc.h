@@ -368,6 +368,10 @@ int i2pc_gemm_set_engine(int mode);
  *                 (within the network parity tolerance, tests/test_gemm_engines_gpu.py)
  *   "gemm_split_tile" split-K slice tile: 0 = 256 x 256 x 64 (default), 1 = 128 x 128 x 32
  *   "gemm_tile192" 1 = 384 x 192 tiles for N % 192 == 0 calls that fit one round
+ *   "gemm_lnp_p"  1 = LayerNorm-fold producers (ln_part) on the persistent engine (160 x 256 or
+ *                 256 x 256 tiles, N % 256 == 0), 0 = on the tile kernel (default: measured faster)
+ *   "gemm_tail160" 1 = a persistent GEMM's last partial round as 160 x 256 tiles where 256 x 128
+ *                 tiles do not fit one round (DPT-Large FC1)
  *   "unp_rows"    1 = the row-sweep unprojection kernel
  *   "unp_nt"      1 = non-temporal point stores
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
@@ -384,8 +388,8 @@ int i2pc_gemm_set_engine(int mode);
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  *   "ln_f2"       1 = the register-resident LayerNorm for dim 384 (k_layernorm2)
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _GEMM_SPLIT_TILE / _GEMM_TILE192 /
- * _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR environment variables, else
- * 1, 1, 1, 0, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
+ * _GEMM_LNP_P / _GEMM_TAIL160 / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR
+ * environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
  * the kernels it captured: re-capture after changing a knob.  An unknown name fails with I2PC_EINVAL
  * and an error message listing every knob. */
 int i2pc_set_tuning(const char* name, int value);

@@ -281,3 +281,31 @@ def test_tile_384x192_bitexact(M, N, K, res):
     y = h.float() @ w.float().T + b
     y = x0 + y if res else F.gelu(y)
     assert _fro(got, y) <= 8e-3
+
+
+@pytest.mark.parametrize("lnf", [False, True])
+@pytest.mark.parametrize("M,N", [(18464, 4096), (6500, 4096)])
+def test_tail160_bitexact(M, N, lnf):
+    """A persistent GEMM whose last partial round runs as 160 x 256 tiles (knob gemm_tail160; DPT-Large
+    FC1: 4 rounds of 256^2 + 13 x 16 tiles of 160 rows) computes every output exactly as the
+    un-split launch: plain GELU epilogue and the LayerNorm-fold consumer (EPI_LNF)."""
+    from image_to_pointcloud_amd import ops
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M + N + lnf)
+    K = 1024
+    x = ((torch.rand(M, K, generator=g) * 2 - 1)).to(torch.bfloat16).to(dev)
+    w = ((torch.rand(N, K, generator=g) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    kw = {}
+    if lnf:
+        kw = dict(ln_rows=torch.stack([torch.rand(M, generator=g) + 0.5, torch.randn(M, generator=g)], 1).to(dev),
+                  col_sum=torch.randn(N, generator=g).to(dev))
+    outs = []
+    try:
+        for on in (1, 0):
+            ops.set_tuning("gemm_tail160", on)
+            outs.append(ops.linear(x, w, bias=b, act="gelu", **kw))
+            torch.cuda.synchronize()
+    finally:
+        ops.set_tuning("gemm_tail160", 1)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))

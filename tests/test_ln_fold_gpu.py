@@ -59,6 +59,46 @@ def test_producer_outputs(M, N, K, C):
     assert torch.allclose(p[..., 1], m2, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("M,N,K,C,shifted", [(18464, 1024, 1024, 64, True), (18464, 1024, 4096, 64, True),
+                                             (1000, 1024, 1024, 64, False), (18464, 1024, 1024, 32, True),
+                                             (333, 768, 768, 64, True), (36928, 768, 3072, 64, True)])
+def test_producer_persistent_matches_tile_kernel(M, N, K, C, shifted):
+    """The LN-fold producer on the persistent engine (EPI_LNP, 160- or 256-row tiles; knob gemm_lnp_p)
+    writes exactly the tile kernel's bytes: the fp32 output, the bf16 shifted copy and the chunk
+    partials, whose sums follow the tile kernel's reduction order (gemm.hip epilogue_p)."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M * 7 + K + C)
+    a = _rand((M, K), g).to(torch.bfloat16).to(dev)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = _rand((N,), g, 0.1).to(torch.float32).to(dev)
+    x0 = (_rand((M, N), g) + 0.5).to(torch.float32).to(dev)
+    shift = (_rand((M,), g) * 3).to(torch.float32).to(dev) if shifted else None
+    outs = []
+    labels = []
+    try:
+        for on in (1, 0):
+            ops.set_tuning("gemm_lnp_p", on)
+            y = x0.clone()
+            part = torch.full((M, N // C, 2), float("nan"), dtype=torch.float32, device=dev)
+            yb = torch.zeros((M, N), dtype=torch.bfloat16, device=dev)
+            d = ops.GemmDesc()
+            d.m, d.n, d.k, d.lda, d.ldw, d.ldc, d.ldr, d.res_f32, d.c_f32 = M, N, K, K, K, N, N, 1, 1
+            d.a = d.w = d.c = d.res = d.ln_part = d.c_bf16 = 16
+            d.ldc_bf16, d.ln_chunk = N, C
+            labels.append(ops.gemm_kernel_label(d))
+            ops.linear(a, w, bias=b, res=y, out=y, ln_part=part, out_bf16=yb, ln_shift=shift, ln_chunk=C)
+            torch.cuda.synchronize()
+            outs.append((y, yb, part))
+    finally:
+        ops.set_tuning("gemm_lnp_p", 0)
+    assert labels[0].startswith("k_gemm_p<") and labels[0].endswith("ln_prod>"), labels
+    assert labels[1].startswith("k_gemm<"), labels
+    for got, ref, what in zip(outs[0], outs[1], ("fp32 output", "bf16 copy", "chunk partials")):
+        assert torch.equal(got.view(torch.int32) if got.dtype == torch.float32 else got.view(torch.int16),
+                           ref.view(torch.int32) if ref.dtype == torch.float32 else ref.view(torch.int16)), what
+
+
 @pytest.mark.parametrize("N,C", [(1024, 64), (384, 32), (1024, 32)])
 def test_rowstats_match_layernorm_statistics(N, C):
     ops = _ops()

@@ -1,6 +1,7 @@
 """Cost of the tile GEMM's epilogues on the DPT-Large O-projection shape (M 18464, N 1024, K 1024,
 320 x 256 tiles): bf16 out, fp32 out, fp32 out + fp32 residual in place, + the LayerNorm-fold
-producer (bf16 copy + chunk partials); and the same for FC2 (K 4096).  Interleaved rounds."""
+producer (bf16 copy + chunk partials) on the tile kernel and on the persistent engine's EPI_LNP (knob
+gemm_lnp_p); and the same for FC2 (K 4096).  Interleaved rounds."""
 import math, os, statistics, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -33,8 +34,10 @@ for K in (1024, 4096):
         "bf16 out": lambda: ops.linear(x, w, bias=b, out=o16),
         "fp32 out": lambda: ops.linear(x, w, bias=b, out=o32, out_f32=True),
         "fp32 + res (in place)": lambda: ops.linear(x, w, bias=b, res=res, out=res),
-        "fp32 + res + LN producer": lambda: ops.linear(x, w, bias=b, res=res, out=res, ln_part=part, out_bf16=ln,
-                                                       ln_shift=shift),
+        "fp32 + res + LN producer (tile)": lambda: (ops.set_tuning("gemm_lnp_p", 0), ops.linear(
+            x, w, bias=b, res=res, out=res, ln_part=part, out_bf16=ln, ln_shift=shift)),
+        "LN producer (persistent 160)": lambda: (ops.set_tuning("gemm_lnp_p", 1), ops.linear(
+            x, w, bias=b, res=res, out=res, ln_part=part, out_bf16=ln, ln_shift=shift)),
     }
     t = {k: [] for k in variants}
     for _ in range(5):
