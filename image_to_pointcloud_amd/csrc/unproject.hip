@@ -40,6 +40,9 @@ namespace unproj {
 
 constexpr int kSlots = 4;
 constexpr int kMaxTgt = 10;  // p2 / p98 ranks (4); with NaN / Inf also their shifted twins (4) + the median (2)
+// the selection from scratch: per image a level-0 histogram (top 11 key bits), kMaxTgt level-1
+// histograms (next 11 bits) and kMaxTgt level-2 histograms (last 10 bits)
+constexpr int kScrL1 = 2048, kScrL2 = kScrL1 + kMaxTgt * 2048, kScrWords = kScrL2 + kMaxTgt * 1024;
 constexpr int kBins = 2048;
 constexpr int kBlock = 256;
 constexpr int kMaxRows = 4;   // unprojection rows per workgroup (register-prefetched RGB)
@@ -77,7 +80,9 @@ constexpr int kMaxBandRanks = 256;
 
 // PH_INIT: level-0 sweep pending; PH_SEL: targets being narrowed; PH_SLOW: handed to
 // k_sel_slow (non-finite map); PH_DONE: p2 / p98 / mode final.
-enum Phase : uint32_t { PH_INIT = 0, PH_SEL = 1, PH_SLOW = 2, PH_DONE = 5 };
+// PH_SCR1 / PH_SCR2: the selection from scratch between its grid-wide radix levels (k_sel_slow ->
+// k_scratch<1> -> k_scratch<2>)
+enum Phase : uint32_t { PH_INIT = 0, PH_SEL = 1, PH_SLOW = 2, PH_SCR1 = 3, PH_SCR2 = 4, PH_DONE = 5 };
 enum SlotMode : uint32_t { SM_HIST = 0, SM_COMPACT = 1 };
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
@@ -152,7 +157,7 @@ struct Geo {
 inline double cv_scale(int in, int out) { return 1.0 / ((double)out / (double)in); }
 
 struct Layout {
-  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, mhist, gsend, grecv, wpart, field, tmp, total;
+  size_t state, hist, cand, rpart, xtab, ytab, trig, ex, mhist, gsend, grecv, wpart, slow, scr, field, tmp, total;
   uint32_t cap;   // candidate keys per slot and image (compaction sweeps)
 };
 
@@ -204,6 +209,8 @@ static Layout layout(int B, int H, int W, int smooth, int nranks = 0) {
   L.gsend = off; off = align_up(off + (nranks > 0 || B == 1 ? sizeof(uint32_t) * kBandWords : 0), 256);
   L.grecv = off; off = align_up(off + sizeof(uint32_t) * kBandWords * (size_t)std::max(nranks, 0), 256);
   L.wpart = off; off = align_up(off + sizeof(uint32_t) * kBelowSlots * 4 * (size_t)B, 256);
+  L.slow = off;  off = align_up(off + sizeof(uint32_t) * 8 * (size_t)B, 256);   // k_sel_slow's ticket, range, counts
+  L.scr = off;   off = align_up(off + sizeof(uint32_t) * kScrWords * (size_t)B, 256);   // from-scratch histograms
   L.field = off;
   if (smooth) {
     off = align_up(off + sizeof(double) * (size_t)B * H * W, 256);
@@ -397,7 +404,7 @@ __device__ __forceinline__ bool key_nonfinite(uint32_t k) { return k >= kKeyPosI
 __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, int m, int n, SelState* st,
                                                     uint32_t* hist, uint32_t* rpart, Tap* xt, Tap* yt, int dh, int dw,
                                                     int H, int W, double sx, double sy, double* trig, uint32_t* mhist,
-                                                    int nrc, uint32_t* wpart) {
+                                                    int nrc, uint32_t* wpart, uint32_t* slow, uint32_t* scr) {
   __shared__ uint32_t red[2][kBlock / 64];
   const int gtid = blockIdx.x * kBlock + threadIdx.x;
   const int nthr = gridDim.x * kBlock;
@@ -432,6 +439,10 @@ __global__ __launch_bounds__(kBlock) void k_prepare(const float* depth, int B, i
     for (size_t i = gtid; i < (size_t)B * kBins; i += nthr) mhist[i] = 0;
   if (wpart)       // k_sweep_w's below-window slots
     for (size_t i = gtid; i < (size_t)B * kBelowSlots * 4; i += nthr) wpart[i] = 0;
+  if (slow)        // k_sel_slow: {ticket, min key, max key, NaN, non-finite, -inf, +inf, -} per image
+    for (int i = gtid; i < 8 * B; i += nthr) slow[i] = (i & 7) == 1 ? 0xffffffffu : 0u;
+  if (scr)         // the from-scratch level-0 histograms (the later levels: zeroed by the level before)
+    for (size_t i = gtid; i < (size_t)B * kScrL1; i += nthr) scr[(i / kScrL1) * kScrWords + i % kScrL1] = 0;
   if (trig) {       // equirectangular ray tables (the oracle evaluates the same expressions)
     const double pi = 3.141592653589793;
     for (int i = gtid; i < W + H; i += nthr) {
@@ -925,6 +936,11 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
   uint32_t mnF[NW], mxF[NW], mnL[NW], mxL[NW];
   uint32_t wc[NW];                 // keys in this wave's LDS buffer of window w (wave-uniform)
   uint32_t* wbuf = &sh[0][0] + wid * kWaveBuf;      // + w * kStageW
+  // the finite range of the swept pixels (r04: app.py:198-199's min / max branch for near-constant
+  // maps, so k_sel_slow needs no pass of its own): float min / max, NaN ignored (minnum), +-inf
+  // masked in the rare non-finite branch; key order == float order on finite values but -0 < +0,
+  // which the end of k_sweep_w checks
+  float fmn = INFINITY, fmx = -INFINITY;
   uint32_t* cw_dst[NW];
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
@@ -963,7 +979,9 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float x = val[j];
+      float xr = x;                                   // x for the range: NaN unless finite
       if (__ballot(!__builtin_isfinite(x))) {     // rare: split the non-finite pixels (edge lanes' NaN aside)
+        xr = __builtin_isfinite(x) ? x : __builtin_nanf("");
         const uint64_t am = __ballot(act[j]);
         const bool ni = x == -INFINITY;
         const uint64_t nfm = __ballot(!__builtin_isfinite(x)) & am;
@@ -976,6 +994,8 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
 #pragma unroll
         for (int w = 0; w < NW; ++w) below[w] -= ni ? 1u : 0u;   // -inf compares below every window
       }
+      fmn = fminf(fmn, xr);
+      fmx = fmaxf(fmx, xr);
       bool inw[NW], anyl = false;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
@@ -1030,6 +1050,22 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
           wc[w] += cnt;
         }
       }
+    }
+  }
+  // the wave's finite range -> the image's key range (one atomic pair per wave).  The float min / max
+  // may pick +0 over -0 (or the reverse): exact keys unless a zero is an end of the range and the
+  // model map holds a value <= -0 (only then can a -0 pixel exist); such an image is flagged and
+  // k_sel_slow counts its range itself (SelState::pad3[0] bit 1)
+  for (int o = 32; o > 0; o >>= 1) {
+    fmn = fminf(fmn, __shfl_xor(fmn, o));
+    fmx = fmaxf(fmx, __shfl_xor(fmx, o));
+  }
+  if (lane == 0 && fmn <= fmx) {
+    if ((fmn == 0.f || fmx == 0.f) && S->rlo < f2key(0.f)) {
+      atomicOr(&S->pad3[0], 2u);
+    } else {
+      atomicMin(&S->kmin, f2key(fmn));
+      atomicMax(&S->kmax, f2key(fmx));
     }
   }
   // wave totals -> red[wave][...]: 0 nf, 1 nnan, 2 nneg, 3 npos, 4 + w below, then per window
@@ -1905,84 +1941,119 @@ __global__ __launch_bounds__(kBlock) void k_resolve_w(SelState* st, const uint32
   body();
 }
 
-// Non-finite maps (app.py:194-196: NaN / +-Inf filled with np.nanmedian, then the
-// percentiles of the filled map) and any image the fast levels did not finish: the whole
-// selection of one image in one workgroup, 3-level radix select on the key bits (11 + 11 +
-// 10) over every output row of the image (the model map is whole on every band, so this
-// needs no exchange in tile-parallel mode).  Rare path: one launch that returns at once
-// for every other image.
-__device__ void slow_radix(const Geo& g, int b, bool fill, float med, const uint32_t* rank_in, int ntgt,
-                           uint32_t* keys_out, uint32_t* sh, uint32_t* sc, uint32_t* rbin, uint32_t* rrem,
-                           uint32_t (*red)[kSlowBlock / 64], uint32_t* kmm) {
-  uint32_t prefix[4] = {0, 0, 0, 0}, rank[4] = {0, 0, 0, 0}, slot[4] = {0, 0, 0, 0}, sp[4] = {0, 0, 0, 0};
-  for (int t = 0; t < ntgt; ++t) rank[t] = rank_in[t];
-  const int n = g.H * g.W;
-  for (int level = 0; level < 3; ++level) {
-    int nslot = 1;
-    if (level > 0) {
-      nslot = 0;
-      for (int t = 0; t < ntgt; ++t) {
-        int found = -1;
-        for (int q = 0; q < nslot; ++q) if (sp[q] == prefix[t]) found = q;
-        if (found < 0) { found = nslot; sp[nslot++] = prefix[t]; }
-        slot[t] = (uint32_t)found;
-      }
+// Pixels of rows [v0, v1) of image b, resampled as sample() (the cv2 taps), handed to f(val);
+// thread-strided columns, one row at a time.
+template <class F>
+__device__ __forceinline__ void for_rows(const Geo& g, int b, int v0, int v1, F&& f) {
+  const float* D = g.depth + (size_t)b * g.dh * g.dw;
+  for (int v = v0; v < v1; ++v) {
+    if (g.same) {
+      for (int u = threadIdx.x; u < g.W; u += kSlowBlock) f(D[(size_t)v * g.dw + u]);
+      continue;
     }
-    const int match_shift = level == 1 ? 21 : 10;
-    const int bin_shift = level == 0 ? 21 : (level == 1 ? 10 : 0);
-    const uint32_t bin_mask = level == 2 ? 1023u : 2047u;
-    for (int i = threadIdx.x; i < nslot * kBins; i += kSlowBlock) sh[i] = 0;
-    __syncthreads();
-    uint32_t kmin = 0xffffffffu, kmax = 0u;
-    for (int p = threadIdx.x; p < n; p += kSlowBlock) {
-      const int v = p / g.W, u = p - v * g.W;
-      float val = sample(g, b, v, u);
-      if (fill && !isfinite(val)) val = med;
-      if (isnan(val)) continue;
-      const uint32_t key = f2key(val);
-      if (level == 0) {
-        kmin = min(kmin, key);
-        kmax = max(kmax, key);
-        atomicAdd(&sh[(key >> bin_shift) & bin_mask], 1u);
+    const Tap ty = g.yt[v];
+    const float* r0 = D + (size_t)ty.i0 * g.dw;
+    const float* r1 = D + (size_t)ty.i1 * g.dw;
+    for (int u = threadIdx.x; u < g.W; u += kSlowBlock) {
+      const Tap tx = g.xt[u];
+      float h0, h1;
+      if (tx.i1 < 0) {
+        h0 = r0[tx.i0];
+        h1 = r1[tx.i0];
       } else {
-        for (int q = 0; q < nslot; ++q)
-          if ((key >> match_shift) == sp[q]) atomicAdd(&sh[q * kBins + ((key >> bin_shift) & bin_mask)], 1u);
+        h0 = r0[tx.i0] * tx.w0 + r0[tx.i1] * tx.w1;
+        h1 = r1[tx.i0] * tx.w0 + r1[tx.i1] * tx.w1;
       }
-    }
-    if (level == 0) {
-      kmin = wave_min_u32(kmin);
-      kmax = wave_max_u32(kmax);
-      if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = kmin; red[1][threadIdx.x >> 6] = kmax; }
-    }
-    __syncthreads();
-    if (level == 0 && threadIdx.x == 0) {
-      uint32_t mn = 0xffffffffu, mx = 0u;
-      for (int w = 0; w < kSlowBlock / 64; ++w) { mn = min(mn, red[0][w]); mx = max(mx, red[1][w]); }
-      kmm[0] = mn;
-      kmm[1] = mx;
-    }
-    const int nb = level == 2 ? 1024 : kBins;
-    const int bits = level == 2 ? 10 : 11;
-    for (int t = 0; t < ntgt; ++t) {
-      if (threadIdx.x == 0) { *rbin = 0; *rrem = 0; }
-      __syncthreads();
-      find_bins<kSlowBlock>(sh + slot[t] * kBins, nb, &rank[t], 1, sc, rbin, rrem);
-      prefix[t] = (prefix[t] << bits) | *rbin;
-      rank[t] = *rrem;
-      __syncthreads();
+      f(h0 * ty.w0 + h1 * ty.w1);
     }
   }
-  for (int t = 0; t < ntgt; ++t) keys_out[t] = prefix[t];
 }
 
-__global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, int B) {
-  __shared__ uint32_t sh[kSlots * kBins];
-  __shared__ uint32_t sc[kSlowBlock];
-  __shared__ uint32_t red[2][kSlowBlock / 64];
-  __shared__ uint32_t rbin, rrem, kmm[2], keys[4];
-  __shared__ int done;
+// A workgroup's share of a grid-wide pass is published (its atomics / stores done: every wave's
+// vmcnt(0), the barrier, one agent release), then it takes the image's ticket; true in the one
+// workgroup that arrives last, which then acquires (cdna_hip_programming.md Guideline 16).
+__device__ __forceinline__ bool arrive_last(uint32_t* ticket, int P, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *flag = P == 1 || atomicAdd(ticket, 1u) == (uint32_t)(P - 1);
+    if (*flag) {
+      atomicExch(ticket, 0u);    // (every workgroup has arrived: the next pass reuses it)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// The from-scratch selection's level resolve (the last arriving workgroup): every unresolved target
+// t (tslot != kNoSlot) has its key prefix in tlo[t] and its rank among the F keys under that prefix
+// in rank[t]; slot q of `hist` (global, nb bins each) holds the next `bits` key bits of the keys
+// under prefix pre[q].  Narrows every target; returns the number still unresolved.
+__device__ int scratch_resolve(SelState& s, const uint32_t* hist, int nb, int bits, const uint32_t* pre, int nslot,
+                               bool last_level, uint32_t* lh, uint32_t* wsum, uint32_t* rb, uint32_t* rr) {
+  __shared__ uint32_t trk[kMaxTgt];
+  __shared__ int tq[kMaxTgt], ntq;
+  for (int q = 0; q < nslot; ++q) {
+    for (int i = threadIdx.x; i < nb; i += kSlowBlock) lh[i] = hist[q * nb + i];
+    if (threadIdx.x == 0) {
+      ntq = 0;
+      for (int t = 0; t < (int)s.ntgt; ++t)
+        if (s.tslot[t] != kNoSlot && s.tlo[t] == pre[q]) { tq[ntq] = t; trk[ntq++] = s.rank[t]; }
+    }
+    __syncthreads();
+    find_bins<kSlowBlock>(lh, nb, trk, ntq, wsum, rb, rr);
+    if (threadIdx.x == 0)
+      for (int i = 0; i < ntq; ++i) {
+        const int t = tq[i];
+        s.tlo[t] = (s.tlo[t] << bits) | rb[i];
+        s.rank[t] = rr[i];
+        if (last_level) { s.thi[t] = s.tlo[t]; s.tslot[t] = kNoSlot; }
+      }
+    __syncthreads();
+  }
+  int open = 0;
+  for (int t = 0; t < (int)s.ntgt; ++t) open += s.tslot[t] != kNoSlot ? 1 : 0;
+  return open;
+}
+
+// Distinct prefixes of the unresolved targets (the level's histogram slots).
+__device__ __forceinline__ int scratch_slots(const SelState& s, uint32_t* pre) {
+  int n = 0;
+  for (int t = 0; t < (int)s.ntgt; ++t) {
+    if (s.tslot[t] == kNoSlot) continue;
+    bool seen = false;
+    for (int q = 0; q < n; ++q) seen |= pre[q] == s.tlo[t];
+    if (!seen) pre[n++] = s.tlo[t];
+  }
+  return n;
+}
+
+// Grid: P workgroups per image (b = blockIdx.x / P).  Every workgroup of an image derives the same
+// decision from st[b] (which only the image's last arriving workgroup writes, after all have read
+// it):
+//  1  finish from the resolved targets;
+//  2  the near-constant branch (p98 <= p2: app.py:198-199 needs the map's min / max) with a range
+//     k_sweep_w could not give (a band of a C4 run, a signed zero at an end): a grid-wide pass, each
+//     workgroup a 1/P share of the rows, partial keys combined by agent-scope atomics;
+//  0  the selection from scratch (a window missed, a spike or an overflowed list: err; the levels
+//     path's PH_SLOW): level 0 here -- every workgroup counts its rows' NaN / +-inf pixels and
+//     histograms their finite keys' top 11 bits; the last arriver places the targets (the four
+//     percentile ranks, or fill_targets' ten order statistics of the finite keys with NaN / Inf)
+//     and resolves their level-0 bins -- then k_scratch<1> / <2> narrow them over the grid too.
+// (r04: one workgroup per image did passes 2 and 0: 833 us for 32 x 1024^2 near-constant maps, ~95 ms
+// for one 8192 x 4096 panorama.)  slow[b] = {ticket, min key, max key, NaN, non-finite, -inf, +inf, -}
+// and scr[b]'s level-0 histogram are reset by k_prepare.
+__global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, int B, int P, uint32_t* slow,
+                                                          int swept_range, uint32_t* scr) {
+  __shared__ uint32_t sh[kBins];
+  __shared__ uint32_t wsum[kSlowBlock / 64], rb[kMaxTgt], rr[kMaxTgt], pre[kMaxTgt];
+  __shared__ int done, last;
   __shared__ SelState s;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x / P, part = blockIdx.x - (blockIdx.x / P) * P;
   if (b >= B) return;
   if (threadIdx.x == 0) {     // (usually done: only the phase is read)
     const uint32_t ph = st[b].phase;
@@ -1990,119 +2061,170 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
   }
   __syncthreads();
   if (done) return;
-  if (threadIdx.x == 0) s = st[b];
-  __syncthreads();
-  if (s.phase == PH_INIT) {
-    // window path (k_sweep_w / k_resolve_w): every target resolved unless err; the min / max
-    // branch (p98 <= p2: a near-constant map) is left to the slow path, which counts the range
-    if (s.err == 0) {
-      if (threadIdx.x == 0) {
-        done = finish_targets(s, false) ? 1 : 0;
-        if (done) st[b] = s;
-        // every target resolved, only the min / max branch's range is missing (p98 <= p2: a
-        // constant or near-constant map): one pass for the finite range instead of the selection
-        // from scratch below
-        bool resolved = !done && s.err == 0;
-        for (int t = 0; t < (int)s.ntgt; ++t) resolved = resolved && s.tlo[t] == s.thi[t];
-        if (resolved) done = 2;
-      }
-      __syncthreads();
-      if (done == 1) return;
-      if (done == 2) {
-        const int n = g.H * g.W;
-        uint32_t lo = 0xffffffffu, hi = 0u;
-        for (int p = threadIdx.x; p < n; p += kSlowBlock) {
-          const int v = p / g.W, u = p - v * g.W;
-          const float val = sample(g, b, v, u);
-          if (isfinite(val)) {
-            const uint32_t k = f2key(val);
-            lo = min(lo, k);
-            hi = max(hi, k);
-          }
-        }
-        lo = wave_min_u32(lo);
-        hi = wave_max_u32(hi);
-        if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = lo; red[1][threadIdx.x >> 6] = hi; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          for (int w = 0; w < kSlowBlock / 64; ++w) { lo = min(lo, red[0][w]); hi = max(hi, red[1][w]); }
-          s.kmin = min(s.kmin, lo);      // (with a fill, finish_targets already merged the median)
-          s.kmax = max(s.kmax, hi);
-          if (finish_targets(s, true)) st[b] = s;
-          else done = 0;                 // (not expected: the range was the only thing missing)
-        }
-        __syncthreads();
-        if (done == 2) return;
-      }
+  if (threadIdx.x == 0) {
+    s = st[b];
+    done = 0;
+    if (s.phase == PH_INIT && s.err == 0) {
+      // window path (k_sweep_w / k_resolve_w): every target resolved unless err
+      done = finish_targets(s, false) ? 1 : 0;
+      // every target resolved, only the min / max branch's range is missing (p98 <= p2: a
+      // constant or near-constant map)
+      bool resolved = !done && s.err == 0;
+      for (int t = 0; t < (int)s.ntgt; ++t) resolved = resolved && s.tlo[t] == s.thi[t];
+      if (resolved) done = 2;
+      // k_sweep_w counted the whole image's finite range (kmin / kmax) unless it flagged a signed zero
+      // at an end of it, or the sweep covered a band only (swept_range = 0: C4 runs)
+      if (resolved && swept_range && !(s.pad3[0] & 2u)) done = finish_targets(s, true) ? 1 : 0;
     }
-  } else if (s.phase != PH_SLOW) {
+  }
+  __syncthreads();
+  uint32_t* sl = slow + 8 * (size_t)b;
+  const int v0 = (int)((int64_t)g.H * part / P), v1 = (int)((int64_t)g.H * (part + 1) / P);
+  const int lane = threadIdx.x & 63;
+  if (done == 2) {
+    uint32_t lo = 0xffffffffu, hi = 0u;
+    for_rows(g, b, v0, v1, [&](float val) {
+      if (isfinite(val)) { const uint32_t k = f2key(val); lo = min(lo, k); hi = max(hi, k); }
+    });
+    lo = wave_min_u32(lo);
+    hi = wave_max_u32(hi);
+    if (lane == 0) {
+      if (lo != 0xffffffffu) atomicMin(&sl[1], lo);
+      if (hi) atomicMax(&sl[2], hi);
+    }
+  } else if (done == 0) {
+    for (int i = threadIdx.x; i < kBins; i += kSlowBlock) sh[i] = 0;
+    __syncthreads();
+    uint32_t nnan = 0, nnf = 0, nneg = 0, npos = 0, lo = 0xffffffffu, hi = 0u;
+    for_rows(g, b, v0, v1, [&](float val) {
+      if (!isfinite(val)) {
+        ++nnf;
+        nnan += isnan(val) ? 1u : 0u;
+        nneg += val == -INFINITY ? 1u : 0u;
+        npos += val == INFINITY ? 1u : 0u;
+        return;
+      }
+      const uint32_t k = f2key(val);
+      lo = min(lo, k);
+      hi = max(hi, k);
+      atomicAdd(&sh[k >> 21], 1u);
+    });
+    nnan = wave_sum_u32(nnan); nnf = wave_sum_u32(nnf); nneg = wave_sum_u32(nneg); npos = wave_sum_u32(npos);
+    lo = wave_min_u32(lo); hi = wave_max_u32(hi);
+    if (lane == 0) {
+      if (nnf) { atomicAdd(&sl[3], nnan); atomicAdd(&sl[4], nnf); atomicAdd(&sl[5], nneg); atomicAdd(&sl[6], npos); }
+      if (lo != 0xffffffffu) atomicMin(&sl[1], lo);
+      if (hi) atomicMax(&sl[2], hi);
+    }
+    __syncthreads();
+    uint32_t* h0 = scr + (size_t)b * kScrWords;
+    for (int i = threadIdx.x; i < kBins; i += kSlowBlock)
+      if (sh[i]) atomicAdd(&h0[i], sh[i]);
+  }
+  if (!arrive_last(&sl[0], P, &last)) return;
+  if (done == 1) {
+    if (threadIdx.x == 0) st[b] = s;
     return;
   }
-  const int n = g.H * g.W;
-  uint32_t nan_c = 0, nf_c = 0;
-  for (int p = threadIdx.x; p < n; p += kSlowBlock) {
-    const int v = p / g.W, u = p - v * g.W;
-    const float val = sample(g, b, v, u);
-    nan_c += isnan(val) ? 1u : 0u;
-    nf_c += isfinite(val) ? 0u : 1u;
-  }
-  nan_c = wave_sum_u32(nan_c);
-  nf_c = wave_sum_u32(nf_c);
-  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = nan_c; red[1][threadIdx.x >> 6] = nf_c; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t a = 0, c = 0;
-    for (int w = 0; w < kSlowBlock / 64; ++w) { a += red[0][w]; c += red[1][w]; }
-    s.nan_count = a;
-    s.nonfinite_count = c;
-  }
-  __syncthreads();
-  bool fill = false;
-  float med = __uint_as_float(0x7fc00000u);
-  if (s.nonfinite_count != 0) {
-    const uint32_t m = s.n - s.nan_count;
-    if (m == 0) {                        // all-NaN: nanmedian is NaN, every value stays NaN
-      if (threadIdx.x == 0) {
-        s.has_med = 1;
-        s.mode = 2;
-        s.p2 = s.p98 = (double)__uint_as_float(0x7fc00000u);
-        s.phase = PH_DONE;
-        st[b] = s;
-      }
-      return;
-    }
-    uint32_t r[2];
-    const uint32_t h = m / 2;
-    int nr;
-    if (m & 1u) { r[0] = r[1] = h; nr = 1; }
-    else { r[0] = h - 1; r[1] = h; nr = 2; }
-    slow_radix(g, b, false, 0.f, r, 2, keys, sh, sc, &rbin, &rrem, red, kmm);
-    const float a = key2f(keys[0]);
-    const float c = key2f(keys[1]);
-    med = nr == 1 ? a : (a + c) / 2.0f;   // np.mean of the middle pair in float32
-    fill = true;
+  if (done == 2) {
     if (threadIdx.x == 0) {
-      s.med = med;
-      s.has_med = 1;
-      s.med_ranks = (uint32_t)nr;
+      const uint32_t lo = atomicMin(&sl[1], 0xffffffffu), hi = atomicMax(&sl[2], 0u);   // read at the coherence point
+      s.kmin = min(s.kmin, lo);      // (with a fill, finish_targets already merged the median)
+      s.kmax = max(s.kmax, hi);
+      if (finish_targets(s, true)) st[b] = s;
+      else { s.err = 1; s.phase = PH_SLOW; st[b] = s; }   // (not expected: the range was the only thing missing)
     }
-    if (isnan(med)) {   // e.g. median of {-inf, +inf}: the filled map has NaNs -> np.percentile is NaN
-      if (threadIdx.x == 0) {
-        s.mode = 2;
-        s.p2 = s.p98 = (double)med;
-        s.phase = PH_DONE;
-        st[b] = s;
-      }
-      return;
-    }
+    return;
   }
-  uint32_t r[4];
-  pct_ranks(s.n, r);
-  slow_radix(g, b, fill, med, r, 4, keys, sh, sc, &rbin, &rrem, red, kmm);
+  // from scratch, level 0 resolved by this (last) workgroup
   if (threadIdx.x == 0) {
-    s.kmin = kmm[0];
-    s.kmax = kmm[1];
-    finalize_pct(s, keys);
+    s.nan_count = atomicAdd(&sl[3], 0u);
+    s.nonfinite_count = atomicAdd(&sl[4], 0u);
+    s.ninf_neg = atomicAdd(&sl[5], 0u);
+    s.ninf_pos = atomicAdd(&sl[6], 0u);
+    s.kmin = atomicMin(&sl[1], 0xffffffffu);
+    s.kmax = atomicMax(&sl[2], 0u);
+    s.err = 0;
+    s.has_med = 0;
+    s.fill = 0;
+    done = 0;
+    if (s.nonfinite_count == 0) {
+      uint32_t r[4];
+      pct_ranks(s.n, r);
+      s.ntgt = 4;
+      for (int t = 0; t < 4; ++t) { s.rank[t] = r[t]; s.tslot[t] = 0; s.tlo[t] = 0; s.thi[t] = 0xffffffffu; }
+    } else if (s.nan_count == s.n) {   // all-NaN: nanmedian is NaN, every value stays NaN
+      s.has_med = 1;
+      s.mode = 2;
+      s.p2 = s.p98 = (double)__uint_as_float(0x7fc00000u);
+      s.phase = PH_DONE;
+      done = 1;
+    } else {
+      fill_targets(s, false);          // ten order statistics of the finite keys (tslot 0 = open)
+      for (int t = 0; t < (int)s.ntgt; ++t) if (s.tslot[t] != kNoSlot) s.tlo[t] = 0;
+    }
+    pre[0] = 0;
+  }
+  __syncthreads();
+  if (done) {
+    if (threadIdx.x == 0) st[b] = s;
+    return;
+  }
+  const int open = scratch_resolve(s, scr + (size_t)b * kScrWords, kBins, 11, pre, 1, false, sh, wsum, rb, rr);
+  // the next level's histograms start from zero
+  for (int i = threadIdx.x; i < kMaxTgt * kBins; i += kSlowBlock) scr[(size_t)b * kScrWords + kScrL1 + i] = 0;
+  if (threadIdx.x == 0) {
+    if (open) s.phase = PH_SCR1;
+    else finish_targets(s, true);    // (every target was a +-inf sentinel)
+    st[b] = s;
+  }
+}
+
+// The from-scratch selection's radix levels 1 (key bits 20..10) and 2 (bits 9..0), grid-wide like
+// k_sel_slow: each workgroup histograms its rows' finite keys under each open target's prefix, the
+// last arriver narrows the targets (level 2: to the exact keys, then the finish).  Returns at once for
+// an image in any other phase (one launch each in every selection chain).
+template <int LEVEL>
+__global__ __launch_bounds__(kSlowBlock) void k_scratch(Geo g, SelState* st, int B, int P, uint32_t* slow,
+                                                         uint32_t* scr) {
+  constexpr uint32_t PH = LEVEL == 1 ? PH_SCR1 : PH_SCR2;
+  constexpr int NB = LEVEL == 1 ? kBins : 1024, MATCH = LEVEL == 1 ? 21 : 10, BSH = LEVEL == 1 ? 10 : 0;
+  constexpr int BITS = LEVEL == 1 ? 11 : 10;
+  __shared__ uint32_t lh[kMaxTgt * NB];
+  __shared__ uint32_t wsum[kSlowBlock / 64], rb[kMaxTgt], rr[kMaxTgt], pre[kMaxTgt];
+  __shared__ int go, nslot, last;
+  __shared__ SelState s;
+  const int b = blockIdx.x / P, part = blockIdx.x - (blockIdx.x / P) * P;
+  if (b >= B) return;
+  if (threadIdx.x == 0) go = st[b].phase == PH ? 1 : 0;
+  __syncthreads();
+  if (!go) return;
+  if (threadIdx.x == 0) {
+    s = st[b];
+    nslot = scratch_slots(s, pre);
+  }
+  __syncthreads();
+  const int ns = nslot;
+  for (int i = threadIdx.x; i < ns * NB; i += kSlowBlock) lh[i] = 0;
+  __syncthreads();
+  const int v0 = (int)((int64_t)g.H * part / P), v1 = (int)((int64_t)g.H * (part + 1) / P);
+  for_rows(g, b, v0, v1, [&](float val) {
+    if (!isfinite(val)) return;
+    const uint32_t k = f2key(val);
+    for (int q = 0; q < ns; ++q)
+      if ((k >> MATCH) == pre[q]) atomicAdd(&lh[q * NB + ((k >> BSH) & (NB - 1))], 1u);
+  });
+  __syncthreads();
+  uint32_t* gh = scr + (size_t)b * kScrWords + (LEVEL == 1 ? kScrL1 : kScrL2);
+  for (int i = threadIdx.x; i < ns * NB; i += kSlowBlock)
+    if (lh[i]) atomicAdd(&gh[i], lh[i]);
+  if (!arrive_last(&slow[8 * (size_t)b], P, &last)) return;
+  const int open = scratch_resolve(s, gh, NB, BITS, pre, ns, LEVEL == 2, lh, wsum, rb, rr);
+  if (LEVEL == 1)
+    for (int i = threadIdx.x; i < kMaxTgt * 1024; i += kSlowBlock) scr[(size_t)b * kScrWords + kScrL2 + i] = 0;
+  if (threadIdx.x == 0) {
+    if (LEVEL == 1 && open) s.phase = PH_SCR2;
+    else finish_targets(s, true);
     st[b] = s;
   }
 }
@@ -2563,30 +2685,29 @@ __global__ __launch_bounds__(kBlock) void k_unproject_rows(Geo g, const SelState
   const int rfirst = trow < rpp ? r0 + trow : r1;   // waves past rpp * tpr threads: idle
   const int nrt = rfirst < r1 ? (r1 - rfirst + rpp - 1) / rpp : 0;   // rows of this thread (<= kRowsPT)
   const size_t img_base = (size_t)b * g.H * g.W;
-  auto load_rgb = [&](int row, uint32_t (&q)[4][3]) {
+  // the BGR bytes of this thread's 4 points of a row as dwords: STEP 1 the 12 contiguous bytes;
+  // STEP 2 the 24 bytes of image columns 2 ub .. 2 ub + 7 (point j at byte 6 j); STEP 4 one dword
+  // per point (point j at byte 12 j) -- r04: the byte loads of STEP 2 / 4 (12 per row) and their
+  // one-row prefetch left the medium-density kernel at 0.36 of HBM
+  constexpr int NQ = STEP == 1 ? 3 : STEP == 2 ? 6 : 4;
+  auto load_rgb = [&](int row, uint32_t (&q)[NQ]) {
     const int v = row * STEP;
-    if (STEP == 1) {
-      const uint32_t* p32 = reinterpret_cast<const uint32_t*>(img + (img_base + (size_t)v * g.W + ub) * 3);
-      q[0][0] = p32[0]; q[0][1] = p32[1]; q[0][2] = p32[2];
+    const uint32_t* p32 = reinterpret_cast<const uint32_t*>(img + (img_base + (size_t)v * g.W + (size_t)ub * STEP) * 3);
+    if (STEP == 4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[j] = p32[3 * j];
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint8_t* px = img + (img_base + (size_t)v * g.W + (ub + j) * STEP) * 3;
-        q[j][0] = px[0]; q[j][1] = px[1]; q[j][2] = px[2];
-      }
+      for (int d = 0; d < NQ; ++d) q[d] = p32[d];
     }
   };
-  // STEP 1: the RGB of all of this thread's rows is requested first, so the HBM latency of the
-  // cold image overlaps the model-row staging and the horizontal pass; else one row ahead
-  constexpr int PF = STEP == 1 ? kRowsPT : 1;
-  uint32_t qa[PF][4][3];
-  if (STEP == 1) {
+  // the RGB of all of this thread's rows is requested first, so the HBM latency of the cold
+  // image overlaps the model-row staging and the horizontal pass
+  constexpr int PF = kRowsPT;
+  uint32_t qa[PF][NQ];
 #pragma unroll
-    for (int k = 0; k < PF; ++k)
-      if (k < nrt) load_rgb(rfirst + k * rpp, qa[k]);
-  } else if (nrt > 0) {
-    load_rgb(rfirst, qa[0]);
-  }
+  for (int k = 0; k < PF; ++k)
+    if (k < nrt) load_rgb(rfirst + k * rpp, qa[k]);
   stage_floats(raw, g.depth + ((size_t)b * g.dh + lo) * g.dw, nrows * g.dw);
   __syncthreads();
   int ui[4];
@@ -2616,12 +2737,6 @@ __global__ __launch_bounds__(kBlock) void k_unproject_rows(Geo g, const SelState
   for (int k = 0; k < kRowsPT; ++k) {
     if (k >= nrt) break;
     const int row = rfirst + k * rpp;
-    uint32_t q[4][3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) q[j][c] = qa[STEP == 1 ? k : 0][j][c];
-    if (STEP != 1 && k + 1 < nrt) load_rgb(row + rpp, qa[0]);
     const int v = row * STEP;
     const Tap ty = ytap(g, v);
     const float4 h0 = hrow[(ty.i0 - lo) * kBlock + threadIdx.x];
@@ -2629,18 +2744,17 @@ __global__ __launch_bounds__(kBlock) void k_unproject_rows(Geo g, const SelState
     const float hv0[4] = {h0.x, h0.y, h0.z, h0.w}, hv1[4] = {h1.x, h1.y, h1.z, h1.w};
     const double dv = (double)v - cam.cy;
     uint32_t pc[4][3];   // [point][r,g,b] (source is BGR)
-    if (STEP == 1) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const int byte = 3 * j + (2 - c);
-          pc[j][c] = (q[0][byte >> 2] >> (8 * (byte & 3))) & 0xffu;
+      for (int c = 0; c < 3; ++c) {
+        if (STEP == 4) {
+          pc[j][c] = (qa[k][j] >> (8 * (2 - c))) & 0xffu;
+        } else {
+          const int byte = 3 * STEP * j + (2 - c);
+          pc[j][c] = (qa[k][byte >> 2] >> (8 * (byte & 3))) & 0xffu;
         }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { pc[j][0] = q[j][2]; pc[j][1] = q[j][1]; pc[j][2] = q[j][0]; }
-    }
+      }
     float px[4][3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -3297,6 +3411,13 @@ static int select_level(const Geo& g, SelState* st, uint32_t* hist, uint32_t* ca
 // "sel_windows" (I2PC_SEL_WIN): 1 = the window-only batch selection (k_sweep_w / k_resolve_w),
 // 0 = the histogram levels (the band path's); both exact.
 static thread_local int g_sel_windows = [] { const char* e = getenv("I2PC_SEL_WIN"); return e ? atoi(e) : 1; }();
+// "sel_scratch" (I2PC_SEL_SCRATCH, tests / measurement only): every image of a window-path selection
+// goes to the selection from scratch (as if a window had missed)
+static thread_local int g_sel_scratch = [] { const char* e = getenv("I2PC_SEL_SCRATCH"); return e ? atoi(e) : 0; }();
+__global__ void k_force_scratch(SelState* st, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B && st[b].phase == PH_INIT) st[b].err = 1u;
+}
 // output rows per k_sweep_w workgroup ("sel_rows", I2PC_SEL_ROWS)
 static thread_local int g_sel_rows = [] {
   const char* e = getenv("I2PC_SEL_ROWS");
@@ -3304,9 +3425,24 @@ static thread_local int g_sel_rows = [] {
   return v > 0 && v <= kMaxSelRows ? v : 16;
 }();
 
+// k_sel_slow's workgroups per image: ~256 K pixels each (a 1024^2 image: 4), <= 2048 workgroups in all
+static int slow_parts(int H, int W, int B) {
+  const int64_t want = std::max<int64_t>(1, (int64_t)H * W / 262144);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(1, 2048 / std::max(B, 1))));
+}
+
+// the selection's finish: k_sel_slow (finish / range / from-scratch level 0) and the from-scratch
+// radix levels 1 and 2 (no-ops unless an image needs them)
+static void launch_slow(const Geo& g, SelState* st, int B, uint32_t* slow, uint32_t* scr, int swept, hipStream_t s) {
+  const int P = slow_parts(g.H, g.W, B);
+  hipLaunchKernelGGL(k_sel_slow, dim3(B * P), dim3(kSlowBlock), 0, s, g, st, B, P, slow, swept, scr);
+  hipLaunchKernelGGL(k_scratch<1>, dim3(B * P), dim3(kSlowBlock), 0, s, g, st, B, P, slow, scr);
+  hipLaunchKernelGGL(k_scratch<2>, dim3(B * P), dim3(kSlowBlock), 0, s, g, st, B, P, slow, scr);
+}
+
 static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* cand, const uint32_t* rpart,
-                         uint32_t* mhist, uint32_t* wpart, uint32_t cap, int B, const Sweep& sw, hipStream_t s,
-                         const Exchange* x = nullptr, int nrc = 0) {
+                         uint32_t* mhist, uint32_t* wpart, uint32_t* slow, uint32_t* scr, uint32_t cap, int B,
+                         const Sweep& sw, hipStream_t s, const Exchange* x = nullptr, int nrc = 0) {
   if (nrc <= 0) nrc = range_chunks(B);
   // full-resolution sample of ~64 K points per image for the level-0 estimate
   const SamplePlan sp = sample_plan(g.H, g.W, B);
@@ -3341,11 +3477,13 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
       if (x->gather(x->user, x->send, x->recv, kBandWords, s) != 0)
         return set_error(I2PC_ELAUNCH, "gather callback failed (target bins)");
       hipLaunchKernelGGL(k_bandw_final, dim3(kMaxTgt), dim3(kBlock), 0, s, st, x->recv, x->nranks, cand, kSlots * cap);
-      hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
+      if (g_sel_scratch) hipLaunchKernelGGL(k_force_scratch, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
+      launch_slow(g, st, B, slow, scr, sw.row0 == 0 && sw.row_end == g.H ? 1 : 0, s);
       return check_launch("select");
     }
     hipLaunchKernelGGL(k_resolve_w, dim3(B * 3), dim3(kBlock), 0, s, st, cand, cap, B, wpart);
-    hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
+    if (g_sel_scratch) hipLaunchKernelGGL(k_force_scratch, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
+    launch_slow(g, st, B, slow, scr, sw.row0 == 0 && sw.row_end == g.H ? 1 : 0, s);
     return check_launch("select");
   }
   int rc;
@@ -3353,7 +3491,7 @@ static int launch_select(const Geo& g, SelState* st, uint32_t* hist, uint32_t* c
   if ((rc = select_level<1>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   if ((rc = select_level<2>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
   if ((rc = select_level<3>(g, st, hist, cand, cap, B, sw, s, x))) return rc;
-  hipLaunchKernelGGL(k_sel_slow, dim3(B), dim3(kSlowBlock), 0, s, g, st, B);
+  launch_slow(g, st, B, slow, scr, 0, s);
   return check_launch("select");
 }
 
@@ -3492,7 +3630,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   hipLaunchKernelGGL(k_prepare, dim3(batch * range_chunks(batch)), dim3(kBlock), 0, s, depth, batch, dep_h * dep_w, n,
                      st, (xch || lband || !g_sel_windows) ? hist : nullptr, rpart, xt, yt, dep_h, dep_w, img_h, img_w,
                      cv_scale(dep_w, img_w), cv_scale(dep_h, img_h), trig, reinterpret_cast<uint32_t*>(ws + L.mhist),
-                     range_chunks(batch), reinterpret_cast<uint32_t*>(ws + L.wpart));
+                     range_chunks(batch), reinterpret_cast<uint32_t*>(ws + L.wpart), reinterpret_cast<uint32_t*>(ws + L.slow),
+                     reinterpret_cast<uint32_t*>(ws + L.scr));
 
   Geo g{depth, dep_h, dep_w, img_h, img_w, xt, yt, (dep_h == img_h && dep_w == img_w) ? 1 : 0,
         cv_scale(dep_w, img_w), cv_scale(dep_h, img_h)};
@@ -3513,6 +3652,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
   uint32_t* cand = reinterpret_cast<uint32_t*>(ws + L.cand);
   uint32_t* mhist = reinterpret_cast<uint32_t*>(ws + L.mhist);
   uint32_t* wpart = reinterpret_cast<uint32_t*>(ws + L.wpart);
+  uint32_t* slow = reinterpret_cast<uint32_t*>(ws + L.slow);
+  uint32_t* scr = reinterpret_cast<uint32_t*>(ws + L.scr);
   const int nrc = range_chunks(batch);
   int rc;
   const int parts = xch ? 1 : select_parts(batch);
@@ -3530,7 +3671,7 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
       gq.depth = g.depth + (size_t)b0 * dep_h * dep_w;
       rc = launch_select(gq, st + b0, hist + (size_t)b0 * kSlots * kBins, cand + (size_t)b0 * kSlots * L.cap,
                          rpart + (size_t)b0 * nrc * 2, mhist + (size_t)b0 * kBins, wpart + (size_t)b0 * kBelowSlots * 4,
-                         L.cap, b1 - b0, ssel, sq, nullptr, nrc);
+                         slow + (size_t)b0 * 8, scr + (size_t)b0 * kScrWords, L.cap, b1 - b0, ssel, sq, nullptr, nrc);
       if (rc) return rc;
       if (q > 0) {
         if (hipEventRecord(ax.join[q - 1], sq) != hipSuccess || hipStreamWaitEvent(s, ax.join[q - 1], 0) != hipSuccess)
@@ -3538,7 +3679,8 @@ static int run_unproject(const float* depth, int dep_h, int dep_w, const uint8_t
       }
     }
   } else {
-    rc = launch_select(g, st, hist, cand, rpart, mhist, wpart, L.cap, batch, ssel, s, (xch || lband) ? &xb : nullptr, nrc);
+    rc = launch_select(g, st, hist, cand, rpart, mhist, wpart, slow, scr, L.cap, batch, ssel, s,
+                       (xch || lband) ? &xb : nullptr, nrc);
     if (rc) return rc;
   }
 
@@ -3722,12 +3864,14 @@ extern "C" int i2pc_depth_preview(const float* depth, int batch, int h, int w, i
   uint32_t* rpart = reinterpret_cast<uint32_t*>(ws + L.rpart);
   hipLaunchKernelGGL(k_prepare, dim3(batch * range_chunks(batch)), dim3(kBlock), 0, s, depth, batch, n, n, st,
                      g_sel_windows ? nullptr : hist, rpart, xt, yt, h, w, h, w, 1.0, 1.0, nullptr,
-                     reinterpret_cast<uint32_t*>(ws + L.mhist), range_chunks(batch), reinterpret_cast<uint32_t*>(ws + L.wpart));
+                     reinterpret_cast<uint32_t*>(ws + L.mhist), range_chunks(batch), reinterpret_cast<uint32_t*>(ws + L.wpart),
+                     reinterpret_cast<uint32_t*>(ws + L.slow), reinterpret_cast<uint32_t*>(ws + L.scr));
   Geo g{depth, h, w, h, w, xt, yt, 1, 1.0, 1.0};
   const Sweep ssel = plan_select(h, w, h, w, true, 0, h);
   int rc = launch_select(g, st, hist, reinterpret_cast<uint32_t*>(ws + L.cand), rpart,
-                         reinterpret_cast<uint32_t*>(ws + L.mhist), reinterpret_cast<uint32_t*>(ws + L.wpart), L.cap,
-                         batch, ssel, s);
+                         reinterpret_cast<uint32_t*>(ws + L.mhist), reinterpret_cast<uint32_t*>(ws + L.wpart),
+                         reinterpret_cast<uint32_t*>(ws + L.slow), reinterpret_cast<uint32_t*>(ws + L.scr), L.cap, batch,
+                         ssel, s);
   if (rc) return rc;
   const int64_t total = (int64_t)batch * n;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
@@ -3741,6 +3885,7 @@ bool i2pc_unproject_tune(const char* name, int value) {
   if (std::strcmp(name, "unp_nt") == 0) { i2pc::unproj::g_unp_nt = value; return true; }
   if (std::strcmp(name, "unp_rpt") == 0) { i2pc::unproj::g_unp_rpt = value; return true; }
   if (std::strcmp(name, "sel_windows") == 0) { i2pc::unproj::g_sel_windows = value; return true; }
+  if (std::strcmp(name, "sel_scratch") == 0) { i2pc::unproj::g_sel_scratch = value; return true; }
   if (std::strcmp(name, "sel_parts") == 0) { g_sel_parts = value; return true; }
   if (std::strcmp(name, "sel_lband") == 0) { g_sel_lband = value; return true; }
   if (std::strcmp(name, "sel_rows") == 0) {

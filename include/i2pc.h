@@ -384,6 +384,8 @@ int i2pc_gemm_set_engine(int mode);
  *   "sel_lband"   a single image's windows resolved by the band kernels with a local exchange
  *                 (fine histogram and target-bin compaction over 96 workgroups) instead of one
  *                 workgroup per window: -1 = automatic (from 2 M pixels; default), 0 = off, 1 = on
+ *   "sel_scratch" 1 = every image of a window selection goes to the selection from scratch (the
+ *                 fallback of a missed window; tests and measurement only), default 0
  *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  *   "ln_f2"       1 = the register-resident LayerNorm for dim 384 (k_layernorm2)

@@ -248,7 +248,7 @@ def test_c4_panorama_full_size_bands_and_oracle():
 
 
 def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole", smooth=False, smooth_ksize=5,
-                window=False):
+                window=False, scratch=False):
     """`parts` ranks (threads on their own streams, an in-process all-reduce / all-gather as the
     exchange) each unproject a row band; checks the bands against the whole image.  window:
     the one-sweep window mode (i2pc_unproject_band_w) instead of the histogram levels."""
@@ -298,6 +298,9 @@ def _band_check(dep, img, parts, density, depth_scale=12.0, projection="pinhole"
 
     def run(i):
         try:
+            if scratch:                     # (thread-local knob: every rank selects from scratch)
+                from image_to_pointcloud_amd import ops
+                ops.set_tuning("sel_scratch", 1)
             with torch.cuda.stream(torch.cuda.Stream()):
                 r0, r1 = bands[i]
                 ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -543,6 +546,75 @@ def test_window_selection_matches_histogram_levels_and_oracle(size):
             ep, _ = ref.depth_to_point_cloud(imgs[i], deps[i], density="high", invert=True, depth_scale=10.0,
                                              loop=False)
         assert _same_bits(outs[0][0][i], ep), (k, _first_diff(outs[0][0][i], ep))
+
+
+def test_selection_from_scratch_matches_windows_and_oracle():
+    """The selection from scratch (the fallback of a missed window: k_sel_slow's level 0 and the
+    k_scratch radix levels, grid-wide; knob sel_scratch forces it) gives the window path's bits on
+    every stress map, NaN / Inf fills, constant and all-NaN maps included, and the oracle's."""
+    from image_to_pointcloud_amd import ops
+    g = _geom()
+    dev = torch.device("cuda")
+    H, W = 300, 400
+    cases = _sel_cases()
+    names = list(cases)
+    deps = np.stack([cases[k] for k in names])
+    imgs = np.stack([_rgb(H, W, 170 + i) for i in range(len(names))])
+    outs = []
+    try:
+        for scr in (0, 1):
+            ops.set_tuning("sel_scratch", scr)
+            pb = g.unproject_batch(torch.from_numpy(deps).to(dev), torch.from_numpy(imgs).to(dev), density="high",
+                                   invert=True, depth_scale=10.0)
+            outs.append((pb.xyz.cpu().numpy(), pb.stats.cpu().numpy()))
+    finally:
+        ops.set_tuning("sel_scratch", 0)
+    for i, k in enumerate(names):
+        assert _same_bits(outs[0][1][i], outs[1][1][i]), (k, outs[0][1][i], outs[1][1][i])
+        assert _same_bits(outs[0][0][i], outs[1][0][i]), (k, _first_diff(outs[0][0][i], outs[1][0][i]))
+        with np.errstate(all="ignore"):
+            ep, _ = ref.depth_to_point_cloud(imgs[i], deps[i], density="high", invert=True, depth_scale=10.0,
+                                             loop=False)
+        assert _same_bits(outs[1][0][i], ep), (k, _first_diff(outs[1][0][i], ep))
+
+
+@pytest.mark.parametrize("parts", [1, 3])
+def test_band_selection_from_scratch(parts):
+    """C4 band mode with every rank forced to the selection from scratch (each rank selects the whole
+    image; no exchange): bands still concatenate bit-identically to the whole image."""
+    dep = _smooth_depth(48, 64, 151)
+    dep[3, 4] = np.nan
+    _band_check(dep, _rgb(301, 410, 152), parts, "high", window=True, scratch=True)
+
+
+def test_panorama_selection_from_scratch_time():
+    """One 8192 x 4096 panorama forced to the selection from scratch (~95 ms when one
+    workgroup did it): bit-identical to the window path, and well under 3 ms per call."""
+    from image_to_pointcloud_amd import ops
+    g = _geom()
+    dev = torch.device("cuda")
+    dep = torch.from_numpy(_smooth_depth(518, 1036, 171)).to(dev)[None]
+    img = torch.from_numpy(_rgb(4096, 8192, 172)).to(dev)[None]
+    ws = torch.empty(g.workspace_bytes(1, 4096, 8192), dtype=torch.uint8, device=dev)
+    ref_out = g.unproject_batch(dep, img, density="high", workspace=ws)
+    ref_xyz, ref_stats = ref_out.xyz.cpu().numpy(), ref_out.stats.cpu().numpy()
+    try:
+        ops.set_tuning("sel_scratch", 1)
+        got = g.unproject_batch(dep, img, density="high", workspace=ws)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            g.unproject_batch(dep, img, density="high", workspace=ws, out=got)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 5
+    finally:
+        ops.set_tuning("sel_scratch", 0)
+    print(f"parity {{\"test\": \"panorama_scratch\", \"ms_per_call\": {ms:.3f}}}")
+    assert _same_bits(got.xyz.cpu().numpy(), ref_xyz)
+    assert _same_bits(got.stats.cpu().numpy(), ref_stats)
+    assert ms < 3.0, ms
 
 
 @pytest.mark.parametrize("parts", [1, 2, 3, 4])
