@@ -91,6 +91,8 @@ struct Args {
   float* lnp; bf16_t* cbf; int64_t ldcb;
   const float* lnsh;
   int lnc;
+  int stagger;    // persistent engine: waves 4-7 issue the next K-stage's loads half-way through a step
+                  // (knob "gemm_stagger")
   int dbg_drop;   // diagnostic (I2PC_GEMM_DROP_STORES=1): the persistent engine's output stores are issued to an
                   // empty buffer range (dropped), to measure what the stores cost the next tile's K-loop
 };
@@ -127,15 +129,12 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 }
 
 // ReLU on 8 packed bf16 (pre-activation residual units): clear negative lanes.
+// As signed 16-bit integers the bf16 values with the sign bit set are exactly the negative ones, so
+// max(x, 0) on packed int16 (v_pk_max_i16, one VALU per pair) clears them to +0 and keeps the rest.
 __device__ __forceinline__ bf16x8 relu8(bf16x8 v) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 u = __builtin_bit_cast(u32x4, v);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t neg = (u[i] >> 15) & 0x00010001u;
-    u[i] &= ~(neg * 0xFFFFu);
-  }
-  return __builtin_bit_cast(bf16x8, u);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 x = __builtin_bit_cast(s16x8, v);
+  return __builtin_bit_cast(bf16x8, __builtin_elementwise_max(x, s16x8{0, 0, 0, 0, 0, 0, 0, 0}));
 }
 
 __device__ __forceinline__ void tile_coords(const Args& p, int bid, int& tm, int& tn) {
@@ -494,13 +493,21 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
+  // 8 waves: the second half (the SIMD partners of waves 0-3) issue the next stage half-way through
+  // the step, so one wave's MFMAs cover the other's LDS-DMA issue (the persistent engine's stagger)
+  const bool late = NW == 8 && SUB == 2 && p.stagger && wid >= 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt0 + kt + 1) * KB);
+    if (kt + 1 < nk && !late) stage(cur ^ 1, (kt0 + kt + 1) * KB);
     const uint8_t* sA = smem + cur * STAGE;
     const uint8_t* sW = sA + A_BYTES;
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
+      if (s == 1 && late && kt + 1 < nk) {
+        __builtin_amdgcn_sched_barrier(0);
+        stage(cur ^ 1, (kt0 + kt + 1) * KB);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       bf16x8 wf[RN];
       const int lchunk = 4 * s + fq;
 #pragma unroll
@@ -536,12 +543,17 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   STAMP(3);
 }
 
+// 8-wave GEMM kernels (tile and persistent): waves 4-7 issue each next K-stage half-way through the
+// step (I2PC_GEMM_STAGGER / "gemm_stagger"; bit-identical either way)
+static thread_local int g_stagger = [] { const char* e = getenv("I2PC_GEMM_STAGGER"); return e ? atoi(e) : 1; }();
+
 template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>
 static void launch(const Args& p, hipStream_t s, int splits = 1) {
   Args q = p;
   q.tiles_m = (p.M + BM - 1) / BM;
   q.tiles_n = p.N / BN;
   q.group_m = group_m_for(q.tiles_m);
+  q.stagger = g_stagger;
   const int smem = 2 * (BM + BN) * KB * 2;
   auto kern = k_gemm<BM, BN, WM, WN, KB, CONV, RELU_A>;
   static bool attr = false;
@@ -1019,6 +1031,9 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   auto setup = [&](int tile) {
     int tm, tn;
     grouped(p, tile, tm, tn);
+#ifdef I2PC_STAMPS
+    if (p.dbg_drop & 2) tm = tn = 0;   // diagnostic: every tile computes tile (0, 0) (all loads L2 hits)
+#endif
     nm0 = tm * BM;
     nn0 = tn * BN;
     if constexpr (!CONV) {
@@ -1075,6 +1090,9 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
       kx = kk - ky * p.ck;
       ci0 = k0 - kk * p.cc;
     }
+#ifdef I2PC_STAMPS
+    if (p.dbg_drop & 4) return;   // diagnostic: no operand loads (MFMA + LDS reads on stale LDS)
+#endif
     if constexpr (!CONV) {
 #pragma unroll
       for (int j = 0; j < A_LOADS; ++j)
@@ -1160,17 +1178,30 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
       st_wait += st_b - st_a;
 #endif
       if (kt == 0) PSTAMP(tord, 1);
-      if (kt + 1 < nk) {
-        stage((g + 1) & 1, (kt + 1) * KSTEP, -1);
-      } else if (has_next) {
-        setup(t_next);
-        stage((g + 1) & 1, 0, tpar ^ 1);
-      }
+      // the next K-stage's LDS-DMA issue (8 buffer_load ... lds per wave, ~60-185 cycles of issue each):
+      // with the stagger, waves 4-7 issue theirs half-way through the step, so each SIMD's MFMA pipe
+      // runs one wave's MFMAs while its partner (wave w +- 4) issues loads, instead of both issuing
+      // at the top of the step (buffer (g + 1) & 1 was last read in step g - 1: any point is legal)
+      const bool late = p.stagger && wid >= 4;
+      auto issue_next = [&]() {
+        if (kt + 1 < nk) {
+          stage((g + 1) & 1, (kt + 1) * KSTEP, -1);
+        } else if (has_next) {
+          setup(t_next);
+          stage((g + 1) & 1, 0, tpar ^ 1);
+        }
+      };
+      if (!late) issue_next();
       const uint8_t* sA = smem + (g & 1) * STAGE;
       const uint8_t* sW = sA + A_BYTES;
       if constexpr (!F8) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
+          if (s == 1 && late) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue_next();
+            __builtin_amdgcn_sched_barrier(0);
+          }
           bf16x8 wf[RN];
           const int lchunk = 4 * s + fq;
 #pragma unroll
@@ -1202,6 +1233,11 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
         }
 #pragma unroll
         for (int i = 0; i < RM; ++i) {
+          if (i == RM / 2 && late) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue_next();
+            __builtin_amdgcn_sched_barrier(0);
+          }
           const int row = wm * TM + i * 16 + frow;
           const uint8_t* r = sA + row * ROWB;
           const i32x4 lo = *reinterpret_cast<const i32x4*>(r + ((fq ^ (row & 7)) << 4));
@@ -1743,6 +1779,7 @@ static void launch_p(const Args& p, hipStream_t s) {
   }
   static const int drop = [] { const char* e = getenv("I2PC_GEMM_DROP_STORES"); return e ? atoi(e) : 0; }();
   q.dbg_drop = drop;
+  q.stagger = g_stagger;
   const int tiles = q.tiles_m * q.tiles_n;
   const int grid = std::min(tiles, num_cus());
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
@@ -2395,7 +2432,7 @@ extern "C" int i2pc_gemm_set_engine(int mode) {
 }
 
 // per-host-thread tuning knobs (i2pc_set_tuning; thread_local above): gemm_tail, gemm_bn128,
-// gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_tail160
+// gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_tail160, gemm_stagger
 bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
@@ -2404,5 +2441,6 @@ bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_tile192") == 0) { i2pc::gemm::g_tile192 = value; return true; }
   if (std::strcmp(name, "gemm_lnp_p") == 0) { i2pc::gemm::g_lnp_p = value; return true; }
   if (std::strcmp(name, "gemm_tail160") == 0) { i2pc::gemm::g_tail160 = value; return true; }
+  if (std::strcmp(name, "gemm_stagger") == 0) { i2pc::gemm::g_stagger = value; return true; }
   return false;
 }

@@ -372,6 +372,9 @@ int i2pc_gemm_set_engine(int mode);
  *                 256 x 256 tiles, N % 256 == 0), 0 = on the tile kernel (default: measured faster)
  *   "gemm_tail160" 1 = a persistent GEMM's last partial round as 160 x 256 tiles where 256 x 128
  *                 tiles do not fit one round (DPT-Large FC1)
+ *   "gemm_stagger" 1 = in the 8-wave GEMM kernels waves 4-7 issue the next K-stage's loads half-way
+ *                 through each K-step (their SIMD partners' MFMAs cover the issue), 0 = every wave at
+ *                 the top of the step
  *   "unp_rows"    1 = the row-sweep unprojection kernel
  *   "unp_nt"      1 = non-temporal point stores
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
@@ -390,8 +393,8 @@ int i2pc_gemm_set_engine(int mode);
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  *   "ln_f2"       1 = the register-resident LayerNorm for dim 384 (k_layernorm2)
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _GEMM_SPLIT_TILE / _GEMM_TILE192 /
- * _GEMM_LNP_P / _GEMM_TAIL160 / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR
- * environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
+ * _GEMM_LNP_P / _GEMM_TAIL160 / _GEMM_STAGGER / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR
+ * environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
  * the kernels it captured: re-capture after changing a knob.  An unknown name fails with I2PC_EINVAL
  * and an error message listing every knob. */
 int i2pc_set_tuning(const char* name, int value);

@@ -1,0 +1,13 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+O=gpurun_out/diag6.txt; rm -f $O
+timeout -k 10 300 python -u -m pytest tests/test_gemm_engines_gpu.py tests/test_ln_fold_gpu.py tests/test_padding_gpu.py tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/eng.log 2>&1 || { tail -20 gpurun_out/eng.log; exit 1; }
+tail -1 gpurun_out/eng.log >> $O
+for a in "18464 1024 1024 320 256 lnp" "18464 1024 4096 320 256 lnp" "43840 384 1536 384 192 bf16"; do
+  I2PC_LIB=image_to_pointcloud_amd/libi2pc_stamps.so timeout -k 10 120 python -u tools/stamps_tile.py $a >> $O 2>&1 || exit 1
+done
+timeout -k 10 300 python -u tools/epi_cost.py >> $O 2>&1 || exit 1
+timeout -k 10 600 python -u tools/ab_pipeline.py --variant base: --variant nostagger:gemm_stagger=0 >> $O 2>&1 || exit 1
+timeout -k 10 600 python -u tools/ab_pipeline.py --model depth-anything-v2 --variant base: --variant nostagger:gemm_stagger=0 >> $O 2>&1 || exit 1
+grep -v amdgpu.ids $O
