@@ -91,6 +91,7 @@ struct Args {
   float* lnp; bf16_t* cbf; int64_t ldcb;
   const float* lnsh;
   int lnc;
+  const float* rsh;   // bf16 residual stored relative to rsh[row] (i2pc.h res_shift)
   int stagger;    // persistent engine: waves 4-7 issue the next K-stage's loads half-way through a step
                   // (knob "gemm_stagger")
   int dbg_drop;   // diagnostic (I2PC_GEMM_DROP_STORES=1): the persistent engine's output stores are issued to an
@@ -151,6 +152,13 @@ __device__ __forceinline__ void tile_coords(const Args& p, int bid, int& tm, int
   const int in = tile - g * gsz;
   tm = first + in % gm;
   tn = in / gm;
+}
+
+// v of another lane by a DPP permutation (0xB1: lane ^ 1, 0x4E: lane ^ 2 inside a quad; 0x141: the
+// 8-lane half-row mirror, lane 7 - i)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
 // ---------------------------------------------------------------------------
@@ -253,8 +261,17 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       } else {
         const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
+        if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
+          const float rs = p.rsh[orow];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) { v[2 * t] += __uint_as_float(q[t] << 16); v[2 * t + 1] += __uint_as_float(q[t] & 0xffff0000u); }
+          for (int t = 0; t < 4; ++t) {
+            v[2 * t] += __uint_as_float(q[t] << 16) + rs;
+            v[2 * t + 1] += __uint_as_float(q[t] & 0xffff0000u) + rs;
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) { v[2 * t] += __uint_as_float(q[t] << 16); v[2 * t + 1] += __uint_as_float(q[t] & 0xffff0000u); }
+        }
       }
     }
     if (p.res2) {
@@ -264,10 +281,12 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
 #pragma unroll
       for (int t = 0; t < 4; ++t) { v[2 * t] += __uint_as_float(q[t] << 16); v[2 * t + 1] += __uint_as_float(q[t] & 0xffff0000u); }
     }
-    if (p.c_f32) {
-      float* c = static_cast<float*>(p.C) + off;
-      *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    if (p.c_f32 || p.lnp) {
+      if (p.c_f32) {
+        float* c = static_cast<float*>(p.C) + off;
+        *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
       if constexpr (LPR % 4 == 0) {
         if (p.lnp) {
           // LayerNorm producer: the bf16 copy of out - shift[m], and (mean, M2) of each 64-column
@@ -282,18 +301,21 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
           o.z = (uint32_t)f2bf(u[4]) | ((uint32_t)f2bf(u[5]) << 16);
           o.w = (uint32_t)f2bf(u[6]) | ((uint32_t)f2bf(u[7]) << 16);
           *reinterpret_cast<uint4*>(p.cbf + (int64_t)m * p.ldcb + n) = o;
+          // chunk sums across the row's lanes by DPP (one VALU each) instead of ds_bpermute round trips:
+          // lane ^ 1, lane ^ 2 inside a quad, then the mirrored lane of the 8-lane group (7 - lane: the
+          // other quad, whose lanes all hold that quad's sum by then) -- the same operands as xor 4
           float sm = ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
-          sm += __shfl_xor(sm, 1);
-          sm += __shfl_xor(sm, 2);
+          sm += dpp_f<0xB1>(sm);
+          sm += dpp_f<0x4E>(sm);
           const bool c64 = LPR % 8 == 0 && p.lnc == 64;   // the host allows 64 only where LPR % 8 == 0
-          if (c64) sm += __shfl_xor(sm, 4);
+          if (c64) sm += dpp_f<0x141>(sm);
           const float mean = sm * (c64 ? 1.0f / 64.0f : 1.0f / 32.0f);
           float q = 0.f;
 #pragma unroll
           for (int t = 0; t < 8; ++t) q = __builtin_fmaf(u[t] - mean, u[t] - mean, q);
-          q += __shfl_xor(q, 1);
-          q += __shfl_xor(q, 2);
-          if (c64) q += __shfl_xor(q, 4);
+          q += dpp_f<0xB1>(q);
+          q += dpp_f<0x4E>(q);
+          if (c64) q += dpp_f<0x141>(q);
           if ((c8 & (c64 ? 7 : 3)) == 0) {
             const int cs = c64 ? 6 : 5;
             *reinterpret_cast<float2*>(p.lnp + ((int64_t)m * (p.N >> cs) + (n >> cs)) * 2) = make_float2(mean, q);
@@ -2326,11 +2348,19 @@ static int make_args(const i2pc_gemm_desc* d, gemm::Args& p) {
   p.lnp = d->ln_part; p.cbf = static_cast<gemm::bf16_t*>(d->c_bf16); p.ldcb = d->ldc_bf16;
   p.lnsh = d->ln_part ? d->ln_shift : nullptr;
   p.lnc = d->ln_chunk ? d->ln_chunk : 64;
+  p.rsh = d->res_shift;
   if (d->ln_rows) I2PC_REQUIRE(d->col_sum, "gemm: ln_rows needs col_sum");
+  if (d->res_shift) I2PC_REQUIRE(d->res && !d->res_f32 && d->ln_part, "gemm: res_shift needs a bf16 res in a producer call");
+  if (d->ln_part && !d->c_f32) {
+    // bf16 residual stream: C is the shifted bf16 copy itself
+    I2PC_REQUIRE(!d->c_bf16 || d->c_bf16 == d->c, "gemm: a bf16-output producer writes its copy to c (c_bf16 NULL or c)");
+    p.cbf = static_cast<gemm::bf16_t*>(d->c);
+    p.ldcb = d->ldc;
+  }
   if (d->ln_part) {
     I2PC_REQUIRE(p.lnc == 32 || p.lnc == 64, "gemm: ln_chunk=%d must be 0, 32 or 64", d->ln_chunk);
-    I2PC_REQUIRE(d->c_bf16 && d->c_f32 && d->n % p.lnc == 0 && d->ldc_bf16 % 8 == 0 && d->ldc_bf16 >= d->n,
-                 "gemm: ln_part needs c_bf16 (ldc_bf16 %% 8, >= n), an fp32 output and n %% ln_chunk == 0");
+    I2PC_REQUIRE(p.cbf && d->n % p.lnc == 0 && p.ldcb % 8 == 0 && p.ldcb >= d->n,
+                 "gemm: ln_part needs c_bf16 (ldc_bf16 %% 8, >= n) or a bf16 output, and n %% ln_chunk == 0");
     I2PC_REQUIRE(d->out_group == 0 && d->out_offset == 0 && d->convt_s == 0, "gemm: ln_part needs a linear output row map");
     I2PC_REQUIRE(!d->ln_rows, "gemm: ln_part and ln_rows in one call");
   }

@@ -272,6 +272,34 @@ __global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ 
   }
 }
 
+// LayerNorm of a bf16 row block from its row statistics (i2pc_ln_apply): y = bf16(gamma * (rs.x * x +
+// rs.y) + beta) with rs = (rstd, -rstd * mean) of the rows as ln_rowstats gives them (x = the shifted
+// bf16 residual stream: the statistics were taken of the same shifted values).  8 columns per thread
+// (one 16-B load and store), grid-stride over rows x dim / 8.
+__global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, int64_t ldx8, const float2* __restrict__ rs,
+                                                  const float4* __restrict__ gamma, const float4* __restrict__ beta,
+                                                  int rows, int d8, uint4* __restrict__ y, int64_t ldy8) {
+  const int64_t n = (int64_t)rows * d8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int r = (int)(i / d8);
+    const int c = (int)(i - (int64_t)r * d8);
+    const uint4 v = x[r * ldx8 + c];
+    const float2 s = rs[r];
+    const float4 g0 = gamma[2 * c], g1 = gamma[2 * c + 1], b0 = beta[2 * c], b1 = beta[2 * c + 1];
+    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float lo = __builtin_fmaf(g[2 * t], __builtin_fmaf(__uint_as_float(q[t] << 16), s.x, s.y), b[2 * t]);
+      const float hi = __builtin_fmaf(g[2 * t + 1], __builtin_fmaf(__uint_as_float(q[t] & 0xffff0000u), s.x, s.y), b[2 * t + 1]);
+      o[t] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    y[r * ldy8 + c] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 static int grid_for(int64_t work, int per_block = 256) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((work + per_block - 1) / per_block, 256 * 16));
 }
@@ -299,6 +327,23 @@ extern "C" int i2pc_ln_rowstats_w(const float* part, int rows, int parts, int ch
                      reinterpret_cast<const float2*>(part), rows, parts, (float)chunk_cols, eps,
                      reinterpret_cast<float2*>(rows_out), shift_in, shift_out);
   return check_launch("ln_rowstats");
+}
+
+extern "C" int i2pc_ln_apply(const void* x, int64_t ldx, const float* rows_stats, const float* gamma, const float* beta,
+                             int rows, int dim, void* y, int64_t ldy, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(x && rows_stats && gamma && beta && y, "NULL pointer");
+  I2PC_REQUIRE(rows > 0 && dim > 0 && dim % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && ldx >= dim && ldy >= dim,
+               "ln_apply: dim, ldx, ldy must be multiples of 8 (ld >= dim)");
+  I2PC_REQUIRE((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 == 0 &&
+                   (reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) % 16 == 0,
+               "ln_apply: 16-byte aligned operands");
+  const int d8 = dim / 8;
+  hipLaunchKernelGGL(k_ln_apply, dim3(grid_for((int64_t)rows * d8)), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint4*>(x), ldx / 8, reinterpret_cast<const float2*>(rows_stats),
+                     reinterpret_cast<const float4*>(gamma), reinterpret_cast<const float4*>(beta), rows, d8,
+                     static_cast<uint4*>(y), ldy / 8);
+  return check_launch("ln_apply");
 }
 
 extern "C" int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out,

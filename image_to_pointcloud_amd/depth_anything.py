@@ -337,7 +337,8 @@ class DepthAnythingModel:
         e = lambda shape, dt=torch.bfloat16: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
         b = dict(x=e((M, D), torch.float32), ln=e((M, D)), qkv=e((M, 3 * D)), att=e((M, D)), mlp=e((M, s.mlp)),
                  hs=[e((M, D)) for _ in s.out_indices],
-                 part=e((M, D // LN_CHUNK, 2), torch.float32), rs=e((M, 2), torch.float32), shift=e((M,), torch.float32))
+                 part=e((M, D // LN_CHUNK, 2), torch.float32), rs=e((M, 2), torch.float32), shift=e((M,), torch.float32),
+                 shift2=e((M,), torch.float32))
         b["ln_fold"] = dpt.LN_FOLD and D % LN_CHUNK == 0 and self._ln_fold_ok(b, M)
         self._bufs[key] = b
         return b
@@ -362,6 +363,12 @@ class DepthAnythingModel:
                  name(b["ln"], L["w_1_f"], b["mlp"], **dict(consumer, col_sum=L["s_1"].data_ptr(), act=1)),
                  name(b["att"], L["w_o"], b["x"], **producer),
                  name(b["mlp"], L["w_2"], b["x"], **producer)]
+        if dpt.BF16_STREAM:   # bf16-output producers (layer 0's attention-out reads the fp32 embeddings)
+            stream = dict(res=b["ln"].data_ptr(), res_f32=0, ldr=D, ln_part=b["part"].data_ptr(), ln_chunk=LN_CHUNK,
+                          ln_shift=b["shift"].data_ptr(), res_shift=b["shift2"].data_ptr())
+            names += [name(b["att"], L["w_o"], b["ln"], **dict(producer, c_bf16=0, ldc_bf16=0)),
+                      name(b["att"], L["w_o"], b["ln"], **stream),
+                      name(b["mlp"], L["w_2"], b["ln"], **stream)]
         return "invalid" not in names
 
     # ------------------------------------------------------------------ forward
@@ -419,6 +426,8 @@ class DepthAnythingModel:
         nl = len(self.layers)
         hs_i = 0
         a_in = None
+        if dpt.BF16_STREAM:
+            return self._encoder_stream(buf, B, T, scale)
         for i, L in enumerate(self.layers):
             if a_in is None:      # layer 0: norm1 of the embeddings (its row means: the first shift)
                 ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"], mean_out=buf["shift"])
@@ -444,6 +453,37 @@ class DepthAnythingModel:
                 ops.linear(h, L["w_2"], bias=L["b_2"], res=x, out=x)
             if (i + 1) in s.out_indices:
                 ops.layernorm(x, self.ln_g, self.ln_b, s.eps, out=buf["hs"][hs_i])    # backbone LayerNorm
+                hs_i += 1
+
+    def _encoder_stream(self, buf, B, T, scale):
+        """The folded encoder on the shifted bf16 residual stream (dpt.BF16_STREAM; i2pc.h "bf16
+        residual stream"): attention-out and FC2 read buf["ln"] (stored relative to one shift buffer)
+        and write it back in place relative to the other, the latest LayerNorm mean; the backbone
+        LayerNorm of a kept hidden state is applied from FC2's row statistics (ops.ln_apply) instead of
+        a LayerNorm pass over an fp32 stream."""
+        s = self.spec
+        sh0, sh1 = buf["shift"], buf["shift2"]
+        hs_i = 0
+        res, rsh = buf["x"], None          # layer 0: the residual is the fp32 embeddings
+        for i, L in enumerate(self.layers):
+            if i == 0:                     # norm1 of the embeddings (its row means: the first shift)
+                ln = ops.layernorm(buf["x"], L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"], mean_out=sh0)
+                qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
+            else:
+                qkv = ops.linear(buf["ln"], L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
+                                 out=buf["qkv"])
+            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            ops.linear(att, L["w_o"], bias=L["b_o"], res=res, res_shift=rsh, out=buf["ln"], ln_part=buf["part"],
+                       ln_shift=sh0, ln_chunk=LN_CHUNK)
+            ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=sh0, shift_out=sh1, chunk=LN_CHUNK)
+            h = ops.linear(buf["ln"], L["w_1_f"], bias=L["b_1_f"], act="gelu", ln_rows=buf["rs"], col_sum=L["s_1"],
+                           out=buf["mlp"])
+            ops.linear(h, L["w_2"], bias=L["b_2"], res=buf["ln"], res_shift=sh0, out=buf["ln"], ln_part=buf["part"],
+                       ln_shift=sh1, ln_chunk=LN_CHUNK)
+            ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=sh1, shift_out=sh0, chunk=LN_CHUNK)
+            res, rsh = buf["ln"], sh1
+            if (i + 1) in s.out_indices:   # backbone LayerNorm (same eps) from the same row statistics
+                ops.ln_apply(buf["ln"], buf["rs"], self.ln_g, self.ln_b, out=buf["hs"][hs_i])
                 hs_i += 1
 
     def _reassemble(self, j, hs, B, gh, gw):

@@ -37,6 +37,11 @@ FUSED_HEAD = True
 # weights with the normalisation applied in their epilogue -- no separate LayerNorm pass
 # (47 of the 48 in DPT-Large; layer 0's LN1 follows the embeddings).  False: LN kernels.
 LN_FOLD = True
+# With the fold: the residual stream between the encoder GEMMs is the shifted bf16 copy itself
+# (i2pc.h "bf16 residual stream": attention-out / FC2 read it as res + res_shift and write it back
+# as bf16(x - ln_shift)), as in the torch-bf16 forward, instead of an fp32 stream plus a bf16 copy:
+# those two epilogues move 76 MB instead of 189 MB per call at C2.  False: the fp32 stream.
+BF16_STREAM = __import__("os").environ.get("I2PC_BF16_STREAM", "1") != "0"
 
 from . import ops
 
@@ -315,7 +320,8 @@ class DPTDepthModel:
         e = lambda shape, dt=torch.bfloat16: torch.empty(shape, dtype=dt, device=dev)   # noqa: E731
         b = dict(x=e((M, D), torch.float32), ln=e((M, D)), qkv=e((M, 3 * D)), att=e((M, D)), mlp=e((M, s.mlp)),
                  hs=[e((M, D)) for _ in s.out_indices], rb=e((B, D), torch.float32), tok=e((B * gh * gw, D)),
-                 part=e((M, D // 64, 2), torch.float32), rs=e((M, 2), torch.float32), shift=e((M,), torch.float32))
+                 part=e((M, D // 64, 2), torch.float32), rs=e((M, 2), torch.float32), shift=e((M,), torch.float32),
+                 shift2=e((M,), torch.float32))
         b["ln_fold"] = LN_FOLD and D % 64 == 0 and self._ln_fold_ok(b, M)
         self._bufs[(B, gh, gw)] = b
         return b
@@ -341,6 +347,12 @@ class DPTDepthModel:
                  name(b["ln"], L["w_1_f"], b["mlp"], **dict(consumer, col_sum=L["s_1"].data_ptr(), act=1)),
                  name(b["att"], L["w_o"], b["x"], **producer),
                  name(b["mlp"], L["w_2"], b["x"], **producer)]
+        if BF16_STREAM:   # bf16-output producers (layer 0's attention-out still reads the fp32 embeddings)
+            stream = dict(res=b["ln"].data_ptr(), res_f32=0, ldr=D, ln_part=b["part"].data_ptr(),
+                          ln_shift=b["shift"].data_ptr(), res_shift=b["shift2"].data_ptr())
+            names += [name(b["att"], L["w_o"], b["ln"], **dict(producer, c_bf16=0, ldc_bf16=0)),
+                      name(b["att"], L["w_o"], b["ln"], **stream),
+                      name(b["mlp"], L["w_2"], b["ln"], **stream)]
         return "invalid" not in names
 
     # ------------------------------------------------------------------ forward
@@ -384,6 +396,9 @@ class DPTDepthModel:
                 qkv = ops.linear(a_in, L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
                                  out=buf["qkv"])
             att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            if BF16_STREAM:
+                a_in = self._stream_layer(i, L, att, a_in, buf)
+                continue
             # the residual's bf16 copy is stored minus the previous LayerNorm's row mean (shift),
             # so rows whose mean is large against their spread keep their precision
             ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x, ln_part=buf["part"], out_bf16=buf["ln"],
@@ -414,6 +429,38 @@ class DPTDepthModel:
         return ops.head_out(t2, self.w_h4, self.b_h4)
 
     __call__ = forward
+
+    def _stream_layer(self, i, L, att, a_in, buf):
+        """The rest of encoder layer i on the shifted bf16 residual stream (BF16_STREAM): attention-out
+        and FC2 read the stream (a_in, stored relative to the shift buf["_rsh"]; layer 0: the fp32
+        embeddings) and write it back relative to the latest LayerNorm mean; ln_rowstats alternates
+        between the two shift buffers (the one the stream is stored relative to is never overwritten
+        while it is read).  Layers whose hidden state the neck reads store it unshifted (shift 0).
+        Returns the stream after FC2 (the next QKV's A)."""
+        s = self.spec
+        kept = i in s.out_indices
+        sh = (buf["shift"], buf["shift2"])
+        if a_in is None:          # layer 0: the residual is the fp32 embeddings; LN1's means are in shift
+            res, rsh, cur = buf["x"], None, 0
+        else:
+            res, rsh, cur = a_in, buf["_rsh"], buf["_cur"]
+        # attention-out: stream -> buf["ln"], relative to sh[cur] (LN1's mean)
+        ops.linear(att, L["w_o"], bias=L["b_o"], res=res, res_shift=rsh, out=buf["ln"], ln_part=buf["part"],
+                   ln_shift=sh[cur])
+        ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=sh[cur], shift_out=sh[cur ^ 1])
+        h = ops.linear(buf["ln"], L["w_1_f"], bias=L["b_1_f"], act="gelu", ln_rows=buf["rs"], col_sum=L["s_1"],
+                       out=buf["mlp"])
+        # FC2: stream -> buf["ln"] in place relative to sh[cur ^ 1] (LN2's mean), or a kept hidden state
+        if kept:
+            dst, osh = buf["hs"][s.out_indices.index(i)], None
+        else:
+            dst, osh = buf["ln"], sh[cur ^ 1]
+        ops.linear(h, L["w_2"], bias=L["b_2"], res=buf["ln"], res_shift=sh[cur], out=dst, ln_part=buf["part"],
+                   ln_shift=osh)
+        if i + 1 < len(self.layers):
+            ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=osh, shift_out=sh[cur])
+        buf["_rsh"], buf["_cur"] = osh, cur
+        return dst
 
     def _reassemble(self, j, hs, B, buf):
         s, st = self.spec, self.stages[j]

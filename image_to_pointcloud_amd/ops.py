@@ -35,7 +35,7 @@ class GemmDesc(ctypes.Structure):
         ("out_group", c_int32), ("out_group_stride", c_int32), ("out_offset", c_int32),
         ("convt_s", c_int32), ("convt_h", c_int32), ("convt_w", c_int32), ("convt_c", c_int32),
         ("ln_rows", c_void_p), ("col_sum", c_void_p), ("ln_part", c_void_p), ("c_bf16", c_void_p),
-        ("ldc_bf16", c_int64), ("ln_shift", c_void_p), ("ln_chunk", c_int32),
+        ("ldc_bf16", c_int64), ("ln_shift", c_void_p), ("ln_chunk", c_int32), ("res_shift", c_void_p),
     ]
 
 
@@ -49,6 +49,8 @@ _lib.register("i2pc_ln_rowstats", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.
                                                  c_void_p, c_void_p, c_void_p])
 _lib.register("i2pc_ln_rowstats_w", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                                    c_void_p, c_void_p, c_void_p, c_void_p])
+_lib.register("i2pc_ln_apply", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, ctypes.c_int,
+                                              ctypes.c_int, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_layernorm_stats", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
                                                      ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p, c_void_p])
 _lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_void_p, ctypes.c_float,
@@ -158,8 +160,10 @@ def gemm_bytes(d: GemmDesc, esz: float = 2.0, c_esz: float = None) -> float:
         b += M * N * (4.0 if d.res_f32 else 2.0)
     if d.res2:
         b += M * N * 2.0
-    if d.ln_part:          # LN-fold producer: the bf16 copy + chunk partials
-        b += M * N * 2.0 + M * (N // (d.ln_chunk or 64)) * 8.0
+    if d.ln_part:          # LN-fold producer: the bf16 copy (unless it is the output) + chunk partials
+        b += (M * N * 2.0 if d.c_f32 else 0.0) + M * (N // (d.ln_chunk or 64)) * 8.0
+    if d.res_shift:
+        b += M * 4.0
     if d.ln_rows:          # LN-fold consumer: row scales + column sums
         b += M * 8.0 + N * 4.0
     return b
@@ -236,7 +240,7 @@ def _linear_padded(x, w, bias, act, res, res2, out, out_f32, rows):
 def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=False,
            a_map=(0, 0, 0), out_map=(0, 0, 0), rows=None, row_bias=None, row_bias_group=1,
            table=None, table_rows=1, ldc=None, ln_rows=None, col_sum=None, ln_part=None, out_bf16=None,
-           ln_shift=None, ln_chunk=64):
+           ln_shift=None, ln_chunk=64, res_shift=None):
     """out = act(x @ w.T + bias + row_bias + table) + res + res2.
 
     x: bf16 [*, K] (row stride x.stride(0)); w: bf16 [N, K]; rows = M (defaults to x rows).
@@ -244,7 +248,9 @@ def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=Fal
     LayerNorm fold (i2pc.h): ln_rows fp32 [M, 2] (ln_rowstats) + col_sum fp32 [N] make this the
     consumer (out = act(rs.x * acc + rs.y * col_sum + bias)); ln_part fp32 [M, N / ln_chunk, 2] +
     out_bf16 bf16 [M, N] make an fp32-output call the producer (of out - ln_shift[row] when given;
-    ln_chunk 64 or 32 columns per partial).
+    ln_chunk 64 or 32 columns per partial).  With a bf16 `out` and no out_bf16 the producer's only
+    output is out = bf16(value - ln_shift[row]) (the shifted bf16 residual stream); a bf16 `res` is
+    then read as res + res_shift[row] (the shift it was stored relative to).
     """
     torch = _torch()
     _check(x, torch.bfloat16, "x")
@@ -283,13 +289,21 @@ def linear(x, w, bias=None, act=None, res=None, res2=None, out=None, out_f32=Fal
         _check(out_bf16, torch.bfloat16, "out_bf16")
         if ln_chunk not in (32, 64):
             raise ValueError(f"ln_chunk={ln_chunk} must be 32 or 64")
-        if ln_part.numel() < 2 * M * (N // ln_chunk) or out_bf16.shape[0] < M or out_bf16.shape[-1] < N:
+        if out_bf16 is None and out.dtype != torch.bfloat16:
+            raise ValueError("ln_part: an fp32 out needs out_bf16 (or pass a bf16 out: the shifted residual stream)")
+        cb = out if out_bf16 is None else out_bf16
+        if ln_part.numel() < 2 * M * (N // ln_chunk) or cb.shape[0] < M or cb.shape[-1] < N:
             raise ValueError("ln_part / out_bf16 too small for the call")
-        d.ln_part, d.c_bf16, d.ldc_bf16 = _p(ln_part), _p(out_bf16), out_bf16.stride(0)
+        if out_bf16 is not None:
+            d.c_bf16, d.ldc_bf16 = _p(out_bf16), out_bf16.stride(0)
+        d.ln_part = _p(ln_part)
         d.ln_chunk = ln_chunk
         if ln_shift is not None:
             _check(ln_shift, torch.float32, "ln_shift")
             d.ln_shift = _p(ln_shift)
+    if res_shift is not None:
+        _check(res_shift, torch.float32, "res_shift")
+        d.res_shift = _p(res_shift)
     gemm(d)
     return out
 
@@ -309,6 +323,21 @@ def ln_rowstats(part, eps, out=None, shift_in=None, shift_out=None, chunk=64):
     with _Timed("k_ln_rowstats", 0.0, nb):
         _lib.call("i2pc_ln_rowstats_w", _p(part), M, P, int(chunk), float(eps), _p(out), _p(shift_in), _p(shift_out),
                   _stream())
+    return out
+
+
+def ln_apply(x, rows_stats, gamma, beta, out=None):
+    """LayerNorm of bf16 rows x [M, D] from ln_rowstats' (rstd, -rstd * mean) rows (i2pc_ln_apply):
+    bf16(gamma * (rstd * x - rstd * mean) + beta)."""
+    torch = _torch()
+    _check(x, torch.bfloat16, "x")
+    _check(rows_stats, torch.float32, "rows_stats")
+    M, D = x.shape
+    if out is None:
+        out = torch.empty((M, D), dtype=torch.bfloat16, device=x.device)
+    with _Timed("k_ln_apply", 0.0, M * D * 4.0 + M * 8.0):
+        _lib.call("i2pc_ln_apply", _p(x), x.stride(0), _p(rows_stats), _p(gamma), _p(beta), M, D, _p(out),
+                  out.stride(0), _stream())
     return out
 
 

@@ -252,11 +252,19 @@ typedef struct i2pc_gemm_desc {
    *   computes act(rs.x * acc + rs.y * col_sum[n] + bias[n]) with rs = ln_rows float2 [m] =
    *   (rstd, -rstd * mean) (i2pc_ln_rowstats), col_sum fp32 [n] = sum_k of W's bf16 row, bias =
    *   b + W beta: the LayerNorm of A's rows applied after the product.  Dense A, bf16 output, no
-   *   residuals / row bias / table (the persistent engine runs it). */
+   *   residuals / row bias / table (the persistent engine runs it).
+   * bf16 residual stream (a producer with c_f32 = 0; c_bf16 NULL or == c): the output C itself is
+   *   bf16(out - ln_shift[row]) -- the shifted residual stream the next consumer reads as A and the
+   *   next producer reads as res -- and no fp32 copy is written.  A bf16 res is then taken as
+   *   res[row][n] + res_shift[row] when res_shift (fp32 [m]) is set: the shift it was stored
+   *   relative to (may differ from ln_shift, which tracks the latest LayerNorm mean).  The torch-bf16
+   *   forward keeps its residual stream in bf16 too; the shift keeps each row's rounding at its
+   *   spread rather than its mean. */
   const float* ln_rows; const float* col_sum;
   float* ln_part; void* c_bf16; int64_t ldc_bf16;
   const float* ln_shift;
   int32_t ln_chunk;
+  const float* res_shift;
 } i2pc_gemm_desc;
 
 /* LayerNorm row statistics from i2pc_gemm's producer partials: rows_out float2 [rows] =
@@ -267,6 +275,13 @@ typedef struct i2pc_gemm_desc {
  * means, shift_in + mean (the next producer's shift; may alias shift_in).  parts <= 64. */
 int i2pc_ln_rowstats(const float* part, int rows, int parts, float eps, float* rows_out, const float* shift_in,
                      float* shift_out, void* stream);
+/* LayerNorm of bf16 rows from their statistics: y[r][c] = bf16(gamma[c] * (rs.x * x[r][c] + rs.y) +
+ * beta[c]) with rows_stats float2 [rows] = (rstd, -rstd * mean) from i2pc_ln_rowstats of the producer
+ * that wrote x (x may be the shifted bf16 residual stream: the statistics are of the same shifted
+ * values).  E.g. Depth-Anything's backbone LayerNorm of a kept hidden state
+ * (modeling_dinov2.py: `self.layernorm(hidden_state)` on out_features).  dim, ldx, ldy % 8 == 0. */
+int i2pc_ln_apply(const void* x, int64_t ldx, const float* rows_stats, const float* gamma, const float* beta,
+                  int rows, int dim, void* y, int64_t ldy, void* stream);
 /* The same for chunk_cols-column chunks (32 or 64; i2pc_ln_rowstats = chunk_cols 64). */
 int i2pc_ln_rowstats_w(const float* part, int rows, int parts, int chunk_cols, float eps, float* rows_out,
                        const float* shift_in, float* shift_out, void* stream);

@@ -222,3 +222,89 @@ def test_depth_anything_ln_fold_matches_unfused_forward():
     from test_dpt_gpu import _report
     _report("depth-anything-v2 ln-fold vs LN kernels", rel_l2=rel)
     assert rel <= 2e-2, rel
+
+
+@pytest.mark.parametrize("M,N,K,C,shifted", [(18464, 1024, 1024, 64, True), (18464, 1024, 4096, 64, False),
+                                             (43840, 384, 1536, 32, True), (1000, 384, 384, 32, True)])
+def test_bf16_stream_producer(M, N, K, C, shifted):
+    """The bf16 residual stream (i2pc.h): a producer with a bf16 output reads res + res_shift[row] and
+    writes only bf16(out - ln_shift[row]) (in place) plus the chunk partials of out - ln_shift.  Against
+    the fp32 producer on the same values: the stored stream is exactly the bf16 copy that one writes
+    (both round out - shift once), the partials are the same numbers."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M + 3 * K + C)
+    a = _rand((M, K), g).to(torch.bfloat16).to(dev)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = _rand((N,), g, 0.1).to(torch.float32).to(dev)
+    s_in = (_rand((M,), g) * 5).to(torch.float32).to(dev)
+    s_out = (_rand((M,), g) * 5).to(torch.float32).to(dev) if shifted else None
+    r = (_rand((M, N), g) + 0.5).to(torch.bfloat16).to(dev)      # the stream, stored relative to s_in
+    # reference: the fp32 producer on x = r + s_in
+    x = r.float() + s_in[:, None]
+    part_ref = torch.empty((M, N // C, 2), dtype=torch.float32, device=dev)
+    yb_ref = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    ops.linear(a, w, bias=b, res=x, out=x, ln_part=part_ref, out_bf16=yb_ref, ln_shift=s_out, ln_chunk=C)
+    part = torch.empty((M, N // C, 2), dtype=torch.float32, device=dev)
+    ops.linear(a, w, bias=b, res=r, res_shift=s_in, out=r, ln_part=part, ln_shift=s_out, ln_chunk=C)
+    torch.cuda.synchronize()
+    assert torch.equal(r, yb_ref), "the bf16 stream is not bf16(out - ln_shift)"
+    assert torch.equal(part, part_ref), "chunk partials differ from the fp32 producer's"
+
+
+def test_ln_apply_matches_layernorm():
+    """i2pc_ln_apply from producer row statistics == nn.LayerNorm of the same (shifted) rows within the
+    bf16 output rounding (the DA-v2 backbone LayerNorm of a kept hidden state on the bf16 stream)."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(11)
+    M, N, C = 5000, 384, 32
+    x = (_rand((M, N), g) * 2 + 0.3).to(torch.bfloat16).to(dev)
+    xd = x.double()
+    xc = xd.view(M, N // C, C)
+    mean_c = xc.mean(-1)
+    part = torch.stack([mean_c, ((xc - mean_c[..., None]) ** 2).sum(-1)], -1).float()
+    rs = ops.ln_rowstats(part, 1e-6, chunk=C)
+    gamma = (_rand((N,), g) + 1).float().to(dev)
+    beta = _rand((N,), g, 0.2).float().to(dev)
+    y = ops.ln_apply(x, rs, gamma, beta)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.layer_norm(xd, (N,), gamma.double(), beta.double(), 1e-6)
+    err = (y.double() - ref).abs().max().item()
+    assert err <= 2.0 ** -7 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("model", ["dpt-large", "depth-anything-v2"])
+def test_bf16_stream_forward_matches_fp32_stream(model):
+    """The folded encoder on the bf16 residual stream (dpt.BF16_STREAM) against the fp32 stream on the
+    same input: within the bf16 noise of each other (both are checked against transformers fp32 in
+    test_dpt_gpu.py / test_depth_anything_gpu.py, whose bounds are relative to the torch-bf16 control,
+    which keeps its residual stream in bf16 too)."""
+    from image_to_pointcloud_amd import dpt
+    dev = torch.device("cuda")
+    if model == "dpt-large":
+        from image_to_pointcloud_amd.dpt import DPT_LARGE as spec, DPTDepthModel as Model, synthetic_state_dict
+        B, gh, gw, K = 2, 24, 24, 768
+    else:
+        from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL as spec, DepthAnythingModel as Model
+        from image_to_pointcloud_amd.depth_anything import synthetic_state_dict
+        B, gh, gw, K = 2, 37, 37, 640
+    net = Model(spec, synthetic_state_dict(spec, 0), dev)
+    g = torch.Generator().manual_seed(8)
+    patches = torch.randn((B * gh * gw, K), generator=g).to(torch.bfloat16).to(dev)
+    old = dpt.BF16_STREAM
+    try:
+        out = []
+        for on in (True, False):
+            dpt.BF16_STREAM = on
+            net._bufs.clear()
+            out.append(net(patches, B, gh, gw).clone())
+            assert net.buffers(B, gh, gw)["ln_fold"]
+    finally:
+        dpt.BF16_STREAM = old
+        net._bufs.clear()
+    torch.cuda.synchronize()
+    rel = ((out[0] - out[1]).norm() / out[1].norm()).item()
+    from test_dpt_gpu import _report
+    _report(f"{model} bf16 stream vs fp32 stream", rel_l2=rel)
+    assert rel <= 2e-2, rel

@@ -38,6 +38,8 @@ for K in (1024, 4096):
             x, w, bias=b, res=res, out=res, ln_part=part, out_bf16=ln, ln_shift=shift)),
         "LN producer (persistent 160)": lambda: (ops.set_tuning("gemm_lnp_p", 1), ops.linear(
             x, w, bias=b, res=res, out=res, ln_part=part, out_bf16=ln, ln_shift=shift)),
+        "bf16-stream producer (tile)": lambda: (ops.set_tuning("gemm_lnp_p", 0), ops.linear(
+            x, w, bias=b, res=ln, res_shift=shift, out=ln, ln_part=part, ln_shift=shift)),
     }
     t = {k: [] for k in variants}
     for _ in range(5):

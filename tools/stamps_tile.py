@@ -1,6 +1,6 @@
 """Diagnostic: per-block s_memtime phases of the tile GEMM kernel k_gemm (I2PC_LIB=.../libi2pc_stamps.so).
 
-usage: I2PC_LIB=image_to_pointcloud_amd/libi2pc_stamps.so python tools/stamps_tile.py M N K BM BN [bf16|lnp]
+usage: I2PC_LIB=image_to_pointcloud_amd/libi2pc_stamps.so python tools/stamps_tile.py M N K BM BN [bf16|lnp|lnpbf]
 (lnp: fp32 residual in place + the LayerNorm-fold producer, the DPT-Large O / FC2 epilogue)
 Prints the per-block start / first-stage wait / K-loop / epilogue phase 1 / phase 2 medians and the
 distribution of block end times (cycles of s_memtime, the shader clock)."""
@@ -18,6 +18,10 @@ if mode == "lnp":
     out = torch.randn(m, n, device=dev)
     kw = dict(res=out, ln_part=torch.empty(m, n // 64, 2, device=dev),
               out_bf16=torch.empty(m, n, dtype=torch.bfloat16, device=dev), ln_shift=torch.zeros(m, device=dev))
+elif mode == "lnpbf":   # the bf16 residual stream: res = out (bf16, in place) + res_shift, bf16 shifted output
+    out = torch.randn(m, n, device=dev).to(torch.bfloat16)
+    kw = dict(res=out, res_shift=torch.zeros(m, device=dev), ln_part=torch.empty(m, n // 64, 2, device=dev),
+              ln_shift=torch.zeros(m, device=dev))
 else:
     out = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
     kw = {}
