@@ -168,15 +168,41 @@ __device__ __forceinline__ float dpp_f(float v) {
 // the wave's LDS region (16-B units XOR-swizzled by row).  Phase 2 (row layout):
 // each lane owns 8 consecutive columns of one row: + res + res2 with 16/32-B loads,
 // then one 16-B (bf16) or 2 x 16-B (fp32) store; a wave writes whole 128-B lines.
-template <int RM, int RN>
-__device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int ni, int mrow0,
+template <int RM, int RN, int NI>
+__device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int mrow0,
                                               int ncol0, float* lds) {
+  constexpr int ni = NI;
   constexpr int TN = RN * 16;
   constexpr int U = TN / 4;                 // 16-B units per LDS row
   constexpr int SW = U >= 8 ? 7 : U - 1;    // swizzle mask
   const int lane = threadIdx.x & 63;
   const int frow = lane & 15;
   const int fq = lane >> 4;
+  // phase 2 layout: lanes per row = TN/8, rows per pass = 64 / (TN/8)
+  constexpr int LPR = TN / 8;
+  constexpr int RPP = 64 / LPR;
+  constexpr int ITS = (NI * 16 + RPP - 1) / RPP;
+  const int c8 = lane % LPR;
+  const int rr = lane / LPR;
+  // LayerNorm producer: the row shifts of this pass's phase-2 iterations are loaded before any of its
+  // stores.  vmcnt retires in issue order, so a load issued behind a store cannot be consumed before
+  // that store has completed; loaded in each iteration, they chained every iteration behind the
+  // previous one's stores (r04, tools/diag12.sh: O 70 -> 68 us, DA-v2's 384 x 192 producer 100 -> 95 us).
+  // Prefetching the residual rows too pushed the 320 x 256 kernel into scratch (10x slower K-loop).
+  constexpr bool PRE_SH = ITS <= 10;
+  const bool pre = p.lnp && p.ct_s == 0;
+  float pre_rs[PRE_SH ? ITS : 1], pre_sh[PRE_SH ? ITS : 1];
+  if (PRE_SH && pre) {
+#pragma unroll
+    for (int it = 0; it < ITS; ++it) {
+      const int r = it * RPP + rr;
+      const int m = mrow0 + i0 * 16 + r;
+      if ((LPR * RPP < 64 && (rr >= RPP || r >= ni * 16)) || m >= p.M) continue;
+      const int orow = remap(m, p.o_g, p.o_gs, p.o_o);
+      if (p.rsh) pre_rs[it] = p.rsh[orow];
+      if (p.lnsh) pre_sh[it] = p.lnsh[m];
+    }
+  }
   // bias depends on the column only: load it once, all loads in flight together
   float4 bias4[RN];
 #pragma unroll
@@ -217,13 +243,11 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (i0 == 0) STAMP(4);
-  // phase 2: lanes per row = TN/8, rows per pass = 64 / (TN/8)
-  constexpr int LPR = TN / 8;
-  constexpr int RPP = 64 / LPR;
-  const int c8 = lane % LPR;
-  const int rr = lane / LPR;
+  // phase 2
   const int rows = ni * 16;
-  for (int r0 = 0; r0 < rows; r0 += RPP) {
+#pragma unroll
+  for (int it = 0; it < ITS; ++it) {
+    const int r0 = it * RPP;
     const int r = r0 + rr;
     // TN = 96: 12 lanes per row, 5 rows per pass (60 lanes), and 48 rows are not a multiple of 5
     if (LPR * RPP < 64 && (rr >= RPP || r >= rows)) continue;
@@ -262,7 +286,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
         if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
-          const float rs = p.rsh[orow];
+          const float rs = PRE_SH && pre ? pre_rs[PRE_SH ? it : 0] : p.rsh[orow];
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             v[2 * t] += __uint_as_float(q[t] << 16) + rs;
@@ -291,7 +315,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         if (p.lnp) {
           // LayerNorm producer: the bf16 copy of out - shift[m], and (mean, M2) of each 64-column
           // chunk (= 8 lanes) of it, or of each 32-column chunk (4 lanes; lnc = 32)
-          const float shf = p.lnsh ? p.lnsh[m] : 0.f;
+          const float shf = p.lnsh ? (PRE_SH && pre ? pre_sh[PRE_SH ? it : 0] : p.lnsh[m]) : 0.f;
           float u[8];
 #pragma unroll
           for (int t = 0; t < 8; ++t) u[t] = v[t] - shf;
@@ -558,7 +582,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   static_assert(EP_RM >= 1 && RM % EP_RM == 0, "epilogue LDS");
 #pragma unroll
   for (int i0 = 0; i0 < RM; i0 += EP_RM) {
-    tile_epilogue<RM, RN>(p, acc, i0, EP_RM, m0 + wm * TM, n0 + wn * TN,
+    tile_epilogue<RM, RN, EP_RM>(p, acc, i0, m0 + wm * TM, n0 + wn * TN,
                           reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
     __builtin_amdgcn_wave_barrier();
   }
@@ -1204,7 +1228,9 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
       // with the stagger, waves 4-7 issue theirs half-way through the step, so each SIMD's MFMA pipe
       // runs one wave's MFMAs while its partner (wave w +- 4) issues loads, instead of both issuing
       // at the top of the step (buffer (g + 1) & 1 was last read in step g - 1: any point is legal)
-      const bool late = p.stagger && wid >= 4;
+      // (bf16 only: in the fp8 engine the mid-step issue pushed the register allocation into scratch,
+      // whose VMEM operations would break the counted vmcnt waits)
+      const bool late = !F8 && p.stagger && wid >= 4;
       auto issue_next = [&]() {
         if (kt + 1 < nk) {
           stage((g + 1) & 1, (kt + 1) * KSTEP, -1);
@@ -1255,11 +1281,6 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
         }
 #pragma unroll
         for (int i = 0; i < RM; ++i) {
-          if (i == RM / 2 && late) {
-            __builtin_amdgcn_sched_barrier(0);
-            issue_next();
-            __builtin_amdgcn_sched_barrier(0);
-          }
           const int row = wm * TM + i * 16 + frow;
           const uint8_t* r = sA + row * ROWB;
           const i32x4 lo = *reinterpret_cast<const i32x4*>(r + ((fq ^ (row & 7)) << 4));

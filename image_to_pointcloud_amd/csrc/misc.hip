@@ -275,14 +275,15 @@ __global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ 
 // LayerNorm of a bf16 row block from its row statistics (i2pc_ln_apply): y = bf16(gamma * (rs.x * x +
 // rs.y) + beta) with rs = (rstd, -rstd * mean) of the rows as ln_rowstats gives them (x = the shifted
 // bf16 residual stream: the statistics were taken of the same shifted values).  8 columns per thread
-// (one 16-B load and store), grid-stride over rows x dim / 8.
+// (one 16-B load and store), one workgroup row per matrix row.
 __global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, int64_t ldx8, const float2* __restrict__ rs,
                                                   const float4* __restrict__ gamma, const float4* __restrict__ beta,
                                                   int rows, int d8, uint4* __restrict__ y, int64_t ldy8) {
-  const int64_t n = (int64_t)rows * d8;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int r = (int)(i / d8);
-    const int c = (int)(i - (int64_t)r * d8);
+  // one 8-column group per thread: row r = blockIdx.y, group c = blockIdx.x * 256 + threadIdx.x
+  (void)rows;
+  const int r = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < d8) {
     const uint4 v = x[r * ldx8 + c];
     const float2 s = rs[r];
     const float4 g0 = gamma[2 * c], g1 = gamma[2 * c + 1], b0 = beta[2 * c], b1 = beta[2 * c + 1];
@@ -339,10 +340,14 @@ extern "C" int i2pc_ln_apply(const void* x, int64_t ldx, const float* rows_stats
                    (reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) % 16 == 0,
                "ln_apply: 16-byte aligned operands");
   const int d8 = dim / 8;
-  hipLaunchKernelGGL(k_ln_apply, dim3(grid_for((int64_t)rows * d8)), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint4*>(x), ldx / 8, reinterpret_cast<const float2*>(rows_stats),
-                     reinterpret_cast<const float4*>(gamma), reinterpret_cast<const float4*>(beta), rows, d8,
-                     static_cast<uint4*>(y), ldy / 8);
+  for (int r0 = 0; r0 < rows; r0 += 65535) {   // (grid y <= 65535 rows per launch)
+    const int nr = std::min(rows - r0, 65535);
+    hipLaunchKernelGGL(k_ln_apply, dim3((d8 + 255) / 256, nr), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint4*>(x) + (int64_t)r0 * (ldx / 8), ldx / 8,
+                       reinterpret_cast<const float2*>(rows_stats) + r0, reinterpret_cast<const float4*>(gamma),
+                       reinterpret_cast<const float4*>(beta), nr, d8, static_cast<uint4*>(y) + (int64_t)r0 * (ldy / 8),
+                       ldy / 8);
+  }
   return check_launch("ln_apply");
 }
 
