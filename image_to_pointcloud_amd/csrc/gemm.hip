@@ -168,6 +168,15 @@ __device__ __forceinline__ float dpp_f(float v) {
 // the wave's LDS region (16-B units XOR-swizzled by row).  Phase 2 (row layout):
 // each lane owns 8 consecutive columns of one row: + res + res2 with 16/32-B loads,
 // then one 16-B (bf16) or 2 x 16-B (fp32) store; a wave writes whole 128-B lines.
+// f(0), f(1), ..., f(N - 1) as straight-line code (each call inlined with a constant argument)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void epi_passes(F&& f) {
+  if constexpr (I < N) {
+    f(I);
+    epi_passes<N, I + 1>(f);
+  }
+}
+
 template <int RM, int RN, int NI>
 __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int mrow0,
                                               int ncol0, float* lds) {
@@ -188,7 +197,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   // stores.  vmcnt retires in issue order, so a load issued behind a store cannot be consumed before
   // that store has completed; loaded in each iteration, they chained every iteration behind the
   // previous one's stores (r04, tools/diag12.sh: O 70 -> 68 us, DA-v2's 384 x 192 producer 100 -> 95 us).
-  // Prefetching the residual rows too pushed the 320 x 256 kernel into scratch (10x slower K-loop).
+  // Prefetching the residual rows as well was no faster: before phase 1 it pushed the 320 x 256 kernel
+  // into scratch, after phase 1 (registers free) it measured 2-3 % slower (tools/diag17.sh).
   constexpr bool PRE_SH = ITS <= 10;
   const bool pre = p.lnp && p.ct_s == 0;
   float pre_rs[PRE_SH ? ITS : 1], pre_sh[PRE_SH ? ITS : 1];
@@ -580,12 +590,13 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   constexpr int EP_RM = RM % EP_RM1 == 0 ? EP_RM1 : RM % (EP_RM1 - 1) == 0 ? EP_RM1 - 1
                       : RM % (EP_RM1 - 2) == 0 ? EP_RM1 - 2 : 1;   // largest divisor of RM that fits
   static_assert(EP_RM >= 1 && RM % EP_RM == 0, "epilogue LDS");
-#pragma unroll
-  for (int i0 = 0; i0 < RM; i0 += EP_RM) {
-    tile_epilogue<RM, RN, EP_RM>(p, acc, i0, m0 + wm * TM, n0 + wn * TN,
-                          reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
+  // the passes as a compile-time sequence (a `#pragma unroll` loop over them can exceed the
+  // unroller's size limit, and a rolled loop puts acc[][] in scratch)
+  epi_passes<RM / EP_RM>([&](int pass) {
+    tile_epilogue<RM, RN, EP_RM>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
+                                 reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
     __builtin_amdgcn_wave_barrier();
-  }
+  });
   STAMP(3);
 }
 

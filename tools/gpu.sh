@@ -18,6 +18,7 @@
 #                              only; TAG=<suffix> names the output directory)
 #   pmc-unp                    SQ counters of the unprojection microbench
 #   c4                         tools/c4_panorama.py on one rank: window / levels / smooth / equirect / network stream
+#   clock [tag] [bench args]   effective shader clock per kernel (GRBM_GUI_ACTIVE / 8 / wall) -> profiles/<round>_<tag>_clock.json
 set -o pipefail
 R=${ROUND:-r03}
 TASK=$1; shift
@@ -184,5 +185,12 @@ case "$TASK" in
       timeout -k 10 120 rocprofv3 --pmc $P --kernel-trace -d $D/c$i -o c --output-format csv -- python tools/c4_panorama.py --steps 2 --warmup 1 > $D/c$i.txt 2>&1 || exit 1
     done
     for i in 1 2; do echo "== C2 pass $i"; python tools/pmc_summary.py $D/u$i k_sweep_w; echo "== C4 pass $i"; python tools/pmc_summary.py $D/c$i k_sweep_w; done ;;
+  clock)      # effective shader clock per kernel (GRBM_GUI_ACTIVE / 8 / wall; DVFS give-back) of the bench network
+    TAG=${1:-dpt-large-bf16}; shift || true
+    D=gpurun_out/clock_$TAG; rm -rf $D; mkdir -p $D
+    timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace -d $D/p -o p --output-format csv -- \
+      python bench.py --steps 3 --warmup 0 --no-graph --no-kernel-profile --no-cpu-baseline "$@" > $D/run.txt 2>&1 \
+      || { tail -5 $D/run.txt; exit 1; }
+    python tools/pmc_clock.py $D/p "profiles/${R}_${TAG}_clock.json" && cp "profiles/${R}_${TAG}_clock.json" gpurun_out/ ;;
   *) echo "unknown task '$TASK' (see the header of tools/gpu.sh)"; exit 2 ;;
 esac
