@@ -231,6 +231,21 @@ __global__ __launch_bounds__(256) void k_head_out(const bf16_t* __restrict__ x, 
   }
 }
 
+// Sum over the 16 lanes of a DPP row by one DPP move per step (lane ^ 1, lane ^ 2 inside a quad, then
+// the half-row mirror 7 - i and the row mirror 15 - i, whose partners hold the other quad's / half's
+// sum by then) instead of ds_bpermute round trips; every lane ends with the row's sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  return v;
+}
+
 // LayerNorm row statistics from the cw-column chunk partials (cw = 64 or 32) an i2pc_gemm producer
 // epilogue wrote ((mean, M2) per chunk of out - shift): Chan's combination for equal chunk counts,
 // mean = avg(mean_c), M2 = sum M2_c + cw sum (mean_c - mean)^2, var = M2 / (cw P) (biased, as
@@ -249,10 +264,7 @@ __global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ 
   float sm = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) sm += v[j].x;
-  sm += __shfl_xor(sm, 1);
-  sm += __shfl_xor(sm, 2);
-  sm += __shfl_xor(sm, 4);
-  sm += __shfl_xor(sm, 8);
+  sm = row16_sum(sm);
   const float mean = sm / (float)P;
   float m2 = 0.f;
 #pragma unroll
@@ -261,10 +273,7 @@ __global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ 
       const float d = v[j].x - mean;
       m2 += v[j].y + cw * d * d;
     }
-  m2 += __shfl_xor(m2, 1);
-  m2 += __shfl_xor(m2, 2);
-  m2 += __shfl_xor(m2, 4);
-  m2 += __shfl_xor(m2, 8);
+  m2 = row16_sum(m2);
   if (ok && l == 0) {
     const float rstd = 1.0f / sqrtf(m2 / (cw * (float)P) + eps);
     out[r] = make_float2(rstd, -rstd * mean);
