@@ -309,3 +309,33 @@ def test_tail160_bitexact(M, N, lnf):
     finally:
         ops.set_tuning("gemm_tail160", 1)
     assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+
+
+@pytest.mark.parametrize("M,N,K,act,res", [(18464, 3072, 1024, None, False), (18464, 4096, 1024, "gelu", False),
+                                           (18464, 1024, 1024, None, True), (18464, 1024, 4096, None, True),
+                                           (43840, 384, 1536, None, True), (6000, 2048, 640, None, False)])
+def test_stagger_bitexact(M, N, K, act, res):
+    """gemm_stagger (waves 4-7 issue the next K-stage half-way through the step) changes only when the
+    LDS-DMA loads are issued, never what is multiplied: outputs are bit-identical with it off, on the
+    persistent engine (QKV / FC1 shapes), the 320 x 256 and 384 x 192 tile kernels (O / FC2 shapes)."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = _bf(torch.randn(M, K, generator=g)).to(dev)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    x0 = torch.randn(M, N, generator=g).to(dev)
+    outs = []
+    try:
+        for on in (1, 0):
+            ops.set_tuning("gemm_stagger", on)
+            if res:
+                y = x0.clone()
+                ops.linear(x, w, bias=b, res=y, out=y)
+            else:
+                y = ops.linear(x, w, bias=b, act=act)
+            torch.cuda.synchronize()
+            outs.append(y)
+    finally:
+        ops.set_tuning("gemm_stagger", 1)
+    assert torch.equal(outs[0], outs[1])
