@@ -147,6 +147,19 @@ def _pmc_traffic(tag: str):
         return json.load(fh).get("kernels", {}), os.path.relpath(files[-1], ROOT)
 
 
+def _profiled_clock(tag: str, name: str):
+    """Effective shader clock (GHz) of a kernel label from the newest profiles/r*_<tag>_clock.json
+    (tools/gpu.sh clock: GRBM_GUI_ACTIVE / 8 / wall in a profiled eager pass; VERDICT r03 asked for it
+    beside frac -- it says how much of the gap to the peak is clock), or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_clock.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        e = json.load(fh).get("kernels", {}).get(name)
+    return (e["clock_ghz"], os.path.relpath(files[-1], ROOT)) if e else (None, None)
+
+
 def _traffic(table, src, *names, calls_per_step=None):
     """PMC HBM bytes per CALL of a kernel label: the label's dispatches of one step summed (a GEMM
     call may be a main and a tail launch) / the calls per step; the per-dispatch average when the
@@ -380,6 +393,14 @@ def main():
             roofline["algorithmic_bytes_per_launch"] = round(d["bytes"] / d["n"])
             if roofline["traffic"]:
                 roofline["traffic_over_algorithmic"] = round(roofline["traffic"] / (d["bytes"] / d["n"]), 3)
+            tag = (f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
+                   + ("" if a.density == "high" else f"-{a.density}"))
+            clk, clk_src = _profiled_clock(tag, name)
+            if clk:
+                # beside frac, not instead of it: frac at the clock the chip held in the profiled pass
+                roofline["clock_ghz_profiled"] = clk
+                roofline["frac_at_profiled_clock"] = round(ach / (pk * clk / 2.4), 4)
+                roofline["clock_source"] = clk_src
             if name.startswith("k_gemm_p"):
                 roofline["note"] = ("avg_us and traffic are per i2pc_gemm call: the persistent launch plus, where "
                                     "the round-quantisation split applies (QKV), its 256x128 tail launch; rocprofv3 "
