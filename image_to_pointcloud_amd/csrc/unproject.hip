@@ -879,7 +879,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep(Geo g, SelState* st, uint32_t*
 template <bool SAME, int NW>
 __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t* cand, uint32_t cap, int b,
                                              int v0, int v1, int cw, int c0, const Tap* tys,
-                                             uint32_t (*sh)[kStageW], uint32_t (*red)[28],
+                                             uint32_t (*sh)[kStageW], uint32_t (*red)[32],
                                              const float* vlo, const float* vhi, const float* vF,
                                              const float* vL, const uint32_t* spk) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1052,7 +1052,7 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
       }
     }
   }
-  // the wave's finite range -> the image's key range (one atomic pair per wave).  The float min / max
+  // the wave's finite range -> red (the image's key range: k_sweep_w, once per workgroup).  The float min / max
   // may pick +0 over -0 (or the reverse): exact keys unless a zero is an end of the range and the
   // model map holds a value <= -0 (only then can a -0 pixel exist); such an image is flagged and
   // k_sel_slow counts its range itself (SelState::pad3[0] bit 1)
@@ -1060,22 +1060,25 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
     fmn = fminf(fmn, __shfl_xor(fmn, o));
     fmx = fmaxf(fmx, __shfl_xor(fmx, o));
   }
-  if (lane == 0 && fmn <= fmx) {
+  // (the workgroup's range goes to the image with one check-then-atomic pair at the end of k_sweep_w)
+  uint32_t rk_lo = 0xffffffffu, rk_hi = 0u;
+  if (fmn <= fmx) {
     if ((fmn == 0.f || fmx == 0.f) && S->rlo < f2key(0.f)) {
-      atomicOr(&S->pad3[0], 2u);
+      if (lane == 0) atomicOr(&S->pad3[0], 2u);
     } else {
-      atomicMin(&S->kmin, f2key(fmn));
-      atomicMax(&S->kmax, f2key(fmx));
+      rk_lo = f2key(fmn); rk_hi = f2key(fmx);
     }
   }
+  if (lane == 0) { red[wid][28] = rk_lo; red[wid][29] = rk_hi; }
   // wave totals -> red[wave][...]: 0 nf, 1 nnan, 2 nneg, 3 npos, 4 + w below, then per window
-  // 6 + 6 w: F count / min / max, L count / min / max
+  // 7 + 6 w: F count / min / max, L count / min / max; 25 + w: keys left in the wave's buffer;
+  // 28 / 29: the finite key range (r03 put window 0's spike count on 6 = below[2])
 #pragma unroll
   for (int w = 0; w < NW; ++w) below[w] = wave_sum_u32(below[w]);
   if (lane == 0) {
     red[wid][0] = nf; red[wid][1] = nnan; red[wid][2] = nneg; red[wid][3] = npos;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) { red[wid][4 + w] = below[w]; red[wid][24 + w] = wc[w]; }
+    for (int w = 0; w < NW; ++w) { red[wid][4 + w] = below[w]; red[wid][25 + w] = wc[w]; }
   }
   if (any_spike) {
 #pragma unroll
@@ -1083,8 +1086,8 @@ __device__ __forceinline__ void sweep_w_rows(const Geo& g, SelState* S, uint32_t
       const uint32_t a = wave_sum_u32(cF[w]), c = wave_min_u32(mnF[w]), d = wave_max_u32(mxF[w]);
       const uint32_t e = wave_sum_u32(cL[w]), f = wave_min_u32(mnL[w]), h = wave_max_u32(mxL[w]);
       if (lane == 0) {
-        red[wid][6 + 6 * w] = a; red[wid][7 + 6 * w] = c; red[wid][8 + 6 * w] = d;
-        red[wid][9 + 6 * w] = e; red[wid][10 + 6 * w] = f; red[wid][11 + 6 * w] = h;
+        red[wid][7 + 6 * w] = a; red[wid][8 + 6 * w] = c; red[wid][9 + 6 * w] = d;
+        red[wid][10 + 6 * w] = e; red[wid][11 + 6 * w] = f; red[wid][12 + 6 * w] = h;
       }
     }
   }
@@ -1097,7 +1100,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
   // R output rows.  The horizontal cv2 pass of a model row is a thread's own business (its 4
   // columns), so it stays in registers.
   __shared__ uint32_t sh[3][kStageW];               // per window: the waves' key buffers (kWaveBuf each)
-  __shared__ uint32_t red[kBlock / 64][28];
+  __shared__ uint32_t red[kBlock / 64][32];
   __shared__ uint32_t gbase[3];
   __shared__ Tap tys[kMaxSelRows];                  // the block's row taps (no global load in the row loop)
   int b, chunk;
@@ -1129,6 +1132,15 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
     uint32_t c[4] = {0, 0, 0, 0};
     for (int w = 0; w < kBlock / 64; ++w)
       for (int i = 0; i < 4; ++i) c[i] += red[w][i];
+    // kmin only falls and kmax only rises, so the atomic is skipped when a relaxed read already
+    // shows a value at least as extreme (a stale read errs towards issuing it): one 8192x4096 image
+    // is 2 K workgroups on the same two words (per-wave unconditional atomics: C4 sweep 61 -> 210 us)
+    uint32_t klo = 0xffffffffu, khi = 0u;
+    for (int w = 0; w < kBlock / 64; ++w) { klo = min(klo, red[w][28]); khi = max(khi, red[w][29]); }
+    if (klo <= khi) {
+      if (klo < __hip_atomic_load(&S->kmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&S->kmin, klo);
+      if (khi > __hip_atomic_load(&S->kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&S->kmax, khi);
+    }
     if (c[0]) {
       atomicAdd(&S->nonfinite_count, c[0]);
       if (c[1]) atomicAdd(&S->nan_count, c[1]);
@@ -1140,13 +1152,13 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
       for (int w = 0; w < kBlock / 64; ++w) bw += red[w][4 + q];
       if (bw) atomicAdd(&wpart[((size_t)b * kBelowSlots + (blockIdx.x % kBelowSlots)) * 4 + q], bw);
       uint32_t nq = 0;                 // the waves' leftover keys: one reservation per window
-      for (int w = 0; w < kBlock / 64; ++w) nq += red[w][24 + q];
+      for (int w = 0; w < kBlock / 64; ++w) nq += red[w][25 + q];
       gbase[q] = nq ? atomicAdd(&S->ccount[q], nq) : 0u;
       if (spk[q]) {
         uint32_t a = 0, cmn = 0xffffffffu, dmx = 0, e = 0, fmn = 0xffffffffu, hmx = 0;
         for (int w = 0; w < kBlock / 64; ++w) {
-          a += red[w][6 + 6 * q]; cmn = min(cmn, red[w][7 + 6 * q]); dmx = max(dmx, red[w][8 + 6 * q]);
-          e += red[w][9 + 6 * q]; fmn = min(fmn, red[w][10 + 6 * q]); hmx = max(hmx, red[w][11 + 6 * q]);
+          a += red[w][7 + 6 * q]; cmn = min(cmn, red[w][8 + 6 * q]); dmx = max(dmx, red[w][9 + 6 * q]);
+          e += red[w][10 + 6 * q]; fmn = min(fmn, red[w][11 + 6 * q]); hmx = max(hmx, red[w][12 + 6 * q]);
         }
         if (a) { atomicAdd(&S->wcntF[q], a); atomicMin(&S->wminF[q], cmn); atomicMax(&S->wmaxF[q], dmx); }
         if (e) { atomicAdd(&S->wcntL[q], e); atomicMin(&S->wminL[q], fmn); atomicMax(&S->wmaxL[q], hmx); }
@@ -1157,8 +1169,8 @@ __global__ __launch_bounds__(kBlock) void k_sweep_w(Geo g, SelState* st, uint32_
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int q = 0; q < nwin; ++q) {
     uint32_t off = gbase[q];
-    for (int w = 0; w < wid; ++w) off += red[w][24 + q];
-    const uint32_t nq = red[wid][24 + q];
+    for (int w = 0; w < wid; ++w) off += red[w][25 + q];
+    const uint32_t nq = red[wid][25 + q];
     uint32_t* dst = cand + ((size_t)b * kSlots + q) * cap;
     for (uint32_t i = lane; i < nq; i += 64)
       if (off + i < cap) dst[off + i] = sh[q][wid * kWaveBuf + i];

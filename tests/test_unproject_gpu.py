@@ -486,6 +486,11 @@ def _sel_cases():
         d = base.copy()
         d.ravel()[rng.permutation(d.size)[:int(frac * d.size)]] = np.float32(base.max())
         out[f"sat_{frac}"] = d
+    # a spike window next to the nanmedian fill's third window (k_sweep_w's per-wave spike and
+    # below-window counts share one LDS row: r03 laid window 0's spike count over below[2])
+    for k in ("zero_0.025", "zero_0.3", "sat_0.05"):
+        d = out[k].copy(); d[7, 8] = np.nan; d[50, 90] = np.nan
+        out[k + "_nan"] = d
     out["quantised"] = (np.round(base * 16) / 16).astype(np.float32)
     out["two_valued"] = np.where(rng.random(base.shape) < 0.5, 1.0, 2.0).astype(np.float32)
     d = base.copy(); d[3, 4] = np.nan; d[10, 11] = np.inf; d[20, 0] = -np.inf
