@@ -160,6 +160,23 @@ def _profiled_clock(tag: str, name: str):
     return (e["clock_ghz"], os.path.relpath(files[-1], ROOT)) if e else (None, None)
 
 
+def _profiled_us(tag: str, prefix: str):
+    """Average duration (us) of the first kernel whose name starts with `prefix` in the newest
+    profiles/r*_<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats over this bench), or
+    (None, None).  A short kernel's HIP-event pair carries a few us of its own, so the profile's
+    figure is printed beside the live one (the contract's value stays the live one)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_kernel_stats.csv")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        for r in csv.DictReader(fh):
+            if r["Name"].startswith(prefix):
+                return float(r["AverageNs"]) / 1e3, os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def _traffic(table, src, *names, calls_per_step=None):
     """PMC HBM bytes per CALL of a kernel label: the label's dispatches of one step summed (a GEMM
     call may be a main and a tail launch) / the calls per step; the per-dispatch average when the
@@ -434,6 +451,15 @@ def main():
             t, src = _traffic(pmc, pmc_src, f"k_unproject_rows<{step}>", f"k_unproject_fast<{step}>",
                               calls_per_step=1)
             rooflines["unproject_kernel"].update(traffic=t, traffic_source=src)
+            tag = (f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
+                   + ("" if a.density == "high" else f"-{a.density}"))
+            for kname in (f"void i2pc::unproj::k_unproject_rows<{step}>", f"void i2pc::unproj::k_unproject_fast<{step}>"):
+                us, us_src = _profiled_us(tag, kname)
+                if us:
+                    rooflines["unproject_kernel"].update(
+                        us_profiled=round(us, 1), frac_profiled=round(geo_bytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                        profiled_source=us_src)
+                    break
         net_t = sum(v["t"] for v in per.values())
         net_f = sum(v["flops"] for v in per.values())
         # mixed-precision networks: the peak is the FLOP-weighted harmonic mean of the kernels'
