@@ -2337,6 +2337,112 @@ static int run8(const Plan8& pl, const Args& p, bool conv, bool relu, hipStream_
   return check_launch("gemm_fp8");
 }
 
+// ---- Skinny GEMM: M <= 64 rows (the DPT readout's CLS half, one row per image: M = batch, N = K =
+// hidden).  The tile kernel runs such a call as N / 64 tiles of 128 x 64, each a serial K-loop
+// (M 32, N 1024, K 1024: 16 tiles, 22.7 us for 67 MFLOP).  Here a workgroup owns 16 output
+// columns of up to 32 rows: its A rows are staged in LDS, thread (column c, slice q) takes the
+// 16-byte K chunks q, q + 16, q + 32, ... of its W row (a wave's 16 slice lanes read 256
+// contiguous bytes of W and of each A row: no LDS bank conflict), sums in fp32 per row, and the 16
+// slice lanes combine by xor shuffles (a fixed order: deterministic).  Then the tile epilogue's
+// bias and activation.  Knob "gemm_skinny" (I2PC_GEMM_SKINNY, default 0), automatic engine mode only.
+// Measured r04 (tools/diag27.sh, C2): 40.7 us per readout call against 22.7 on the tile kernel, C2 step
+// 20.415 vs 20.320 ms -- slower, so off by default; kept as the starting point (bit-stable, tested)
+static thread_local int g_skinny = [] { const char* e = getenv("I2PC_GEMM_SKINNY"); return e ? atoi(e) : 0; }();
+constexpr int kSkCols = 16, kSkRows = 32, kSkMaxK = 1024;   // LDS: (32 + 16) rows x K bf16 <= 96 KB
+
+__global__ __launch_bounds__(256) void k_gemm_skinny(Args p) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t sa[];    // [rows][K]
+  const int n0 = blockIdx.x * kSkCols, m0 = blockIdx.y * kSkRows;
+  const int rows = min(kSkRows, p.M - m0);
+  const int K = p.K, kv = K / 8;                                   // 16-byte chunks per row
+  const int q = threadIdx.x & 15, n = n0 + (threadIdx.x >> 4);
+  // the A rows and the workgroup's 16 W rows into LDS ([rows][K] then [kSkCols][K]) by LDS-DMA: chunk
+  // i of that index space lands at LDS chunk i, so a wave's 64 lanes fill 1 KB in lane order; every
+  // load is in flight before the one wait (past the end: clamped sources into the LDS slack)
+  const int na = rows * kv, total = na + kSkCols * kv;
+  bf16_t* sw = sa + (size_t)rows * K;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int b0 = wave * 64; b0 < total; b0 += 256) {
+    const int i = min(b0 + lane, total - 1);
+    const bool isa = i < na;
+    const int ia = isa ? i : i - na;
+    const int r = ia / kv, c = ia - r * kv;
+    const bf16_t* row = isa ? p.A + remap(m0 + r, p.a_g, p.a_gs, p.a_o) * p.lda
+                            : p.W + (int64_t)min(n0 + r, p.N - 1) * p.ldw;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(row) + c,
+                                     (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(sa) + b0), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float acc[kSkRows];
+#pragma unroll
+  for (int r = 0; r < kSkRows; ++r) acc[r] = 0.f;
+  if (n < p.N) {
+    const uint4* arow = reinterpret_cast<const uint4*>(sa);
+    const uint4* wrow = reinterpret_cast<const uint4*>(sw) + (threadIdx.x >> 4) * kv;   // (W after the rows A has)
+    for (int j = q; j < kv; j += 16) {
+      const uint4 wv = wrow[j];
+      const uint32_t wu[4] = {wv.x, wv.y, wv.z, wv.w};
+      float wf[8];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { wf[2 * t] = __uint_as_float(wu[t] << 16); wf[2 * t + 1] = __uint_as_float(wu[t] & 0xffff0000u); }
+#pragma unroll
+      for (int r = 0; r < kSkRows; ++r) {
+        if (r < rows) {
+          const uint4 av = arow[r * kv + j];
+          const uint32_t au[4] = {av.x, av.y, av.z, av.w};
+          float sacc = acc[r];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            sacc = fmaf(__uint_as_float(au[t] << 16), wf[2 * t], sacc);
+            sacc = fmaf(__uint_as_float(au[t] & 0xffff0000u), wf[2 * t + 1], sacc);
+          }
+          acc[r] = sacc;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kSkRows; ++r) {
+    float v = acc[r];
+    v += __shfl_xor(v, 1); v += __shfl_xor(v, 2); v += __shfl_xor(v, 4); v += __shfl_xor(v, 8);
+    acc[r] = v;
+  }
+  if (n >= p.N) return;
+  const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < kSkRows; ++r) {
+    if ((r & 15) == q && r < rows) {          // lane q writes rows q and q + 16
+      float v = acc[r] + bn;
+      if (p.act == 1) v = gelu_erf(v);
+      else if (p.act == 2) v = fmaxf(v, 0.f);
+      const int64_t off = (int64_t)(m0 + r) * p.ldc + n;
+      if (p.c_f32) static_cast<float*>(p.C)[off] = v;
+      else static_cast<bf16_t*>(p.C)[off] = f2bf(v);
+    }
+  }
+}
+
+static bool skinny_ok(const Args& p, bool conv) {
+  return g_skinny && g_engine == 0 && !conv && p.M <= 2 * kSkRows && p.K % 128 == 0 && p.K <= kSkMaxK &&
+         !p.rbias && !p.tbl && !p.res && !p.res2 && !p.lnr && !p.lnp && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 &&
+         p.act >= 0 && p.act <= 2 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
+         reinterpret_cast<uintptr_t>(p.A) % 16 == 0 && reinterpret_cast<uintptr_t>(p.W) % 16 == 0;
+}
+
+static int run_skinny(const Args& p, hipStream_t s) {
+  const int smem = (kSkRows + kSkCols) * p.K * 2 + 1024;     // + the DMA's tail slack (< 64 chunks)
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_skinny), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (kSkRows + kSkCols) * kSkMaxK * 2 + 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_gemm_skinny, dim3((p.N + kSkCols - 1) / kSkCols, (p.M + kSkRows - 1) / kSkRows), dim3(256), smem,
+                     s, p);
+  return check_launch("gemm (skinny)");
+}
+
 static const char* plan8_name(const Plan8& pl, bool conv, bool relu) {
   static thread_local char buf[96];
   static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8"};
@@ -2413,6 +2519,7 @@ extern "C" int i2pc_gemm_ws(const i2pc_gemm_desc* d, void* workspace, size_t wor
   if (rc != I2PC_OK) return rc;
   hipStream_t s = as_stream(stream);
   const bool conv = d->conv != 0, relu = d->conv_relu_in != 0;
+  if (gemm::skinny_ok(p, conv)) return gemm::run_skinny(p, s);
   const gemm::Plan pl = gemm::plan_for(p, conv, relu);
   const gemm::SplitPlan sp = gemm::split_for(p, pl);
   if (sp.splits > 1 && workspace && (int64_t)workspace_bytes >= sp.bytes) {
@@ -2430,6 +2537,7 @@ extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) { return i2pc_ge
 extern "C" size_t i2pc_gemm_workspace_bytes(const i2pc_gemm_desc* d) {
   gemm::Args p;
   if (make_args(d, p) != I2PC_OK) return 0;
+  if (gemm::skinny_ok(p, d->conv != 0)) return 0;
   const gemm::SplitPlan sp = gemm::split_for(p, gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0));
   return sp.splits > 1 ? (size_t)sp.bytes : 0;
 }
@@ -2480,6 +2588,7 @@ extern "C" const char* i2pc_gemm_fp8_kernel_name(const i2pc_gemm_fp8_desc* d8) {
 extern "C" const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* d) {
   gemm::Args p;
   if (make_args(d, p) != I2PC_OK) return "invalid";
+  if (gemm::skinny_ok(p, d->conv != 0)) return "k_gemm_skinny";
   const gemm::Plan pl = gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0);
   return gemm::plan_name(pl, d->conv != 0, d->conv_relu_in != 0, gemm::split_for(p, pl));
 }
@@ -2494,8 +2603,9 @@ extern "C" int i2pc_gemm_set_engine(int mode) {
 }
 
 // per-host-thread tuning knobs (i2pc_set_tuning; thread_local above): gemm_tail, gemm_bn128,
-// gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_tail160, gemm_stagger
+// gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_tail160, gemm_stagger, gemm_skinny
 bool i2pc_gemm_tune(const char* name, int value) {
+  if (std::strcmp(name, "gemm_skinny") == 0) { i2pc::gemm::g_skinny = value; return true; }
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
   if (std::strcmp(name, "gemm_splitk") == 0) { i2pc::gemm::g_splitk = value; return true; }

@@ -390,6 +390,10 @@ int i2pc_gemm_set_engine(int mode);
  *   "gemm_stagger" 1 = in the 8-wave GEMM kernels waves 4-7 issue the next K-stage's loads half-way
  *                 through each K-step (their SIMD partners' MFMAs cover the issue), 0 = every wave at
  *                 the top of the step
+ *   "gemm_skinny" 1 = calls of at most 64 rows (the DPT readout's CLS half: M = batch) on a skinny
+ *                 kernel (A rows in LDS, 16 output columns per workgroup, K split over 16 lanes;
+ *                 plain / bias / GELU / ReLU epilogues, K % 128 == 0, K <= 1024), automatic engine
+ *                 mode only; 0 = the tile kernel (default: measured faster, r04)
  *   "unp_rows"    1 = the row-sweep unprojection kernel
  *   "unp_nt"      1 = non-temporal point stores
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8
@@ -408,8 +412,8 @@ int i2pc_gemm_set_engine(int mode);
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  *   "ln_f2"       1 = the register-resident LayerNorm for dim 384 (k_layernorm2)
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _GEMM_SPLIT_TILE / _GEMM_TILE192 /
- * _GEMM_LNP_P / _GEMM_TAIL160 / _GEMM_STAGGER / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY / _ATTN_SCALAR
- * environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
+ * _GEMM_LNP_P / _GEMM_TAIL160 / _GEMM_STAGGER / _GEMM_SKINNY / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY /
+ * _ATTN_SCALAR environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 0, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
  * the kernels it captured: re-capture after changing a knob.  An unknown name fails with I2PC_EINVAL
  * and an error message listing every knob. */
 int i2pc_set_tuning(const char* name, int value);
