@@ -2345,8 +2345,10 @@ static int run8(const Plan8& pl, const Args& p, bool conv, bool relu, hipStream_
 // contiguous bytes of W and of each A row: no LDS bank conflict), sums in fp32 per row, and the 16
 // slice lanes combine by xor shuffles (a fixed order: deterministic).  Then the tile epilogue's
 // bias and activation.  Knob "gemm_skinny" (I2PC_GEMM_SKINNY, default 0), automatic engine mode only.
-// Measured r04 (tools/diag27.sh, C2): 40.7 us per readout call against 22.7 on the tile kernel, C2 step
-// 20.415 vs 20.320 ms -- slower, so off by default; kept as the starting point (bit-stable, tested)
+// Measured r04 (tools/diag27.sh / diag29.sh, C2): 40.7 us per readout call with a per-row guard in
+// the inner loop (every LDS read waited on alone), 26.3 us without it, against 22.7 us on the tile
+// kernel (C2 step 21.115 vs 21.064 ms) -- still slower, so off by default; kept as the starting point
+// (bit-stable, tested)
 static thread_local int g_skinny = [] { const char* e = getenv("I2PC_GEMM_SKINNY"); return e ? atoi(e) : 0; }();
 constexpr int kSkCols = 16, kSkRows = 32, kSkMaxK = 1024;   // LDS: (32 + 16) rows x K bf16 <= 96 KB
 
@@ -2359,15 +2361,15 @@ __global__ __launch_bounds__(256) void k_gemm_skinny(Args p) {
   // the A rows and the workgroup's 16 W rows into LDS ([rows][K] then [kSkCols][K]) by LDS-DMA: chunk
   // i of that index space lands at LDS chunk i, so a wave's 64 lanes fill 1 KB in lane order; every
   // load is in flight before the one wait (past the end: clamped sources into the LDS slack)
-  const int na = rows * kv, total = na + kSkCols * kv;
-  bf16_t* sw = sa + (size_t)rows * K;
+  const int na = kSkRows * kv, total = na + kSkCols * kv;      // (all 32 rows: rows past M repeat row M - 1)
+  bf16_t* sw = sa + (size_t)kSkRows * K;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int b0 = wave * 64; b0 < total; b0 += 256) {
     const int i = min(b0 + lane, total - 1);
     const bool isa = i < na;
     const int ia = isa ? i : i - na;
     const int r = ia / kv, c = ia - r * kv;
-    const bf16_t* row = isa ? p.A + remap(m0 + r, p.a_g, p.a_gs, p.a_o) * p.lda
+    const bf16_t* row = isa ? p.A + remap(min(m0 + r, p.M - 1), p.a_g, p.a_gs, p.a_o) * p.lda
                             : p.W + (int64_t)min(n0 + r, p.N - 1) * p.ldw;
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(row) + c,
                                      (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(sa) + b0), 16, 0, 0);
@@ -2387,18 +2389,16 @@ __global__ __launch_bounds__(256) void k_gemm_skinny(Args p) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) { wf[2 * t] = __uint_as_float(wu[t] << 16); wf[2 * t + 1] = __uint_as_float(wu[t] & 0xffff0000u); }
 #pragma unroll
-      for (int r = 0; r < kSkRows; ++r) {
-        if (r < rows) {
-          const uint4 av = arow[r * kv + j];
-          const uint32_t au[4] = {av.x, av.y, av.z, av.w};
-          float sacc = acc[r];
+      for (int r = 0; r < kSkRows; ++r) {     // (no row guard: the LDS reads batch)
+        const uint4 av = arow[r * kv + j];
+        const uint32_t au[4] = {av.x, av.y, av.z, av.w};
+        float sacc = acc[r];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            sacc = fmaf(__uint_as_float(au[t] << 16), wf[2 * t], sacc);
-            sacc = fmaf(__uint_as_float(au[t] & 0xffff0000u), wf[2 * t + 1], sacc);
-          }
-          acc[r] = sacc;
+        for (int t = 0; t < 4; ++t) {
+          sacc = fmaf(__uint_as_float(au[t] << 16), wf[2 * t], sacc);
+          sacc = fmaf(__uint_as_float(au[t] & 0xffff0000u), wf[2 * t + 1], sacc);
         }
+        acc[r] = sacc;
       }
     }
   }
