@@ -135,59 +135,59 @@ def _kernel_profile(pipe, images, reps=5):
     return per, geo_t, (unp_ms * 1e-3 if unp_ms > 0 else None)
 
 
+def _lib_sha16():
+    import hashlib
+    from image_to_pointcloud_amd import _lib
+    with open(_lib.load()._name, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
 def _pmc_traffic(tag: str):
     """HBM bytes per launch by kernel label from the newest profiles/r*_<tag>_pmc_traffic.json
     (tools/gpu.sh profile: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench,
-    gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or ({}, None)."""
+    gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md) -> (table, source, stale), or
+    ({}, None, None).  stale: the table was collected on another build of libi2pc.so than the
+    one this run loaded (or predates the recorded hash)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc_traffic.json")))
     if not files:
-        return {}, None
+        return {}, None, None
     with open(files[-1]) as fh:
-        return json.load(fh).get("kernels", {}), os.path.relpath(files[-1], ROOT)
-
-
-def _profiled_clock(tag: str, name: str):
-    """Effective shader clock (GHz) of a kernel label from the newest profiles/r*_<tag>_clock.json
-    (tools/gpu.sh clock: GRBM_GUI_ACTIVE / 8 / wall in a profiled eager pass; VERDICT r03 asked for it
-    beside frac -- it says how much of the gap to the peak is clock), or (None, None)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_clock.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as fh:
-        e = json.load(fh).get("kernels", {}).get(name)
-    return (e["clock_ghz"], os.path.relpath(files[-1], ROOT)) if e else (None, None)
-
-
-def _profiled_us(tag: str, prefix: str):
-    """Average duration (us) of the first kernel whose name starts with `prefix` in the newest
-    profiles/r*_<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats over this bench), or
-    (None, None).  A short kernel's HIP-event pair carries a few us of its own, so the profile's
-    figure is printed beside the live one (the contract's value stays the live one)."""
-    import csv
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_kernel_stats.csv")))
-    if not files:
-        return None, None
-    with open(files[-1]) as fh:
-        for r in csv.DictReader(fh):
-            if r["Name"].startswith(prefix):
-                return float(r["AverageNs"]) / 1e3, os.path.relpath(files[-1], ROOT)
-    return None, None
+        d = json.load(fh)
+    return d.get("kernels", {}), os.path.relpath(files[-1], ROOT), d.get("lib_sha16") != _lib_sha16()
 
 
 def _traffic(table, src, *names, calls_per_step=None):
-    """PMC HBM bytes per CALL of a kernel label: the label's dispatches of one step summed (a GEMM
-    call may be a main and a tail launch) / the calls per step; the per-dispatch average when the
-    table predates per-step sums or the call count is unknown."""
+    """PMC HBM bytes per CALL of a kernel label: every dispatch of the call in one step summed / the
+    calls per step.  A persistent GEMM call may be a main launch plus a tail launch of another row
+    tile (k_gemm_p<256, ...> + k_gemm_p<160, ...>): all row-tile variants of the label count.  The
+    per-dispatch average when the table predates per-step sums or the call count is unknown."""
+    import re
     for n in names:
-        if n in table:
-            e = table[n]
-            if calls_per_step and "hbm_bytes_per_step" in e:
-                return round(e["hbm_bytes_per_step"] / calls_per_step), f"{src}: {n} (per call)"
-            return e["hbm_bytes_per_launch"], f"{src}: {n} (per dispatch)"
+        m = re.match(r"(k_gemm_p|k_gemm_f8)<\d+, (.*)>$", n)
+        keys = ([k for k in table if re.match(re.escape(m[1]) + r"<\d+, " + re.escape(m[2]) + ">$", k)]
+                if m else [n] if n in table else [])
+        if not keys:
+            continue
+        if calls_per_step and all("hbm_bytes_per_step" in table[k] for k in keys):
+            tot = sum(table[k]["hbm_bytes_per_step"] for k in keys)
+            return round(tot / calls_per_step), f"{src}: {' + '.join(sorted(keys))} (per call)"
+        return table[keys[0]]["hbm_bytes_per_launch"], f"{src}: {keys[0]} (per dispatch)"
     return None, None
+
+
+def _clock_probe(device, iters=16384):
+    """Shader clock (GHz) the chip holds under a dense bf16 MFMA loop right now: median over one
+    workgroup per CU of s_memtime ticks / s_memrealtime (100 MHz) ticks (i2pc_clock_probe)."""
+    import torch
+    from image_to_pointcloud_amd import _lib
+    props = torch.cuda.get_device_properties(device)
+    wg = int(props.multi_processor_count)
+    out = torch.zeros(2 * wg, dtype=torch.int64, device=device)
+    _lib.call("i2pc_clock_probe", wg, iters, out.data_ptr(), torch.cuda.current_stream(device).cuda_stream)
+    v = out.view(wg, 2).double().cpu()
+    ghz = sorted((v[:, 0] / v[:, 1] * 0.1).tolist())
+    return ghz[len(ghz) // 2]
 
 
 def _cpu_model() -> str:
@@ -301,6 +301,7 @@ def _multi_gpu_diag(a, pipe, images, og, own_s, world, device):
             "gather_wait_ms": round(float(v[2]), 3)} for r, v in enumerate(allv)]
     return {"world": world, "backend": backend,
             "rccl_world_size": dist.get_world_size() if backend == "nccl" else None,
+            "rccl_max_channels": int(os.environ["NCCL_MAX_NCHANNELS"]) if backend == "nccl" else None,
             "all_gather": og is not None,
             "gathered_bytes_per_step_per_rank": og.recv_bytes_per_step if og is not None else 0,
             "sent_bytes_per_step_per_rank": og.send_bytes_per_step if og is not None else 0,
@@ -329,6 +330,7 @@ def main():
                       f"--backend gloo lets ranks share one)", file=sys.stderr)
                 sys.exit(2)
             torch.cuda.set_device(local)
+            D.cap_rccl_channels()               # bound RCCL's CU share before the communicator exists
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             local = local % max(ndev, 1)
@@ -355,7 +357,7 @@ def main():
             pipe.capture(images)
             pipe2.capture(images)
             runs = [pipe.replay, pipe2.replay]
-        og = D.OverlappedGather(runs, world, B, pipe.points_per_image, device)
+        og = D.OverlappedGather(runs, world, B, pipe.points_per_image, device, timing=True)
         step, finish = og.step, og.finish
     elif a.no_graph:
         step = lambda: pipe.run(images)     # noqa: E731
@@ -372,6 +374,12 @@ def main():
     torch.cuda.synchronize()
     if gather:
         og.reset_stats()
+    # the shader clock this box holds under dense MFMA load, right before and right after the timed
+    # steps (outside the timed region), so the line's fractions can be read at the run's own clock
+    clk0 = _clock_probe(device) if rank == 0 else None
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
@@ -380,6 +388,13 @@ def main():
     if world > 1:
         dist.barrier()
     own = time.perf_counter() - t0
+    clk1 = _clock_probe(device) if rank == 0 else None
+    clock = None
+    if rank == 0:
+        clock = {"before": round(clk0, 4), "after": round(clk1, 4), "ghz": round((clk0 + clk1) / 2, 4),
+                 "method": "i2pc_clock_probe: one workgroup per CU, 4 x 16384 dense bf16 32x32x16 MFMAs on random "
+                           "operands, median over CUs of s_memtime / s_memrealtime ticks x 0.1 GHz; run right "
+                           "before and right after the timed steps"}
     elapsed = D.max_over_ranks(own, device)
     multi = _multi_gpu_diag(a, pipe, images, og if gather else None, own, world, device) if world > 1 else None
     points_step = world * B * pipe.points_per_image
@@ -390,8 +405,8 @@ def main():
     kernels = None
     if rank == 0 and not a.no_kernel_profile:
         per, geo_t, unp_t = _kernel_profile(pipe, images)
-        pmc, pmc_src = _pmc_traffic(f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
-                                    + ("" if a.density == "high" else f"-{a.density}"))
+        pmc, pmc_src, pmc_stale = _pmc_traffic(f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
+                                               + ("" if a.density == "high" else f"-{a.density}"))
         dom = max(per.items(), key=lambda kv: kv[1]["t"])
         name, d = dom
         # the bound of a kernel: whichever of its algorithmic FLOPs (at the dtype's dense MFMA peak)
@@ -410,18 +425,14 @@ def main():
             roofline["algorithmic_bytes_per_launch"] = round(d["bytes"] / d["n"])
             if roofline["traffic"]:
                 roofline["traffic_over_algorithmic"] = round(roofline["traffic"] / (d["bytes"] / d["n"]), 3)
-            tag = (f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
-                   + ("" if a.density == "high" else f"-{a.density}"))
-            clk, clk_src = _profiled_clock(tag, name)
-            if clk:
-                # beside frac, not instead of it: frac at the clock the chip held in the profiled pass
-                roofline["clock_ghz_profiled"] = clk
-                roofline["frac_at_profiled_clock"] = round(ach / (pk * clk / 2.4), 4)
-                roofline["clock_source"] = clk_src
+            # beside frac, not instead of it: the peak scaled to the clock this run's probe measured
+            roofline["clock_ghz_run"] = clock["ghz"]
+            roofline["frac_at_run_clock"] = round(ach / (pk * clock["ghz"] / 2.4), 4)
             if name.startswith("k_gemm_p"):
-                roofline["note"] = ("avg_us and traffic are per i2pc_gemm call: the persistent launch plus, where "
-                                    "the round-quantisation split applies (QKV), its 256x128 tail launch; rocprofv3 "
-                                    "lists them as k_gemm_p<..., 256, ...> and k_gemm_p<..., 128, ...>")
+                roofline["note"] = ("avg_us and traffic are per i2pc_gemm call: the persistent launch plus its tail "
+                                    "launches (a 256x128 round-quantisation tail, or rows past the last full round on "
+                                    "smaller row tiles); rocprofv3 lists them as k_gemm_p<256, ...> and "
+                                    "k_gemm_p<160, ...>, and traffic sums every one of them")
         else:
             ach = d["bytes"] / (d["t"]) / 1e9
             roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -433,6 +444,8 @@ def main():
             roofline["traffic"], roofline["traffic_source"] = _traffic(pmc, pmc_src, name, calls_per_step=d["n"])
             if roofline["traffic"]:
                 roofline["traffic_over_algorithmic"] = round(roofline["traffic"] / (d["bytes"] / d["n"]), 3)
+        if roofline.get("traffic"):
+            roofline["traffic_stale"] = pmc_stale     # the PMC table came from another libi2pc.so build
         geo_bytes = B * (4.0 * pipe.pre.out_h * pipe.pre.out_w + 18.0 * pipe.points_per_image)
         roof_geo = {"kernel": "i2pc_unproject (select + unproject + bbox launches)", "bound": "hbm",
                     "achieved": round(geo_bytes / geo_t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -451,15 +464,8 @@ def main():
             t, src = _traffic(pmc, pmc_src, f"k_unproject_rows<{step}>", f"k_unproject_fast<{step}>",
                               calls_per_step=1)
             rooflines["unproject_kernel"].update(traffic=t, traffic_source=src)
-            tag = (f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
-                   + ("" if a.density == "high" else f"-{a.density}"))
-            for kname in (f"void i2pc::unproj::k_unproject_rows<{step}>", f"void i2pc::unproj::k_unproject_fast<{step}>"):
-                us, us_src = _profiled_us(tag, kname)
-                if us:
-                    rooflines["unproject_kernel"].update(
-                        us_profiled=round(us, 1), frac_profiled=round(geo_bytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                        profiled_source=us_src)
-                    break
+            if t:
+                rooflines["unproject_kernel"]["traffic_over_algorithmic"] = round(t / geo_bytes, 3)
         net_t = sum(v["t"] for v in per.values())
         net_f = sum(v["flops"] for v in per.values())
         # mixed-precision networks: the peak is the FLOP-weighted harmonic mean of the kernels'
@@ -470,6 +476,7 @@ def main():
                                    "bound": "mfma", "achieved": round(net_f / net_t / 1e12, 1),
                                    "peak": round(mix_peak, 1), "unit": "TFLOP/s",
                                    "frac": round(t_peak / net_t, 4), "traffic": None,
+                                   "frac_at_run_clock": round(t_peak / net_t * 2.4 / clock["ghz"], 4),
                                    "ms": round(net_t * 1e3, 3),
                                    "fp8_flop_share": round(sum(v["flops"] for k, v in per.items()
                                                                if k.startswith("k_gemm_f8")) / max(net_f, 1.0), 4),
@@ -509,6 +516,7 @@ def main():
                        "hip_graph": not a.no_graph},
             "network_tflops": round(flops_img * B * world / (elapsed / a.steps) / 1e12, 1),
             "roofline": roofline,
+            "clock": clock,
             "rooflines": rooflines,
             "cpu_baseline": cpu,
             "multi_gpu": multi,

@@ -35,6 +35,7 @@ SOURCES = [
     "area.hip",
     "fp8.hip",
     "bit.hip",
+    "probe.hip",
     "comm.cpp",
     "writers.cpp",
 ]

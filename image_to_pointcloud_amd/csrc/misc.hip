@@ -310,6 +310,31 @@ __global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, i
   }
 }
 
+// DIAGNOSTIC (r05 root-cause of the r04 nondeterminism): the r04 grid-stride form, knob "ln_apply_gs".
+__global__ __launch_bounds__(256) void k_ln_apply_gs(const uint4* __restrict__ x, int64_t ldx8, const float2* __restrict__ rs,
+                                                     const float4* __restrict__ gamma, const float4* __restrict__ beta,
+                                                     int rows, int d8, uint4* __restrict__ y, int64_t ldy8) {
+  const int64_t n = (int64_t)rows * d8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int r = (int)(i / d8);
+    const int c = (int)(i - (int64_t)r * d8);
+    const uint4 v = x[r * ldx8 + c];
+    const float2 s = rs[r];
+    const float4 g0 = gamma[2 * c], g1 = gamma[2 * c + 1], b0 = beta[2 * c], b1 = beta[2 * c + 1];
+    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float lo = __builtin_fmaf(g[2 * t], __builtin_fmaf(__uint_as_float(q[t] << 16), s.x, s.y), b[2 * t]);
+      const float hi = __builtin_fmaf(g[2 * t + 1], __builtin_fmaf(__uint_as_float(q[t] & 0xffff0000u), s.x, s.y), b[2 * t + 1]);
+      o[t] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    y[r * ldy8 + c] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 static int grid_for(int64_t work, int per_block = 256) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((work + per_block - 1) / per_block, 256 * 16));
 }
@@ -321,9 +346,11 @@ using namespace i2pc;
 using namespace i2pc::misc;
 
 static thread_local int g_ln2 = 1;   // "ln_f2": the float2 row kernel for dim 384
+static thread_local int g_ln_apply_gs = 0;   // "ln_apply_gs": DIAGNOSTIC, the r04 grid-stride ln_apply
 
 bool i2pc_misc_tune(const char* name, int value) {
   if (std::strcmp(name, "ln_f2") == 0) { g_ln2 = value; return true; }
+  if (std::strcmp(name, "ln_apply_gs") == 0) { g_ln_apply_gs = value; return true; }
   return false;
 }
 
@@ -349,6 +376,13 @@ extern "C" int i2pc_ln_apply(const void* x, int64_t ldx, const float* rows_stats
                    (reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) % 16 == 0,
                "ln_apply: 16-byte aligned operands");
   const int d8 = dim / 8;
+  if (g_ln_apply_gs) {
+    hipLaunchKernelGGL(k_ln_apply_gs, dim3(grid_for((int64_t)rows * d8)), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint4*>(x), ldx / 8, reinterpret_cast<const float2*>(rows_stats),
+                       reinterpret_cast<const float4*>(gamma), reinterpret_cast<const float4*>(beta), rows, d8,
+                       static_cast<uint4*>(y), ldy / 8);
+    return check_launch("ln_apply");
+  }
   for (int r0 = 0; r0 < rows; r0 += 65535) {   // (grid y <= 65535 rows per launch)
     const int nr = std::min(rows - r0, 65535);
     hipLaunchKernelGGL(k_ln_apply, dim3((d8 + 255) / 256, nr), dim3(256), 0, as_stream(stream),

@@ -13,6 +13,20 @@ from __future__ import annotations
 
 import os
 
+# RCCL's copy kernels run one workgroup per channel on the same CUs as the network.  C3's all-gather
+# needs ~3.5 GB received per rank per ~21 ms step (≈170 GB/s) at 8 ranks; 16 channels (16 of 256 CUs,
+# 6 %) carry several hundred GB/s over the 7 xGMI links, so the cap bounds RCCL's share of the chip
+# without exposing the gather.  Read by RCCL when the communicator is created.
+RCCL_MAX_CHANNELS = 16
+
+
+def cap_rccl_channels(n: int = None) -> int:
+    """Bound the channels (= CUs) RCCL's collectives may take: sets NCCL_MAX_NCHANNELS unless the
+    environment already does.  Call before the process group / communicator is created.  Returns
+    the cap in force."""
+    os.environ.setdefault("NCCL_MAX_NCHANNELS", str(int(n or RCCL_MAX_CHANNELS)))
+    return int(os.environ["NCCL_MAX_NCHANNELS"])
+
 
 def world():
     """(rank, local_rank, world_size) from the torch.distributed.run environment."""
@@ -58,14 +72,18 @@ class OverlappedGather:
 
     With a gloo process group and device buffers (ranks sharing one GPU, the 1-GPU rehearsal
     of the multi-rank path) the gather is staged through host memory and runs synchronously:
-    gloo moves host tensors; the results are the same bytes."""
+    gloo moves host tensors; the results are the same bytes.
 
-    def __init__(self, runs, world: int, batch: int, points: int, device, group=None):
+    timing=True records an event pair around every wait of the compute stream on a gather
+    (gather_wait_ms; bench.py at N > 1).  Completed pairs are folded into a running total, so a
+    long-running loop keeps at most the pairs still in flight."""
+
+    def __init__(self, runs, world: int, batch: int, points: int, device, group=None, timing: bool = False):
         import torch
         import torch.distributed as dist
         if len(runs) != 2:
             raise ValueError("OverlappedGather needs two step callables (double-buffered point sets)")
-        self.runs, self.group = runs, group
+        self.runs, self.group, self.timing = runs, group, timing
         self.world = dist.get_world_size(group)
         self.gx = [torch.empty((world * batch, points, 3), dtype=torch.float32, device=device) for _ in range(2)]
         self.gr = [torch.empty((world * batch, points, 3), dtype=torch.uint8, device=device) for _ in range(2)]
@@ -80,20 +98,24 @@ class OverlappedGather:
 
     def reset_stats(self):
         """Start a new gather-wait measurement (gather_wait_ms)."""
-        self._wait_s = 0.0         # host-side waits (host-staged gloo, CPU tensors)
+        self._wait_s = 0.0         # host-side waits (host-staged gloo, CPU tensors) + folded event pairs
         self._events = []          # (before, after) CUDA events around the compute stream's waits
 
     def gather_wait_ms(self) -> float:
         """Milliseconds the compute stream (or, host-staged, the host) spent waiting for gathers since
         reset_stats(): for an async RCCL gather the gap between an event recorded before the stream's
         wait on the collective and one recorded after it (0 when the gather finished under the next
-        step's compute)."""
-        ms = self._wait_s * 1e3
+        step's compute).  Device waits are only measured with timing=True."""
         if self._events:
-            import torch
-            torch.cuda.synchronize()
-            ms += sum(a.elapsed_time(b) for a, b in self._events)
-        return ms
+            self._events[-1][1].synchronize()
+            self._fold()
+        return self._wait_s * 1e3
+
+    def _fold(self):
+        """Add the completed (before, after) pairs to the running total and drop them."""
+        while self._events and self._events[0][1].query():
+            a, b = self._events.pop(0)
+            self._wait_s += a.elapsed_time(b) * 1e-3
 
     def step(self):
         import torch.distributed as dist
@@ -121,13 +143,18 @@ class OverlappedGather:
         w = self.works[slot]
         if w is not None:
             if self.gx[0].is_cuda:
-                import torch
-                before, after = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                before.record()
-                for x in w:
-                    x.wait()
-                after.record()
-                self._events.append((before, after))
+                if not self.timing:
+                    for x in w:
+                        x.wait()
+                else:
+                    import torch
+                    before, after = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    before.record()
+                    for x in w:
+                        x.wait()
+                    after.record()
+                    self._fold()
+                    self._events.append((before, after))
             else:
                 import time
                 t0 = time.perf_counter()

@@ -175,6 +175,13 @@ int i2pc_depth_preview(const float* depth, int batch, int h, int w, int invert, 
 int i2pc_profile_enable(int on);
 float i2pc_profile_unproject_ms(void);
 
+/* Measurement aid (no reference counterpart; bench.py's clock_ghz_run): `workgroups` 256-thread
+ * workgroups (one per CU: 256) run `iters` x 4 dense bf16 32x32x16 MFMAs on random operands; for
+ * workgroup g, out[2g] = shader-clock ticks (s_memtime) and out[2g + 1] = 100 MHz ticks
+ * (s_memrealtime) of the chain, so the clock held under MFMA load is out[2g] / out[2g + 1] * 0.1 GHz.
+ * out: device buffer of 2 * workgroups u64. */
+int i2pc_clock_probe(int workgroups, int iters, unsigned long long* out, void* stream);
+
 /* Gather every stride-th point (preview subsample, app.py:496-506):
  * out_xyz/out_rgb [count] with count = ceil(n / stride). */
 int i2pc_gather_stride(const float* xyz, const uint8_t* rgb, int64_t n, int64_t stride,

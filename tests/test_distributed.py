@@ -217,3 +217,13 @@ def test_gather_band_points_assembles_the_image():
     for rank, out in res:
         for gx, gr, full in out:
             assert (gx == full).all() and (gr == (full % 256).astype("uint8")).all()
+
+
+def test_cap_rccl_channels_sets_default_and_keeps_user_value(monkeypatch):
+    """bench.py bounds RCCL's CU share before init_process_group("nccl"): NCCL_MAX_NCHANNELS is set
+    to the default cap unless the environment already names one."""
+    monkeypatch.delenv("NCCL_MAX_NCHANNELS", raising=False)
+    assert D.cap_rccl_channels() == D.RCCL_MAX_CHANNELS
+    assert os.environ["NCCL_MAX_NCHANNELS"] == str(D.RCCL_MAX_CHANNELS)
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "4")
+    assert D.cap_rccl_channels() == 4

@@ -82,6 +82,64 @@ def test_overlapped_gather_two_ranks_on_device_bit_identical():
     assert out[0][3].tobytes() != out[1][3].tobytes()     # the ranks really had different images
 
 
+def _nccl_worker(port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from image_to_pointcloud_amd import distributed as D, geometry
+    from image_to_pointcloud_amd.depth_anything import DA_V2_SMALL
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    import bench
+    cap = D.cap_rccl_channels()                 # as bench.py does before init_process_group("nccl")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        B, S = 2, 256
+        pipe = PointCloudPipeline(B, S, S, spec=DA_V2_SMALL, density="medium", device=dev, seed=0)
+        pipe2 = PointCloudPipeline(B, S, S, spec=DA_V2_SMALL, density="medium", device=dev, model=pipe.model)
+        images = bench._images(B, S, 0, dev)
+        pipe.capture(images)
+        pipe2.capture(images)
+        og = D.OverlappedGather([pipe.replay, pipe2.replay], 1, B, pipe.points_per_image, dev, timing=True)
+        assert dist.get_backend() == "nccl" and not og.host_staged      # the async RCCL branch
+        slots = [og.step() for _ in range(3)]
+        og.finish()
+        wait_ms = og.gather_wait_ms()
+        pending = len(og._events)
+        gx, gr = og.gathered(slots[-1])
+        gx0, gr0 = og.gathered(slots[-2])
+        pipe.infer_depth(images)
+        mine = geometry.unproject_batch(pipe.depth, images, density="medium")
+        torch.cuda.synchronize()
+        q.put((gx.cpu().numpy(), gr.cpu().numpy(), gx0.cpu().numpy(), gr0.cpu().numpy(),
+               mine.xyz.cpu().numpy(), mine.rgb.cpu().numpy(), wait_ms, pending, cap,
+               os.environ.get("NCCL_MAX_NCHANNELS")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_gather_rccl_world1_async_branch():
+    """The RCCL data path of OverlappedGather (the async all_gather_into_tensor works and the
+    compute stream's event-timed waits on them) on a world-size-1 nccl group on cuda:0, with the
+    channel cap bench.py sets: three steps over the two graph-captured slots; both slots' gathered
+    buffers equal the rank's own points (an eager unprojection of the same depth), and the
+    gather-wait figure is finite with no event pair left pending after it is read."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        gx, gr, gx0, gr0, mx, mr, wait_ms, pending, cap, env_cap = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0
+    assert gx.tobytes() == mx.tobytes() and gr.tobytes() == mr.tobytes()
+    assert gx0.tobytes() == mx.tobytes() and gr0.tobytes() == mr.tobytes()
+    assert np.isfinite(wait_ms) and wait_ms >= 0.0 and pending == 0
+    assert cap == int(env_cap) > 0
+
+
 def test_bench_gpus_2_launches_two_ranks():
     """`python bench.py --gpus 2` (no launcher env) starts torch.distributed.run with two ranks as a
     child process and prints rank 0's line with n_gpus 2 and the all-gather in the workload."""

@@ -1,5 +1,14 @@
 """Diagnostic: N processes on one GPU each run the network forward R times (eager, no sync between
-runs except the final compare) and count how many runs differ from their first."""
+runs except the final compare) and count how many runs differ from their first.
+
+    python tools/det_rep.py N R GRAPH [model]
+
+Environment knobs (r05 root-cause of the r04 nondeterminism):
+  DET_GS=1       the r04 grid-stride i2pc_ln_apply (tuning knob "ln_apply_gs")
+  DET_PROBE=1    wrap ops.ln_apply: copy its inputs (x, row stats) right before and its output right
+                 after each call (stream-ordered copies), and report per call whether the inputs, the
+                 output at the call, and the hidden state at the end of the forward match run 1
+  DET_SYNC=1     with DET_PROBE, a host synchronise right after each ln_apply"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -7,16 +16,34 @@ import torch
 
 def worker(rank, q, model, reps, graph):
     import bench
+    from image_to_pointcloud_amd import _lib, ops
     from image_to_pointcloud_amd.pipeline import PointCloudPipeline
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if os.environ.get("DET_GS") == "1":
+        _lib.call("i2pc_set_tuning", b"ln_apply_gs", 1)
+    probe = os.environ.get("DET_PROBE") == "1"
+    sync = os.environ.get("DET_SYNC") == "1"
+    rec = []
+    if probe:
+        orig = ops.ln_apply
+
+        def wrapped(x, rs, g, b, out=None):
+            xin, rsin = x.clone(), rs.clone()
+            o = orig(x, rs, g, b, out=out)
+            if sync:
+                torch.cuda.synchronize()
+            rec.append((xin, rsin, o.clone()))
+            return o
+        ops.ln_apply = wrapped
     B, S = 2, 256
     pipe = PointCloudPipeline(B, S, S, spec=bench._spec(model), density="medium", device=dev, seed=0)
     images = bench._images(B, S, rank, dev)
     if graph:
         pipe.capture(images)
-    outs, hss, rss = [], [], []
+    outs, hss, rss, recs = [], [], [], []
     for _ in range(reps):
+        rec.clear()
         if graph:
             pipe.replay()
         else:
@@ -25,11 +52,21 @@ def worker(rank, q, model, reps, graph):
         bufs = next(iter(pipe.model._bufs.values()))
         hss.append([h.clone() for h in bufs["hs"]])
         rss.append(bufs["rs"].clone())
+        recs.append(list(rec))
     torch.cuda.synchronize()
     bad = sum(0 if torch.equal(o, outs[1]) else 1 for o in outs[1:])
     badh = [sum(0 if torch.equal(h[k], hss[1][k]) else 1 for h in hss[1:]) for k in range(len(hss[0]))]
     badr = sum(0 if torch.equal(r, rss[1]) else 1 for r in rss[1:])
-    q.put((rank, f"proc {rank} graph={graph}: {bad} of {reps - 1} runs differ from run 1; hs differ {badh}; last rs {badr}"))
+    msg = f"proc {rank} graph={graph}: {bad} of {reps - 1} runs differ from run 1; hs differ {badh}; last rs {badr}"
+    if probe and recs[1]:
+        n = len(recs[1])
+        bx = [sum(0 if torch.equal(r[k][0], recs[1][k][0]) else 1 for r in recs[1:]) for k in range(n)]
+        br = [sum(0 if torch.equal(r[k][1], recs[1][k][1]) else 1 for r in recs[1:]) for k in range(n)]
+        bo = [sum(0 if torch.equal(r[k][2], recs[1][k][2]) else 1 for r in recs[1:]) for k in range(n)]
+        # the output at the call against the hidden state at the end of the same forward
+        late = [sum(0 if torch.equal(recs[j][k][2], hss[j][k]) else 1 for j in range(1, reps)) for k in range(n)]
+        msg += f"; probe: x differ {bx}, rs differ {br}, out-at-call differ {bo}, out-at-call != final hs {late}"
+    q.put((rank, msg))
 
 
 if __name__ == "__main__":
