@@ -227,6 +227,7 @@ def _cpu_baseline(spec, size, density, images=3):
     model = Net(Cfg(**spec.hf_config_kwargs()))
     model.load_state_dict(synthetic_state_dict(spec, 0), strict=False)
     model.eval()
+    _log(f"CPU baseline: transformers {spec.name} built, {threads} threads")
     proc = default_processor(spec)
     psize = proc.size if spec.family == "depth-anything" else (spec.image, spec.image)
     t_net = t_geo = 0.0
@@ -246,6 +247,7 @@ def _cpu_baseline(spec, size, density, images=3):
         t_net += t1 - t0
         t_geo += t2 - t1
         n += len(pts)
+        _log(f"CPU baseline: image {i} network {t1 - t0:.2f} s, per-point loop {t2 - t1:.2f} s")
     return {"value": n / (t_net + t_geo) / 1e6, "unit": "Mpoints/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
             "sample": f"{images} images {size}x{size}, density {density} ({n} points): Pillow-exact preprocessing + "
@@ -308,6 +310,11 @@ def _multi_gpu_diag(a, pipe, images, og, own_s, world, device):
             "per_rank": per}
 
 
+def _log(msg: str) -> None:
+    """Progress on stderr (a GPU run that writes nothing for minutes looks hung to its supervisor)."""
+    print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = _args()
     env_world = os.environ.get("WORLD_SIZE")
@@ -343,6 +350,7 @@ def main():
     spec = _spec(a.model)
 
     B, S = a.batch, a.size
+    _log(f"rank {rank}/{world}: building {spec.name} {a.dtype} pipeline, batch {B} x {S}^2")
     pipe = PointCloudPipeline(B, S, S, spec=spec, density=a.density, device=device, seed=0, dtype=a.dtype)
     images = _images(B, S, rank, device)
     gather = world > 1 and not a.no_all_gather
@@ -365,6 +373,7 @@ def main():
     else:
         pipe.capture(images)
         step = pipe.replay
+    _log("captured; warming up")
     for _ in range(a.warmup):
         step()
     finish()
@@ -403,7 +412,9 @@ def main():
 
     roofline = roof_geo = rooflines = None
     kernels = None
+    _log(f"timed {a.steps} steps: {ms:.3f} ms per step")
     if rank == 0 and not a.no_kernel_profile:
+        _log("kernel profile (eager, HIP events)")
         per, geo_t, unp_t = _kernel_profile(pipe, images)
         pmc, pmc_src, pmc_stale = _pmc_traffic(f"{spec.name}-{a.dtype}" + ("" if S == 1024 else f"-{S}")
                                                + ("" if a.density == "high" else f"-{a.density}"))
@@ -491,6 +502,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        _log("CPU baseline (restated reference path)")
         try:
             cpu = _cpu_baseline(spec, S, a.density)
         except Exception as e:   # the GPU figure stands on its own; say why the baseline is missing

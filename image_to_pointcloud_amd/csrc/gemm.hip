@@ -1333,240 +1333,11 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     after_epi = true;
   }
 }
-// ---------------------------------------------------------------------------
-// Quarter-pipelined persistent 256 x 256 x 64 bf16 engine (k_gemm_q).  The LDS holds two
-// K-tiles (128 KB), each split into four 16-KB quarters: A-q0 / A-q1 (the 64-row halves
-// mp of both 128-row wave halves) and B-q0 / B-q1 (the 32-column halves np of every wave's
-// 64 columns).  A K-tile is computed in four phases, one (mp, np) quadrant of every wave's
-// 128 x 64 output each: (0,0) (0,1) (1,1) (1,0), with the A fragments of a quadrant reused by
-// the next one and the B-q0 fragments kept in registers from phase 1 to phase 4.  A quarter is
-// therefore last read in phase 1 (A-q0, B-q0), 2 (B-q1) or 3 (A-q1), and is refilled with the
-// K-tile two ahead right after that phase's barrier: every quarter has two K-tiles of
-// latency cover instead of one, and at most ~7/8 of the LDS is in flight at any time.
-// One barrier per phase: [ds_read this phase's quarter] [lgkmcnt(0)] [vmcnt(N): the quarter
-// the next phase reads has landed] [s_barrier] [refill the quarter this phase released]
-// [16 MFMAs].  The counts N are exact because every wave issues the same 2 glds per quarter;
-// an epilogue between two tiles adds its E_ALL operations to the first waits of the next tile.
-// acc[i][j] covers rows wm*128 + i*16 + (lane & 15), columns wn*64 + j*16 + (lane >> 4)*4 --
-// the k_gemm_p layout, so epilogue_p is shared (bias read from global memory).
+// Counted vmcnt wait (k_gemm_8p): sched barrier, then wait until at most N vector-memory operations remain.
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N < 63 ? N : 63) : "memory");
-}
-
-template <bool CONV, bool RELU_A, int EPI>
-__global__ __launch_bounds__(512) void k_gemm_q(Args p) {
-  constexpr int BM = 256, BN = 256, RM = 8, RN = 4, ROWB = 128, QB = 128 * ROWB;   // quarter bytes
-  constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
-  constexpr int E_ALL = RM * (NRL + NS);
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];   // [2][A-q0, A-q1, B-q0, B-q1]
-
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int frow = lane & 15, fq = lane >> 4;
-  const int lrow = lane >> 3, pchunk = lane & 7;
-
-  const int T = p.tiles_m * p.tiles_n;
-  const int G = gridDim.x;
-  const int xcd = blockIdx.x & 7, xl = blockIdx.x >> 3, xq = G >> 3, xr = G & 7;
-  int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + xl;
-  if (t >= T) return;
-
-  const rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, p.a_bytes, 0x00020000);
-  const rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.W), 0, p.w_bytes, 0x00020000);
-  const int chunk16 = (pchunk ^ lrow) << 4;
-  // quarter row r (0..127) -> tile row / column; this wave fills quarter rows wid*16 + j*8 + lrow
-  auto a_row = [&](int mp, int j) { const int r = wid * 16 + j * 8 + lrow; return (r >> 6) * 128 + mp * 64 + (r & 63); };
-  auto b_row = [&](int np, int j) { const int r = wid * 16 + j * 8 + lrow; return (r >> 5) * 64 + np * 32 + (r & 31); };
-
-  uint32_t a_off[2][2], w_off[2][2];       // dense A / W byte offsets of this lane's rows [quarter][j]
-  int cpix[2][2], cyx[2][2];               // conv: pixel of this lane's A rows
-  int nm0 = 0, nn0 = 0;
-  auto setup = [&](int tile) {
-    int tm, tn;
-    grouped(p, tile, tm, tn);
-    nm0 = tm * BM;
-    nn0 = tn * BN;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int m = nm0 + a_row(q, j);
-        if constexpr (!CONV) {
-          a_off[q][j] = (uint32_t)m * (uint32_t)(p.lda * 2) + chunk16;
-        } else {
-          const int hw = p.coh * p.cow;
-          const int b = m / hw;
-          const int rem = m - b * hw;
-          const int oy = rem / p.cow;
-          const int ox = rem - oy * p.cow;
-          cpix[q][j] = b * p.ch * p.cw;
-          cyx[q][j] = m < p.M ? ((oy * p.cs - p.cp) << 16) | ((ox * p.cs - p.cp) & 0xffff) : (int)(0x4000u << 16);
-        }
-        w_off[q][j] = (uint32_t)(nn0 + b_row(q, j)) * (uint32_t)(p.ldw * 2) + chunk16;
-      }
-  };
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  // one quarter (0: A-q0, 1: A-q1, 2: B-q0, 3: B-q1) of K-tile k0 into buffer `buf`
-  auto fill = [&](int buf, int quarter, int k0) {
-    uint8_t* dst = smem + (buf * 4 + quarter) * QB + wid * 16 * ROWB;
-    if (quarter < 2) {
-      const int q = quarter;
-      if constexpr (!CONV) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(dst + j * 8 * ROWB), 16, a_off[q][j], k0 * 2, 0, 0);
-      } else {
-        const int kk = k0 / p.cc;
-        const int ky = kk / p.ck;
-        const int kx = kk - ky * p.ck;
-        const int ci0 = k0 - kk * p.cc;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int yi = (cyx[q][j] >> 16) + ky, xi = ((int)(short)(cyx[q][j] & 0xffff)) + kx;
-          const bool ok = (unsigned)yi < (unsigned)p.ch && (unsigned)xi < (unsigned)p.cw;
-          const int off = ok ? ((cpix[q][j] + yi * p.cw + xi) * p.cc + ci0) * 2 + chunk16 : OOB;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(dst + j * 8 * ROWB), 16, off, 0, 0, 0);
-        }
-      }
-    } else {
-      const int q = quarter - 2;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rs, (lds_ptr_t)(dst + j * 8 * ROWB), 16, w_off[q][j], k0 * 2, 0, 0);
-    }
-  };
-  auto read_frag = [&](int buf, int quarter, int row, int s) {
-    const uint8_t* base = smem + (buf * 4 + quarter) * QB + row * ROWB;
-    return *reinterpret_cast<const bf16x8*>(base + (((4 * s + fq) ^ (row & 7)) << 4));
-  };
-
-  const rsrc_t c_rs = p.dbg_drop ? __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0, 0x00020000) : make_rsrc(p.C);
-  const rsrc_t r_rs = make_rsrc(p.res);
-  const rsrc_t r2_rs = make_rsrc(p.res2);
-  const int nk = p.K / BK;
-
-  setup(t);
-  // prologue: K-tiles 0 and 1 in quarter order
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    if (kt < nk) {
-      fill(kt, 0, kt * BK); fill(kt, 2, kt * BK); fill(kt, 3, kt * BK); fill(kt, 1, kt * BK);
-    }
-  }
-  if (nk >= 2) I2PC_WAIT_VM(12); else I2PC_WAIT_VM(0);
-  I2PC_LDS_BARRIER();
-
-  int g = 0;                 // global K-tile counter (buffer parity)
-  bool after_epi = false;
-  int m0 = nm0, n0 = nn0;
-  for (;;) {
-    const int t_next = t + G;
-    const bool has_next = t_next < T;
-    f32x4 acc[RM][RN];
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int kt = 0; kt < nk; ++kt) {
-      const int buf = g & 1;
-      // what K-tile two ahead is (this tile's, the next tile's, or none)
-      const bool ahead_here = kt + 2 < nk;
-      const bool ahead_next = !ahead_here && has_next;
-      const bool issue = ahead_here || ahead_next;
-      const int k_ahead = ahead_here ? (kt + 2) * BK : (kt + 2 - nk) * BK;
-      if (kt == nk - 2 && has_next) setup(t_next);        // (nk >= 2) offsets switch to the next tile
-      // the epilogue of the previous tile issued E_ALL operations after the loads that the
-      // first waits of K-tiles 0 and 1 target; with nothing issued ahead (the last tile's
-      // tail) the counted waits would undercount: wait for everything there
-      const bool epi_gap = after_epi && kt < 2;
-      const bool tail = !has_next && kt + 2 >= nk;
-      bf16x8 af[4][2], b0[2][2], b1[2][2];
-      // ---------------- phase 1: (mp 0, np 0)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) af[i][s] = read_frag(buf, 0, wm * 64 + i * 16 + frow, s);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) b0[j][s] = read_frag(buf, 2, wn * 32 + j * 16 + frow, s);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (tail) I2PC_WAIT_VM(0);
-      else if (epi_gap) wait_vm<10 + E_ALL>();
-      else I2PC_WAIT_VM(10);
-      I2PC_LDS_BARRIER();
-      if (issue) { fill(buf, 0, k_ahead); fill(buf, 2, k_ahead); }
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a, acc[i][j], 0, 0, 0);
-        }
-      // ---------------- phase 2: (mp 0, np 1)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) b1[j][s] = read_frag(buf, 3, wn * 32 + j * 16 + frow, s);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (tail) I2PC_WAIT_VM(0);
-      else if (epi_gap) wait_vm<12 + E_ALL>();
-      else I2PC_WAIT_VM(12);
-      I2PC_LDS_BARRIER();
-      if (issue) fill(buf, 3, k_ahead);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a, acc[i][2 + j], 0, 0, 0);
-        }
-      // ---------------- phase 3: (mp 1, np 1)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) af[i][s] = read_frag(buf, 1, wm * 64 + i * 16 + frow, s);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      I2PC_LDS_BARRIER();                                   // (phase 4 reads nothing new)
-      if (issue) fill(buf, 1, k_ahead);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][s], a, acc[4 + i][2 + j], 0, 0, 0);
-        }
-      // ---------------- phase 4: (mp 1, np 0): the next K-tile's A-q0 / B-q0 must land
-      if (tail) I2PC_WAIT_VM(0);
-      else if (epi_gap && kt == 0) wait_vm<12 + E_ALL>();
-      else I2PC_WAIT_VM(12);
-      I2PC_LDS_BARRIER();
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bf16x8 a = RELU_A ? relu8(af[i][s]) : af[i][s];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][s], a, acc[4 + i][j], 0, 0, 0);
-        }
-      ++g;
-    }
-    // ---- epilogue of tile (m0, n0): register-direct, counted; bias straight from memory
-    const float* bias = p.bias ? p.bias + n0 + wn * 64 : reinterpret_cast<const float*>(g_zero);
-    epilogue_p<RM, RN, EPI, false>(p, acc, m0 + wm * 128, n0 + wn * 64, bias, c_rs, r_rs, r2_rs, c_rs);
-    if (!has_next) break;
-    t = t_next;
-    m0 = nm0;
-    n0 = nn0;
-    after_epi = true;
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1858,31 +1629,6 @@ static void launch_8p(const Args& p, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
 }
 
-template <bool CONV, bool RELU_A, int EPI>
-static void launch_q(const Args& p, hipStream_t s) {
-  Args q = p;
-  if (!CONV) {
-    q.A = p.A + (int64_t)p.a_o * p.lda;
-    q.a_o = 0;
-    q.a_bytes = (uint32_t)((int64_t)p.M * p.lda * 2);
-  } else {
-    q.a_bytes = (uint32_t)((int64_t)p.cb * p.ch * p.cw * p.cc * 2);
-  }
-  q.w_bytes = (uint32_t)((int64_t)p.N * p.ldw * 2);
-  q.tiles_m = (p.M + 255) / 256;
-  q.tiles_n = p.N / 256;
-  q.group_m = group_m_for(q.tiles_m);
-  const int smem = 2 * 4 * 128 * 128;
-  auto kern = pers::k_gemm_q<CONV, RELU_A, EPI>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
-  const int grid = std::min(q.tiles_m * q.tiles_n, num_cus());
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
-}
-
 // Which kernel a call runs: the persistent 256-column engine when the epilogue is one it
 // implements and every byte offset fits its 31-bit buffer range; else the tile kernel.
 struct Plan {
@@ -2119,26 +1865,9 @@ static int run_split(const SplitPlan& sp, const Args& p, float* ws, hipStream_t 
   return check_launch("gemm (split-K)");
 }
 
-// I2PC_GEMM_Q=1: the quarter-pipelined engine (k_gemm_q) replaces k_gemm_p wherever the
-// persistent engine was chosen (K >= 128)
-static const int g_quarter = [] { const char* e = getenv("I2PC_GEMM_Q"); return e ? atoi(e) : 0; }();
-
 template <bool CONV, bool RELU_A>
 static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
   using namespace pers;
-  if (g_quarter && p.K >= 128 && pl.epi != EPI_LNF) {
-    if constexpr (!CONV && !RELU_A) {
-      if (pl.epi == EPI_PLAIN) { launch_q<false, false, EPI_PLAIN>(p, s); return check_launch("gemm_q"); }
-      if (pl.epi == EPI_RESF32) { launch_q<false, false, EPI_RESF32>(p, s); return check_launch("gemm_q"); }
-    } else if constexpr (CONV && !RELU_A) {
-      if (pl.epi == EPI_PLAIN) { launch_q<true, false, EPI_PLAIN>(p, s); return check_launch("gemm_q"); }
-      if (pl.epi == EPI_RESBF16) { launch_q<true, false, EPI_RESBF16>(p, s); return check_launch("gemm_q"); }
-      if (pl.epi == EPI_RES2) { launch_q<true, false, EPI_RES2>(p, s); return check_launch("gemm_q"); }
-    } else if constexpr (CONV && RELU_A) {
-      launch_q<true, true, EPI_PLAIN>(p, s);
-      return check_launch("gemm_q");
-    }
-  }
   if (pl.bn == 128) {   // plan: EPI_PLAIN (or EPI_LNF), no ReLU on A
     if constexpr (!RELU_A) {
       if constexpr (!CONV) {
@@ -2205,7 +1934,7 @@ static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
   if constexpr (!CONV && !RELU_A) {
     int ma = 0;
     const bool lnf = pl.epi == pers::EPI_LNF;
-    const int ts = (pl.kind == 1 || pl.kind == 2) && (pl.epi == pers::EPI_PLAIN || lnf) && pl.bn == 256 && !g_quarter
+    const int ts = (pl.kind == 1 || pl.kind == 2) && (pl.epi == pers::EPI_PLAIN || lnf) && pl.bn == 256
                        ? tail_split(p, ma) : 0;
     if (ts) {
       Args pa = p, pb = p;
@@ -2264,8 +1993,7 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu, const SplitPl
     snprintf(buf, sizeof buf, "k_gemm_8p<%s>", pl.epi == pers::EPI_PLAIN ? "plain" : "res_f32");
   } else if (pl.kind == 1) {
     static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8", "ln_fold", "ln_prod"};
-    if (g_quarter && pl.epi != pers::EPI_CT) snprintf(buf, sizeof buf, "k_gemm_q<%s, %s, %s>", c, r, epis[pl.epi]);
-    else if (pl.bn == 128) snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s, 128>", pl.bm, c, r, epis[pl.epi]);
+    if (pl.bn == 128) snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s, 128>", pl.bm, c, r, epis[pl.epi]);
     else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
   } else if (pl.kind == 0) {
     const int wm = pl.bn == 32 || pl.bn == 192 ? 4 : 2, wn = pl.bn == 256 ? 4 : pl.bn == 32 ? 1 : 2;
@@ -2335,112 +2063,6 @@ static int run8(const Plan8& pl, const Args& p, bool conv, bool relu, hipStream_
     launch_p<256, true, false, EPI_RES2, 256, true>(p, s);
   }
   return check_launch("gemm_fp8");
-}
-
-// ---- Skinny GEMM: M <= 64 rows (the DPT readout's CLS half, one row per image: M = batch, N = K =
-// hidden).  The tile kernel runs such a call as N / 64 tiles of 128 x 64, each a serial K-loop
-// (M 32, N 1024, K 1024: 16 tiles, 22.7 us for 67 MFLOP).  Here a workgroup owns 16 output
-// columns of up to 32 rows: its A rows are staged in LDS, thread (column c, slice q) takes the
-// 16-byte K chunks q, q + 16, q + 32, ... of its W row (a wave's 16 slice lanes read 256
-// contiguous bytes of W and of each A row: no LDS bank conflict), sums in fp32 per row, and the 16
-// slice lanes combine by xor shuffles (a fixed order: deterministic).  Then the tile epilogue's
-// bias and activation.  Knob "gemm_skinny" (I2PC_GEMM_SKINNY, default 0), automatic engine mode only.
-// Measured r04 (tools/diag27.sh / diag29.sh, C2): 40.7 us per readout call with a per-row guard in
-// the inner loop (every LDS read waited on alone), 26.3 us without it, against 22.7 us on the tile
-// kernel (C2 step 21.115 vs 21.064 ms) -- still slower, so off by default; kept as the starting point
-// (bit-stable, tested)
-static thread_local int g_skinny = [] { const char* e = getenv("I2PC_GEMM_SKINNY"); return e ? atoi(e) : 0; }();
-constexpr int kSkCols = 16, kSkRows = 32, kSkMaxK = 1024;   // LDS: (32 + 16) rows x K bf16 <= 96 KB
-
-__global__ __launch_bounds__(256) void k_gemm_skinny(Args p) {
-  extern __shared__ __attribute__((aligned(16))) bf16_t sa[];    // [rows][K]
-  const int n0 = blockIdx.x * kSkCols, m0 = blockIdx.y * kSkRows;
-  const int rows = min(kSkRows, p.M - m0);
-  const int K = p.K, kv = K / 8;                                   // 16-byte chunks per row
-  const int q = threadIdx.x & 15, n = n0 + (threadIdx.x >> 4);
-  // the A rows and the workgroup's 16 W rows into LDS ([rows][K] then [kSkCols][K]) by LDS-DMA: chunk
-  // i of that index space lands at LDS chunk i, so a wave's 64 lanes fill 1 KB in lane order; every
-  // load is in flight before the one wait (past the end: clamped sources into the LDS slack)
-  const int na = kSkRows * kv, total = na + kSkCols * kv;      // (all 32 rows: rows past M repeat row M - 1)
-  bf16_t* sw = sa + (size_t)kSkRows * K;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int b0 = wave * 64; b0 < total; b0 += 256) {
-    const int i = min(b0 + lane, total - 1);
-    const bool isa = i < na;
-    const int ia = isa ? i : i - na;
-    const int r = ia / kv, c = ia - r * kv;
-    const bf16_t* row = isa ? p.A + remap(min(m0 + r, p.M - 1), p.a_g, p.a_gs, p.a_o) * p.lda
-                            : p.W + (int64_t)min(n0 + r, p.N - 1) * p.ldw;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(row) + c,
-                                     (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(sa) + b0), 16, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float acc[kSkRows];
-#pragma unroll
-  for (int r = 0; r < kSkRows; ++r) acc[r] = 0.f;
-  if (n < p.N) {
-    const uint4* arow = reinterpret_cast<const uint4*>(sa);
-    const uint4* wrow = reinterpret_cast<const uint4*>(sw) + (threadIdx.x >> 4) * kv;   // (W after the rows A has)
-    for (int j = q; j < kv; j += 16) {
-      const uint4 wv = wrow[j];
-      const uint32_t wu[4] = {wv.x, wv.y, wv.z, wv.w};
-      float wf[8];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) { wf[2 * t] = __uint_as_float(wu[t] << 16); wf[2 * t + 1] = __uint_as_float(wu[t] & 0xffff0000u); }
-#pragma unroll
-      for (int r = 0; r < kSkRows; ++r) {     // (no row guard: the LDS reads batch)
-        const uint4 av = arow[r * kv + j];
-        const uint32_t au[4] = {av.x, av.y, av.z, av.w};
-        float sacc = acc[r];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          sacc = fmaf(__uint_as_float(au[t] << 16), wf[2 * t], sacc);
-          sacc = fmaf(__uint_as_float(au[t] & 0xffff0000u), wf[2 * t + 1], sacc);
-        }
-        acc[r] = sacc;
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < kSkRows; ++r) {
-    float v = acc[r];
-    v += __shfl_xor(v, 1); v += __shfl_xor(v, 2); v += __shfl_xor(v, 4); v += __shfl_xor(v, 8);
-    acc[r] = v;
-  }
-  if (n >= p.N) return;
-  const float bn = p.bias ? p.bias[n] : 0.f;
-#pragma unroll
-  for (int r = 0; r < kSkRows; ++r) {
-    if ((r & 15) == q && r < rows) {          // lane q writes rows q and q + 16
-      float v = acc[r] + bn;
-      if (p.act == 1) v = gelu_erf(v);
-      else if (p.act == 2) v = fmaxf(v, 0.f);
-      const int64_t off = (int64_t)(m0 + r) * p.ldc + n;
-      if (p.c_f32) static_cast<float*>(p.C)[off] = v;
-      else static_cast<bf16_t*>(p.C)[off] = f2bf(v);
-    }
-  }
-}
-
-static bool skinny_ok(const Args& p, bool conv) {
-  return g_skinny && g_engine == 0 && !conv && p.M <= 2 * kSkRows && p.K % 128 == 0 && p.K <= kSkMaxK &&
-         !p.rbias && !p.tbl && !p.res && !p.res2 && !p.lnr && !p.lnp && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 &&
-         p.act >= 0 && p.act <= 2 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
-         reinterpret_cast<uintptr_t>(p.A) % 16 == 0 && reinterpret_cast<uintptr_t>(p.W) % 16 == 0;
-}
-
-static int run_skinny(const Args& p, hipStream_t s) {
-  const int smem = (kSkRows + kSkCols) * p.K * 2 + 1024;     // + the DMA's tail slack (< 64 chunks)
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_gemm_skinny), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (kSkRows + kSkCols) * kSkMaxK * 2 + 1024);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_gemm_skinny, dim3((p.N + kSkCols - 1) / kSkCols, (p.M + kSkRows - 1) / kSkRows), dim3(256), smem,
-                     s, p);
-  return check_launch("gemm (skinny)");
 }
 
 static const char* plan8_name(const Plan8& pl, bool conv, bool relu) {
@@ -2519,7 +2141,6 @@ extern "C" int i2pc_gemm_ws(const i2pc_gemm_desc* d, void* workspace, size_t wor
   if (rc != I2PC_OK) return rc;
   hipStream_t s = as_stream(stream);
   const bool conv = d->conv != 0, relu = d->conv_relu_in != 0;
-  if (gemm::skinny_ok(p, conv)) return gemm::run_skinny(p, s);
   const gemm::Plan pl = gemm::plan_for(p, conv, relu);
   const gemm::SplitPlan sp = gemm::split_for(p, pl);
   if (sp.splits > 1 && workspace && (int64_t)workspace_bytes >= sp.bytes) {
@@ -2537,7 +2158,6 @@ extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) { return i2pc_ge
 extern "C" size_t i2pc_gemm_workspace_bytes(const i2pc_gemm_desc* d) {
   gemm::Args p;
   if (make_args(d, p) != I2PC_OK) return 0;
-  if (gemm::skinny_ok(p, d->conv != 0)) return 0;
   const gemm::SplitPlan sp = gemm::split_for(p, gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0));
   return sp.splits > 1 ? (size_t)sp.bytes : 0;
 }
@@ -2588,7 +2208,6 @@ extern "C" const char* i2pc_gemm_fp8_kernel_name(const i2pc_gemm_fp8_desc* d8) {
 extern "C" const char* i2pc_gemm_kernel_name(const i2pc_gemm_desc* d) {
   gemm::Args p;
   if (make_args(d, p) != I2PC_OK) return "invalid";
-  if (gemm::skinny_ok(p, d->conv != 0)) return "k_gemm_skinny";
   const gemm::Plan pl = gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0);
   return gemm::plan_name(pl, d->conv != 0, d->conv_relu_in != 0, gemm::split_for(p, pl));
 }
@@ -2603,9 +2222,8 @@ extern "C" int i2pc_gemm_set_engine(int mode) {
 }
 
 // per-host-thread tuning knobs (i2pc_set_tuning; thread_local above): gemm_tail, gemm_bn128,
-// gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_tail160, gemm_stagger, gemm_skinny
+// gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_tail160, gemm_stagger
 bool i2pc_gemm_tune(const char* name, int value) {
-  if (std::strcmp(name, "gemm_skinny") == 0) { i2pc::gemm::g_skinny = value; return true; }
   if (std::strcmp(name, "gemm_tail") == 0) { i2pc::gemm::g_tail = value; return true; }
   if (std::strcmp(name, "gemm_bn128") == 0) { i2pc::gemm::g_bn128 = value; return true; }
   if (std::strcmp(name, "gemm_splitk") == 0) { i2pc::gemm::g_splitk = value; return true; }

@@ -313,13 +313,28 @@ __global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, i
 // DIAGNOSTIC (r05 root-cause of the r04 nondeterminism): the r04 grid-stride form, knob "ln_apply_gs".
 __global__ __launch_bounds__(256) void k_ln_apply_gs(const uint4* __restrict__ x, int64_t ldx8, const float2* __restrict__ rs,
                                                      const float4* __restrict__ gamma, const float4* __restrict__ beta,
-                                                     int rows, int d8, uint4* __restrict__ y, int64_t ldy8) {
+                                                     int rows, int d8, uint4* __restrict__ y, int64_t ldy8, int mode) {
+  // mode 1: as r04; 2: agent-scope acquire fence first; 3: x and rs read by agent-scope relaxed atomic loads
+  if (mode == 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int64_t n = (int64_t)rows * d8;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int r = (int)(i / d8);
     const int c = (int)(i - (int64_t)r * d8);
-    const uint4 v = x[r * ldx8 + c];
-    const float2 s = rs[r];
+    uint4 v;
+    float2 s;
+    if (mode == 3) {
+      const uint32_t* xp = reinterpret_cast<const uint32_t*>(x + r * ldx8 + c);
+      v.x = __hip_atomic_load(xp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v.y = __hip_atomic_load(xp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v.z = __hip_atomic_load(xp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v.w = __hip_atomic_load(xp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float* sp = reinterpret_cast<const float*>(rs + r);
+      s.x = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s.y = __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      v = x[r * ldx8 + c];
+      s = rs[r];
+    }
     const float4 g0 = gamma[2 * c], g1 = gamma[2 * c + 1], b0 = beta[2 * c], b1 = beta[2 * c + 1];
     const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
     const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -380,7 +395,7 @@ extern "C" int i2pc_ln_apply(const void* x, int64_t ldx, const float* rows_stats
     hipLaunchKernelGGL(k_ln_apply_gs, dim3(grid_for((int64_t)rows * d8)), dim3(256), 0, as_stream(stream),
                        static_cast<const uint4*>(x), ldx / 8, reinterpret_cast<const float2*>(rows_stats),
                        reinterpret_cast<const float4*>(gamma), reinterpret_cast<const float4*>(beta), rows, d8,
-                       static_cast<uint4*>(y), ldy / 8);
+                       static_cast<uint4*>(y), ldy / 8, g_ln_apply_gs);
     return check_launch("ln_apply");
   }
   for (int r0 = 0; r0 < rows; r0 += 65535) {   // (grid y <= 65535 rows per launch)

@@ -36,8 +36,9 @@ def _host(points, colors):
         colors = colors.detach().cpu().numpy()
     pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
     cols = None
-    if colors is not None and len(colors) == len(pts) and len(colors) > 0:
-        c = np.asarray(colors)
+    # batched [B, N, 3] buffers flatten to the points' row-major order before the count check
+    c = None if colors is None else np.asarray(colors).reshape(-1, 3)
+    if c is not None and len(c) == len(pts) and len(c) > 0:
         if c.dtype != np.uint8:
             c = np.clip(c, 0, 255).astype(np.uint8)      # integers 0..255 in the reference (app.py:239-244)
         cols = np.ascontiguousarray(c).reshape(-1, 3)

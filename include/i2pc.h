@@ -397,10 +397,6 @@ int i2pc_gemm_set_engine(int mode);
  *   "gemm_stagger" 1 = in the 8-wave GEMM kernels waves 4-7 issue the next K-stage's loads half-way
  *                 through each K-step (their SIMD partners' MFMAs cover the issue), 0 = every wave at
  *                 the top of the step
- *   "gemm_skinny" 1 = calls of at most 64 rows (the DPT readout's CLS half: M = batch) on a skinny
- *                 kernel (A rows in LDS, 16 output columns per workgroup, K split over 16 lanes;
- *                 plain / bias / GELU / ReLU epilogues, K % 128 == 0, K <= 1024), automatic engine
- *                 mode only; 0 = the tile kernel (default: measured faster, r04)
  *   "unp_rows"    1 = the row-sweep unprojection kernel
  *   "unp_nt"      1 = non-temporal point stores
  *   "unp_rpt"     point rows per thread of the row-sweep kernel, 1..8

@@ -104,7 +104,7 @@ def test_tuning_knob_names():
         pytest.skip("libi2pc.so not built")
     from image_to_pointcloud_amd import ops
     defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "gemm_split_tile": 0, "gemm_tile192": 1, "gemm_lnp_p": 0, "gemm_tail160": 1,
-                "gemm_stagger": 1, "gemm_skinny": 0,
+                "gemm_stagger": 1,
                 "unp_rows": 1, "unp_nt": 1, "unp_rpt": 8, "sel_windows": 1, "sel_parts": 0, "sel_rows": 16,
                 "sel_lband": -1, "sel_scratch": 0, "attn_lazy": 1, "attn_scalar": 1, "ln_f2": 1}
     assert set(defaults) == set(ops.TUNING_KNOBS)

@@ -72,7 +72,7 @@ def test_linear_plain_engines_bitexact(M, N, K, act):
     try:
         ops.set_gemm_engine(2)
         lab = ops.gemm_kernel_label(_desc_of(ops, x, w, b, out))
-        assert "k_gemm_p" in lab or "k_gemm_q" in lab, "persistent engine not selected"
+        assert "k_gemm_p" in lab, "persistent engine not selected"
         ops.set_gemm_engine(4)
         lab = ops.gemm_kernel_label(_desc_of(ops, x, w, b, out))
         assert ("k_gemm_8p" in lab) == (K >= 128 and N % 256 == 0), lab
@@ -339,57 +339,3 @@ def test_stagger_bitexact(M, N, K, act, res):
     finally:
         ops.set_tuning("gemm_stagger", 1)
     assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("M,N,K,act,f32", [(32, 1024, 1024, None, False), (64, 384, 384, "gelu", False),
-                                           (5, 256, 128, "relu", True), (40, 768, 1024, None, True)])
-def test_skinny_matches_tile_kernel_and_torch(M, N, K, act, f32):
-    """Calls of at most 64 rows (the DPT readout's CLS half) on k_gemm_skinny (knob gemm_skinny 1; off
-    by default, measured slower in r04): against the tile kernel (another summation order) and torch
-    fp32, and run to run identical."""
-    ops = _ops()
-    dev = torch.device("cuda")
-    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
-    x = _bf(torch.randn(M, K, generator=g)).to(dev)
-    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
-    b = torch.randn(N, generator=g).to(dev)
-    out = torch.empty(M, N, dtype=torch.float32 if f32 else torch.bfloat16, device=dev)
-    d = _desc_of(ops, x, w, b, out)
-    d.c_f32 = 1 if f32 else 0
-    assert ops.gemm_kernel_label(d).startswith("k_gemm<")          # off by default (measured slower)
-    try:
-        ops.set_tuning("gemm_skinny", 1)
-        assert ops.gemm_kernel_label(d) == "k_gemm_skinny"
-        got = ops.linear(x, w, bias=b, act=act, out=out).clone()
-        again = ops.linear(x, w, bias=b, act=act, out=out).clone()
-    finally:
-        ops.set_tuning("gemm_skinny", 0)
-    tile = ops.linear(x, w, bias=b, act=act, out=out).clone()
-    y = x.float() @ w.float().T + b
-    y = F.gelu(y) if act == "gelu" else F.relu(y) if act == "relu" else y
-    assert torch.equal(got, again)
-    assert _fro(got, tile) <= 2e-3, _fro(got, tile)
-    assert _fro(got, y) <= (1e-5 if f32 else 8e-3), _fro(got, y)
-
-
-def test_skinny_cls_readout_row_map():
-    """The readout's CLS rows through a_map (row r = token 0 of image r, rows T apart), as dpt.py
-    calls it: the same values as the gathered rows through the tile kernel."""
-    ops = _ops()
-    dev = torch.device("cuda")
-    B, T, D = 12, 577, 1024
-    g = torch.Generator(device="cpu").manual_seed(5)
-    hs = _bf(torch.randn(B * T, D, generator=g)).to(dev)
-    w = _bf(torch.randn(D, D, generator=g) / math.sqrt(D)).to(dev)
-    b = torch.randn(D, generator=g).to(dev)
-    try:
-        ops.set_tuning("gemm_skinny", 1)
-        got = ops.linear(hs, w, bias=b, rows=B, a_map=(1, T, 0)).clone()
-    finally:
-        ops.set_tuning("gemm_skinny", 0)
-    cls = hs.view(B, T, D)[:, 0].contiguous()
-    ref = ops.linear(cls, w, bias=b).clone()
-    assert got.shape == ref.shape and got.dtype == ref.dtype
-    assert _fro(got, ref) <= 2e-3, _fro(got, ref)
-    y = cls.float() @ w.float().T + b
-    assert _fro(got, y) <= 8e-3

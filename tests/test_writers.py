@@ -91,3 +91,20 @@ def test_save_point_cloud_dropin(tmp_path, monkeypatch, pipeline_case):
         writers.save_point_cloud(pts, cols, "obj", "job")
     with pytest.raises(ValueError):
         writers.write_las(str(tmp_path / "e.las"), np.zeros((0, 3), np.float32), None)
+
+
+def test_ply_batched_buffers_keep_colours(tmp_path):
+    """Batched [B, N, 3] point and colour buffers (the pipeline's layout) write one cloud of B * N
+    coloured points in image-major order: the colours are flattened before the count check."""
+    from image_to_pointcloud_amd import writers
+    rng = np.random.Generator(np.random.PCG64(5))
+    xyz = rng.normal(size=(3, 7, 3)).astype(np.float32)
+    rgb = rng.integers(0, 256, (3, 7, 3), dtype=np.uint8)
+    path = str(tmp_path / "b.ply")
+    writers.write_ply(path, xyz, rgb)
+    data = open(path, "rb").read()
+    head = data[: data.index(b"end_header\n") + len(b"end_header\n")]
+    assert b"element vertex 21" in head and b"property uchar red" in head
+    rec = np.frombuffer(data[len(head):], dtype=np.dtype([("xyz", "<f8", 3), ("rgb", "u1", 3)]))
+    assert np.array_equal(rec["xyz"], xyz.reshape(-1, 3).astype(np.float64))
+    assert np.array_equal(rec["rgb"], rgb.reshape(-1, 3))

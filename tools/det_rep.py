@@ -4,10 +4,13 @@ runs except the final compare) and count how many runs differ from their first.
     python tools/det_rep.py N R GRAPH [model]
 
 Environment knobs (r05 root-cause of the r04 nondeterminism):
-  DET_GS=1       the r04 grid-stride i2pc_ln_apply (tuning knob "ln_apply_gs")
+  DET_GS=k       the r04 grid-stride i2pc_ln_apply (tuning knob "ln_apply_gs" = k: 1 as r04, 2 with an
+                 agent-scope acquire fence first, 3 with its loads as agent-scope relaxed atomics)
   DET_PROBE=1    wrap ops.ln_apply: copy its inputs (x, row stats) right before and its output right
                  after each call (stream-ordered copies), and report per call whether the inputs, the
                  output at the call, and the hidden state at the end of the forward match run 1
+  DET_PROBE=2    as 1, and each ln_apply runs twice on the same inputs (first into a scratch buffer);
+                 reports per call whether the two outputs of the same run differ
   DET_SYNC=1     with DET_PROBE, a host synchronise right after each ln_apply"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -20,9 +23,10 @@ def worker(rank, q, model, reps, graph):
     from image_to_pointcloud_amd.pipeline import PointCloudPipeline
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    if os.environ.get("DET_GS") == "1":
-        _lib.call("i2pc_set_tuning", b"ln_apply_gs", 1)
-    probe = os.environ.get("DET_PROBE") == "1"
+    if os.environ.get("DET_GS"):
+        _lib.call("i2pc_set_tuning", b"ln_apply_gs", int(os.environ["DET_GS"]))
+    probe = os.environ.get("DET_PROBE") in ("1", "2")
+    twice = os.environ.get("DET_PROBE") == "2"
     sync = os.environ.get("DET_SYNC") == "1"
     rec = []
     if probe:
@@ -30,10 +34,11 @@ def worker(rank, q, model, reps, graph):
 
         def wrapped(x, rs, g, b, out=None):
             xin, rsin = x.clone(), rs.clone()
+            first = orig(x, rs, g, b, out=torch.empty_like(out)) if twice else None
             o = orig(x, rs, g, b, out=out)
             if sync:
                 torch.cuda.synchronize()
-            rec.append((xin, rsin, o.clone()))
+            rec.append((xin, rsin, o.clone(), first))
             return o
         ops.ln_apply = wrapped
     B, S = 2, 256
@@ -66,6 +71,9 @@ def worker(rank, q, model, reps, graph):
         # the output at the call against the hidden state at the end of the same forward
         late = [sum(0 if torch.equal(recs[j][k][2], hss[j][k]) else 1 for j in range(1, reps)) for k in range(n)]
         msg += f"; probe: x differ {bx}, rs differ {br}, out-at-call differ {bo}, out-at-call != final hs {late}"
+        if twice:
+            tw = [sum(0 if torch.equal(recs[j][k][2], recs[j][k][3]) else 1 for j in range(reps)) for k in range(n)]
+            msg += f"; same-run double call differs {tw}"
     q.put((rank, msg))
 
 
