@@ -55,6 +55,7 @@ _SIGNATURES = {
     "i2pc_sor_workspace_bytes": (c_size_t, [c_int64]),
     "i2pc_sor": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "i2pc_clock_probe": (c_int, [c_int, c_int, c_void_p, c_void_p]),
 }
 
 _lib = None
@@ -95,8 +96,13 @@ def register(name: str, restype, argtypes) -> None:
 
 
 def call(name: str, *args) -> int:
+    """Call an entry point whose signature is registered (without argtypes, ctypes would pass a
+    device pointer as a 32-bit int: a truncated address and a memory fault on the GPU)."""
     lib = load()
-    rc = getattr(lib, name)(*args)
+    fn = getattr(lib, name)
+    if fn.argtypes is None:
+        raise I2PCError(f"{name}: no ctypes signature registered (_lib.register)")
+    rc = fn(*args)
     if isinstance(rc, int) and rc != 0:
         msg = lib.i2pc_last_error().decode(errors="replace")
         raise I2PCError(f"{name} failed ({rc}): {msg}")

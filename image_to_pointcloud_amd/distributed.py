@@ -297,7 +297,7 @@ class RcclComm:
 
     def __init__(self, group=None, nranks=None, rank=None, unique_id: bytes = None):
         import ctypes
-        from . import _lib
+        from . import _lib, geometry  # noqa: F401  (geometry registers the i2pc_comm_* signatures)
         lib = _lib.load()
         self._lib = lib
         if nranks is None:
@@ -321,7 +321,7 @@ class RcclComm:
     @staticmethod
     def unique_id() -> bytes:
         import ctypes
-        from . import _lib
+        from . import _lib, geometry  # noqa: F401
         buf = ctypes.create_string_buffer(128)
         _lib.call("i2pc_comm_unique_id", buf, 128)
         return buf.raw
