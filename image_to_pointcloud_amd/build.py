@@ -36,6 +36,7 @@ SOURCES = [
     "fp8.hip",
     "bit.hip",
     "probe.hip",
+    "model.cpp",
     "comm.cpp",
     "writers.cpp",
 ]

@@ -14,6 +14,7 @@
 //                               S accumulators, converted to bf16 in place)
 // so the online-softmax max/sum are lane-local plus one cross-half exchange.
 #include "common.h"
+#include "mx.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -245,12 +246,18 @@ __device__ __forceinline__ v4s tr_read(const uint8_t* p) {
 // MFMAs (MI355X_MICROARCH.md, filler prices) -- and the row max across the two lane halves by
 // v_permlane32_swap instead of ds_bpermute; the same operations, so bit-identical
 
-template <int OCC, bool SC = false>
+// F8OUT: the output is written as the MX fp8 operand of the next GEMM (C5's attention-out) instead of
+// bf16: e4m3 bytes out8[row][NH * 64] and one E8M0 scale byte per 32 d, out8s[row * lds8 + 2 h + dt],
+// quantised from the bf16-rounded values exactly as i2pc_quant_fp8 quantises the bf16 output (so the
+// bytes are those of attention -> quant_fp8, with no bf16 round trip through HBM).
+template <int OCC, bool SC = false, bool F8OUT = false>
 __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restrict__ qkv, int B, int T, int NH,
-                                                           float scale_log2, bf16_t* __restrict__ out, int lazy) {
+                                                           float scale_log2, bf16_t* __restrict__ out, int lazy,
+                                                           uint8_t* __restrict__ out8 = nullptr,
+                                                           uint8_t* __restrict__ out8s = nullptr, int lds8 = 0) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * kTileBytes];
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: LDS-DMA addresses in SGPRs
   const int qtiles = (T + kQ - 1) / kQ;
   // XCD-aware order: workgroups b and b + 8 share an XCD, so give each XCD a contiguous range
   // of (image, head, q-tile) indices (bijective for any count): the q-tiles of one head then
@@ -277,17 +284,33 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qg + qc * ld + 16 * s + 8 * hh);
 
-  // K and V glds: 8 wave-instructions per tile each (8 keys x 128 B), 2 + 2 per wave
+  // K and V by LDS-DMA: 8 wave-instructions per tile each (8 keys x 128 B), 2 + 2 per wave.
+  // Buffer descriptors over this (image, head)'s key rows: a lane's byte offset inside a tile is
+  // fixed (row * ld + swizzled chunk), the tile adds a uniform kt * 64 rows, and keys past T read as
+  // zero by the range check (the last tile masks them to -inf; zero V rows meet p = 0), so the
+  // 64-bit clamped address arithmetic of every tile is gone.  (Bit-identical: the clamped rows were
+  // copies of key T - 1 that met the same mask.)
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  const uint32_t span = (uint32_t)(((int64_t)(T - 1) * ld + 64) * 2);   // bytes through key T - 1's 64 d
+  const __amdgpu_buffer_rsrc_t k_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Kg), 0, span, 0x00020000);
+  const __amdgpu_buffer_rsrc_t v_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Vg), 0, span, 0x00020000);
+  const uint32_t tile_bytes = (uint32_t)(kKV * ld * 2);
+  uint32_t koff[2], voff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wid * 2 + j) * 8 + (lane >> 3);
+    const int pchunk = lane & 7;
+    koff[j] = (uint32_t)((row * ld + (pchunk ^ (row & 7)) * 8) * 2);
+    voff[j] = (uint32_t)((row * ld + (pchunk ^ v_swz(row)) * 8) * 2);
+  }
   auto stage = [&](int buf, int kt) {
     uint8_t* sK = smem + buf * 2 * kTileBytes;
     uint8_t* sV = sK + kTileBytes;
+    const uint32_t t0 = (uint32_t)kt * tile_bytes;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int row = (wid * 2 + j) * 8 + (lane >> 3);
-      const int pchunk = lane & 7;
-      const int key = min(kt * kKV + row, T - 1);
-      glds16(Kg + key * ld + (pchunk ^ (row & 7)) * 8, sK + (wid * 2 + j) * 8 * 128);
-      glds16(Vg + key * ld + (pchunk ^ v_swz(row)) * 8, sV + (wid * 2 + j) * 8 * 128);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(k_rs, (lds_ptr_t)(sK + (wid * 2 + j) * 8 * 128), 16, koff[j] + t0, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(v_rs, (lds_ptr_t)(sV + (wid * 2 + j) * 8 * 128), 16, voff[j] + t0, 0, 0, 0);
     }
   };
 
@@ -412,7 +435,42 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   const float inv = 1.0f / l_tot;
-  if (q < T) {
+  if constexpr (F8OUT) {
+    // lane (lq, hh) holds d = 32 dt + 8 g + 4 hh + e of its query; the 32-d block dt is split over
+    // the lane pair (lq, lq + 32), which trade amax and bytes by v_permlane32_swap (both lanes of a
+    // pair share q, so both take this branch or neither)
+    if (q < T) {
+      const int64_t row = (int64_t)b * T + q;
+      uint32_t sbytes = 0;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        float v[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t w0 = pack_bf16(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+          const uint32_t w1 = pack_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+          v[4 * g + 0] = __uint_as_float(w0 << 16); v[4 * g + 1] = __uint_as_float(w0 & 0xffff0000u);
+          v[4 * g + 2] = __uint_as_float(w1 << 16); v[4 * g + 3] = __uint_as_float(w1 & 0xffff0000u);
+        }
+        float am = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) am = fmaxf(am, fabsf(v[e]));
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(am), __float_as_uint(am), false, false);
+        am = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        const int ex = mx::mx_exponent(am);
+        const float mul = mx::exp2i(-ex);
+        uint32_t d[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) d[g] = mx::pack_e4m3(v[4 * g] * mul, v[4 * g + 1] * mul, v[4 * g + 2] * mul, v[4 * g + 3] * mul);
+        // hh = 0 ends with bytes 0-15 of the block, hh = 1 with bytes 16-31
+        const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+        *reinterpret_cast<uint4*>(out8 + row * (int64_t)D + h * 64 + 32 * dt + 16 * hh) = make_uint4(s0[0], s0[1], s1[0], s1[1]);
+        sbytes |= (uint32_t)(ex + 127) << (8 * dt);
+      }
+      if (hh == 0) *reinterpret_cast<uint16_t*>(out8s + row * (int64_t)lds8 + 2 * h) = (uint16_t)sbytes;
+    }
+  } else if (q < T) {
     bf16_t* orow = out + ((int64_t)b * T + q) * D + h * 64;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
@@ -440,6 +498,23 @@ bool i2pc_attention_tune(const char* name, int value) {
   if (std::strcmp(name, "attn_lazy") == 0) { g_lazy = value; return true; }
   if (std::strcmp(name, "attn_scalar") == 0) { g_scalar = value; return true; }
   return false;
+}
+
+extern "C" int i2pc_attention_fp8(const void* qkv, int batch, int tokens, int heads, float scale, void* out,
+                                  int64_t ldo, void* out_scale, int64_t ldo_scale, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(qkv && out && out_scale, "NULL pointer");
+  I2PC_REQUIRE(batch > 0 && tokens > 0 && heads > 0, "attention_fp8: empty shape");
+  I2PC_REQUIRE(ldo == (int64_t)heads * 64, "attention_fp8: the fp8 rows are dense (ldo = heads * 64)");
+  I2PC_REQUIRE(ldo_scale * 128 >= (int64_t)heads * 64 && (reinterpret_cast<uintptr_t>(out) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(out_scale) % 4) == 0,
+               "attention_fp8: scale rows of ldo_scale dwords cover heads * 2 blocks; 16-B aligned data");
+  const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL((attn::k_attention_tr<3, true, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, nullptr, g_lazy,
+                     static_cast<uint8_t*>(out), static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
+  return check_launch("attention_fp8");
 }
 
 extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scale, void* out, void* stream) {

@@ -368,10 +368,11 @@ class DPTHybridModel(DPTDepthModel):
             else:
                 ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["lnb"])
                 qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
-            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
-            if f8("o"):
-                ops.linear_fp8(ops.quant_fp8(att, out=buf["att8"]), L["w_o"], bias=L["b_o"], res=x, out=x)
+            if f8("o"):       # the attention epilogue writes attention-out's fp8 operand directly
+                att8 = ops.attention(qkv, B, T, s.heads, scale, out=buf["att8"])
+                ops.linear_fp8(att8, L["w_o"], bias=L["b_o"], res=x, out=x)
             else:
+                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
                 ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
             if f8("fc1"):       # FC1's epilogue writes FC2's operand format
                 ln = ops.layernorm_fp8(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])

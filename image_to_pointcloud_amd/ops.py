@@ -57,6 +57,8 @@ _lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_vo
                                                ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_attention", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_float, c_void_p, c_void_p])
+_lib.register("i2pc_attention_fp8", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                                   c_void_p, c_int64, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_upsample2x", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, c_void_p, c_void_p, c_void_p])
 _lib.register("i2pc_resize_bilinear", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -440,12 +442,23 @@ def layernorm(x, gamma, beta, eps, out=None, mean_out=None):
 
 
 def attention(qkv, batch, tokens, heads, scale, out=None):
+    """Fused self-attention (i2pc_attention).  out: bf16 [batch*tokens, heads*64], or an Fp8 of that
+    shape: the MX fp8 operand of the next GEMM written by the kernel's epilogue (i2pc_attention_fp8;
+    the same bytes as quant_fp8 of the bf16 output)."""
     torch = _torch()
     _check(qkv, torch.bfloat16, "qkv")
     D = heads * 64
     if out is None:
         out = torch.empty((batch * tokens, D), dtype=torch.bfloat16, device=qkv.device)
-    with _Timed("k_attention", 4.0 * batch * heads * tokens * tokens * 64, 2.0 * 4 * batch * tokens * D):
+    flops = 4.0 * batch * heads * tokens * tokens * 64
+    if isinstance(out, Fp8):
+        if tuple(out.data.shape) != (batch * tokens, D):
+            raise ValueError(f"attention fp8 out {tuple(out.data.shape)} != {(batch * tokens, D)}")
+        with _Timed("k_attention", flops, 2.0 * 3 * batch * tokens * D + (1.0 + 1.0 / 32) * batch * tokens * D):
+            _lib.call("i2pc_attention_fp8", _p(qkv), batch, tokens, heads, float(scale), _p(out.data), D,
+                      _p(out.scale), out.scale.shape[-1] // 4, _stream())
+        return out
+    with _Timed("k_attention", flops, 2.0 * 4 * batch * tokens * D):
         _lib.call("i2pc_attention", _p(qkv), batch, tokens, heads, float(scale), _p(out), _stream())
     return out
 

@@ -415,8 +415,8 @@ int i2pc_gemm_set_engine(int mode);
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
  *   "ln_f2"       1 = the register-resident LayerNorm for dim 384 (k_layernorm2)
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _GEMM_SPLIT_TILE / _GEMM_TILE192 /
- * _GEMM_LNP_P / _GEMM_TAIL160 / _GEMM_STAGGER / _GEMM_SKINNY / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY /
- * _ATTN_SCALAR environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 0, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
+ * _GEMM_LNP_P / _GEMM_TAIL160 / _GEMM_STAGGER / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY /
+ * _ATTN_SCALAR environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps
  * the kernels it captured: re-capture after changing a knob.  An unknown name fails with I2PC_EINVAL
  * and an error message listing every knob. */
 int i2pc_set_tuning(const char* name, int value);
@@ -435,6 +435,12 @@ int i2pc_layernorm_stats(const float* x, int64_t ldx, const float* gamma, const 
  * qkv: bf16 [batch*tokens][3*heads*64] (Q | K | V column blocks, the fused QKV GEMM output);
  * out: bf16 [batch*tokens][heads*64]. (DPTSelfAttention, modeling_dpt.py:123-154) */
 int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scale, void* out, void* stream);
+/* i2pc_attention writing the MX fp8 operand of the next GEMM (DPT-Hybrid's attention-out on the fp8
+ * engine) instead of bf16: out e4m3fn [batch*tokens][ldo = heads*64], out_scale E8M0 bytes, row r's
+ * 32-column block j at byte r * ldo_scale * 4 + j (ldo_scale in dwords, >= heads*64/128).  The bytes
+ * equal i2pc_quant_fp8 of i2pc_attention's bf16 output (quantised from the bf16-rounded values). */
+int i2pc_attention_fp8(const void* qkv, int batch, int tokens, int heads, float scale, void* out, int64_t ldo,
+                       void* out_scale, int64_t ldo_scale, void* stream);
 
 /* Bilinear 2x upsample, align_corners = True, NHWC bf16 (nn.functional.interpolate,
  * modeling_dpt.py:504-506, 698), optional + add (bf16, output shape). */
@@ -489,6 +495,29 @@ void i2pc_preprocess_plan_destroy(i2pc_preprocess_plan* plan);
  * (c, py, px) (the im2col of the patch-embedding conv, modeling_dpt.py:60-69,
  * modeling_dinov2.py Dinov2PatchEmbeddings); the pad columns are never written (zero them once). */
 int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* bgr, int batch, int layout, void* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Network executor: the whole depth stage of process_with_depth_anything (backend/app.py:99-122:
+ * BGR->RGB :103, the processor :109, the forward :111-116) for a batch, with no Python.  The model is
+ * a prepared-network file (image_to_pointcloud_amd/model_file.py writes it from a loaded network:
+ * Depth-Anything-V2, the reference's `load_model("depth-anything-v2")`, app.py:78-82) made for one
+ * input size; i2pc_model_create uploads its weights and allocates every buffer once, so
+ * i2pc_depth_forward is launch-only and stream-ordered (graph-capturable).  The depth equals the
+ * Python pipeline's (PointCloudPipeline.infer_depth) bit for bit.
+ * ------------------------------------------------------------------------ */
+typedef struct i2pc_model i2pc_model;
+/* Read a prepared-network file for `batch` images of in_h x in_w (must be the size the file was made
+ * for).  EUNSUPPORTED for a family / configuration the executor does not run. */
+int i2pc_model_create(const char* path, int batch, int in_h, int in_w, i2pc_model** model);
+int i2pc_model_destroy(i2pc_model* model);
+/* The batch, input size and model-resolution depth size (depth_h x depth_w) of a model. */
+int i2pc_model_io(const i2pc_model* model, int* batch, int* in_h, int* in_w, int* depth_h, int* depth_w);
+/* bgr: uint8 [batch][in_h][in_w][3] (cv2 order, app.py:99) on the device -> depth fp32
+ * [batch][depth_h][depth_w] (predicted_depth, app.py:116), on `stream`. */
+int i2pc_depth_forward(i2pc_model* model, const uint8_t* bgr, float* depth, void* stream);
+/* Host-only check of a prepared-network file: its 32 header ints, 16 header floats and tensor
+ * count (model_file.py I_* / F_* slots); no device work. */
+int i2pc_model_file_info(const char* path, int32_t* ints32, float* floats16, int* ntensors);
 
 /* ------------------------------------------------------------------------
  * Artefact writers (save_point_cloud, backend/app.py:310-389) from HOST buffers

@@ -150,6 +150,20 @@ def test_attention(dev, B, T, H):
     _close(got, ref, rel=1.2e-2, mx=3e-2)
 
 
+@pytest.mark.parametrize("B,T,H", [(2, 577, 12), (1, 37, 6), (3, 1, 4), (2, 130, 12)])
+def test_attention_fp8_out_bit_exact(dev, B, T, H):
+    """i2pc_attention_fp8 (DPT-Hybrid's attention-out operand written by the attention epilogue) equals
+    i2pc_quant_fp8 of the bf16 attention output byte for byte: e4m3 data and E8M0 scales."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(T * 3 + H)
+    qkv = _bf(torch.randn(B * T, 3 * H * 64, generator=g) * 1.5).to(dev)
+    ref = ops.quant_fp8(ops.attention(qkv, B, T, H, 0.125))
+    got = ops.attention(qkv, B, T, H, 0.125, out=ops.empty_fp8((B * T, H * 64), dev))
+    torch.cuda.synchronize()
+    assert torch.equal(got.data, ref.data)
+    assert torch.equal(got.scale, ref.scale)
+
+
 @pytest.mark.parametrize("B,T,H,spike", [(2, 577, 16, 0), (2, 577, 16, 1), (1, 1370, 6, 1), (2, 130, 12, 1)])
 def test_attention_lazy_rescale_bit_exact(dev, B, T, H, spike):
     """The lazy softmax rescale (attn_lazy, skip when no row's max rose), the scalar exponent FMAs
