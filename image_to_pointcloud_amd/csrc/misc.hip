@@ -314,15 +314,22 @@ __global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, i
 __global__ __launch_bounds__(256) void k_ln_apply_gs(const uint4* __restrict__ x, int64_t ldx8, const float2* __restrict__ rs,
                                                      const float4* __restrict__ gamma, const float4* __restrict__ beta,
                                                      int rows, int d8, uint4* __restrict__ y, int64_t ldy8, int mode) {
-  // mode 1: as r04; 2: agent-scope acquire fence first; 3: x and rs read by agent-scope relaxed atomic loads
+  // mode 1: as r04; 2: agent-scope acquire fence first; 3: x and rs read by agent-scope relaxed atomic loads;
+  // 4: the vector L1 of the CU invalidated first (buffer_inv sc0); 5: rs read by agent-scope loads only
   if (mode == 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (mode == 4) asm volatile("buffer_inv sc0" ::: "memory");
   const int64_t n = (int64_t)rows * d8;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int r = (int)(i / d8);
     const int c = (int)(i - (int64_t)r * d8);
     uint4 v;
     float2 s;
-    if (mode == 3) {
+    if (mode == 5) {
+      v = x[r * ldx8 + c];
+      const float* sp = reinterpret_cast<const float*>(rs + r);
+      s.x = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s.y = __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (mode == 3) {
       const uint32_t* xp = reinterpret_cast<const uint32_t*>(x + r * ldx8 + c);
       v.x = __hip_atomic_load(xp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       v.y = __hip_atomic_load(xp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -5,7 +5,9 @@ runs except the final compare) and count how many runs differ from their first.
 
 Environment knobs (r05 root-cause of the r04 nondeterminism):
   DET_GS=k       the r04 grid-stride i2pc_ln_apply (tuning knob "ln_apply_gs" = k: 1 as r04, 2 with an
-                 agent-scope acquire fence first, 3 with its loads as agent-scope relaxed atomics)
+                 agent-scope acquire fence first, 3 with its loads as agent-scope relaxed atomics, 4 with
+                 the CU's vector L1 invalidated first (buffer_inv sc0), 5 with only the row statistics
+                 read by agent-scope loads)
   DET_PROBE=1    wrap ops.ln_apply: copy its inputs (x, row stats) right before and its output right
                  after each call (stream-ordered copies), and report per call whether the inputs, the
                  output at the call, and the hidden state at the end of the forward match run 1

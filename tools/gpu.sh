@@ -20,7 +20,7 @@
 #   c4                         tools/c4_panorama.py on one rank: window / levels / smooth / equirect / network stream
 #   clock [tag] [bench args]   effective shader clock per kernel (GRBM_GUI_ACTIVE / 8 / wall) -> profiles/<round>_<tag>_clock.json
 set -o pipefail
-R=${ROUND:-r03}
+R=${ROUND:-r05}
 TASK=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out profiles
