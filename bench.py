@@ -135,26 +135,32 @@ def _kernel_profile(pipe, images, reps=5):
     return per, geo_t, (unp_ms * 1e-3 if unp_ms > 0 else None)
 
 
-def _lib_sha16():
+def kernels_sha16() -> str:
+    """Hash of the device-code sources (csrc/*.hip and the headers they include): what a PMC traffic
+    table depends on.  The host-only C++ (ABI glue, executor, writers) does not change a kernel's bytes."""
+    import glob
     import hashlib
-    from image_to_pointcloud_amd import _lib
-    with open(_lib.load()._name, "rb") as fh:
-        return hashlib.sha256(fh.read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "image_to_pointcloud_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 
 def _pmc_traffic(tag: str):
     """HBM bytes per launch by kernel label from the newest profiles/r*_<tag>_pmc_traffic.json
     (tools/gpu.sh profile: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench,
     gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md) -> (table, source, stale), or
-    ({}, None, None).  stale: the table was collected on another build of libi2pc.so than the
-    one this run loaded (or predates the recorded hash)."""
+    ({}, None, None).  stale: the table was collected on other kernel sources than this run's
+    (kernels_sha16), or predates the recorded hash."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc_traffic.json")))
     if not files:
         return {}, None, None
     with open(files[-1]) as fh:
         d = json.load(fh)
-    return d.get("kernels", {}), os.path.relpath(files[-1], ROOT), d.get("lib_sha16") != _lib_sha16()
+    return d.get("kernels", {}), os.path.relpath(files[-1], ROOT), d.get("kernels_sha16") != kernels_sha16()
 
 
 def _traffic(table, src, *names, calls_per_step=None):

@@ -85,9 +85,31 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    _build_example(force)
     if verbose:
         print(f"built {LIB}")
     return LIB
+
+
+EXAMPLE = os.path.join(ROOT, "examples", "depth_forward")
+
+
+def _build_example(force: bool) -> None:
+    """examples/depth_forward: a plain C caller of the network executor (gcc, HIP's C API, libi2pc.so)."""
+    src = EXAMPLE + ".c"
+    if not os.path.exists(src):
+        return
+    if (not force and os.path.exists(EXAMPLE)
+            and os.path.getmtime(EXAMPLE) >= max(os.path.getmtime(src), os.path.getmtime(LIB))):
+        return
+    rocm = os.path.dirname(os.path.dirname(os.path.realpath(hipcc())))
+    cmd = [shutil.which("gcc") or "gcc", "-std=c99", "-O2", "-Wall", "-D__HIP_PLATFORM_AMD__",
+           "-I", os.path.join(rocm, "include"), "-I", os.path.join(ROOT, "include"), src, "-o", EXAMPLE,
+           "-L", PKG, "-li2pc", "-L", os.path.join(rocm, "lib"), "-lamdhip64",
+           "-Wl,-rpath,$ORIGIN/../image_to_pointcloud_amd", "-Wl,-rpath," + os.path.join(rocm, "lib")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"example build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
 def main(argv=None) -> int:

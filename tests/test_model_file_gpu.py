@@ -69,3 +69,27 @@ def test_native_executor_graph_replay_and_errors(tmp_path):
         want = pipe.infer_depth(new).clone()
         torch.cuda.synchronize()
     assert torch.equal(out, want)
+
+
+def test_plain_c_program_runs_the_depth_stage(tmp_path):
+    """examples/depth_forward.c -- a C program linking libi2pc.so and the HIP runtime, no Python --
+    runs the exported network on raw BGR images and writes the raw depth: bit-identical to the
+    Python pipeline's depth of the same images."""
+    import os
+    import subprocess
+    from image_to_pointcloud_amd.model_file import export_depth_anything
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "examples", "depth_forward")
+    assert os.path.exists(exe), "examples/depth_forward not built (python -m image_to_pointcloud_amd.build)"
+    B, H, W = 2, 256, 320
+    pipe = PointCloudPipeline(B, H, W, spec=_spec("small"), density="medium", device=torch.device("cuda"), seed=0)
+    imgs = _imgs(B, H, W, 21)
+    want = pipe.infer_depth(imgs).cpu().numpy()
+    net = export_depth_anything(pipe.model, str(tmp_path / "s.i2pcnet"), H, W)
+    src, dst = tmp_path / "images.u8", tmp_path / "depth.f32"
+    imgs.cpu().numpy().tofile(src)
+    r = subprocess.run([exe, net, str(B), str(H), str(W), str(src), str(dst)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.fromfile(dst, dtype=np.float32).reshape(want.shape)
+    assert got.tobytes() == want.tobytes()

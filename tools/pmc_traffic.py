@@ -9,7 +9,6 @@ Labels follow bench.py's `kernels` keys (ops.gemm_kernel_label / kernel names).
 """
 import csv
 import glob
-import hashlib
 import json
 import os
 import re
@@ -51,11 +50,10 @@ def main(d, out, steps=2):
                   "hbm_bytes_per_launch": round((2 * fetch + write) * 1024),
                   # every dispatch of the label in one step (e.g. a GEMM call's main + tail launch)
                   "hbm_bytes_per_step": round((2 * sum(cs["FETCH_SIZE"]) + sum(cs["WRITE_SIZE"])) * 1024 / steps)}
-    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "image_to_pointcloud_amd",
-                       "libi2pc.so")
-    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib) else None
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernels_sha16
     with open(out, "w") as fh:
-        json.dump({"lib_sha16": sha,      # bench.py flags the table stale when its libi2pc.so differs
+        json.dump({"kernels_sha16": kernels_sha16(),   # bench.py flags the table stale when the kernels differ
                    "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace), "
                              "eager bench steps; hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024; "
                              "hbm_bytes_per_launch averages the label's dispatches, hbm_bytes_per_step sums "
