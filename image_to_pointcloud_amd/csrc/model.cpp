@@ -271,7 +271,8 @@ static int forward_da(i2pc_model* m, const uint8_t* bgr, float* depth, bool plan
   TRY(gemm(m, conv_desc(*hidden, W("H.w1"), Wf("H.b1"), I[I_H1P], 3, 1, 1, false, 0, nullptr, nullptr, m->head_t), plan,
            s));
   if (!plan)
-    TRY(i2pc_head_upconv(m->head_t.p, B, m->head_t.h, m->head_t.w, m->head_t.c, gh * I[I_PATCH], gw * I[I_PATCH],
+    TRY(i2pc_head_upconv(m->head_t.p, B, m->head_t.h, m->head_t.w, m->head_t.c, (I[I_FUSION] / 2 + 31) / 32 * 32,
+                         gh * I[I_PATCH], gw * I[I_PATCH],
                          W("H.w2"), Wf("H.b2"), Wf("H.w3"), m->floats[F_B_H3], depth, s));
   return I2PC_OK;
 }

@@ -407,7 +407,7 @@ class DepthAnythingModel:
         t = ops.conv2d(hidden, self.w_h1, bias=self.b_h1)
         H, W = gh * s.patch, gw * s.patch
         if dpt.FUSED_HEAD and s.head_hidden == 32:
-            return ops.head_upconv(t, H, W, self.w_h2, self.b_h2, self.w_h3, self.b_h3)
+            return ops.head_upconv(t, H, W, self.w_h2, self.b_h2, self.w_h3, self.b_h3, cin=_pad_to(s.fusion // 2, 32))
         u = ops.resize_bilinear(t, H, W, align_corners=True)
         t2 = ops.conv2d(u, self.w_h2, bias=self.b_h2, act="relu")
         return ops.head_out(t2, self.w_h3, self.b_h3)

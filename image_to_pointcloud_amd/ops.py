@@ -70,7 +70,7 @@ _lib.register("i2pc_f32_to_bf16", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_
 _lib.register("i2pc_head_out", ctypes.c_int, [c_void_p, c_int64, ctypes.c_int, c_void_p, ctypes.c_float,
                                               c_void_p, c_void_p])
 _lib.register("i2pc_head_upconv", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                                  ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                                   ctypes.c_float, c_void_p, c_void_p])
 
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2}
@@ -499,20 +499,22 @@ def f32_to_bf16(x, out=None):
     return out
 
 
-def head_upconv(x, out_h, out_w, w2, b2, w4, b4: float, out=None):
+def head_upconv(x, out_h, out_w, w2, b2, w4, b4: float, out=None, cin=None):
     """Fused head tail: align_corners resize to (out_h, out_w) -> 3x3 conv (C -> 32) + bias + ReLU
     -> 1x1 conv (32 -> 1) + bias + ReLU, without materialising the resized map.
-    x: bf16 NHWC [B, h, w, C] (C % 64 == 0); w2: bf16 [32, 9*C]; b2, w4: fp32 [32]."""
+    x: bf16 NHWC [B, h, w, C] (C % 8 == 0); w2: bf16 [32, 9*C]; b2, w4: fp32 [32]; cin: the
+    channels used (default C, a multiple of 32; the rest are the zero padding of a narrower head)."""
     torch = _torch()
     _check(x, torch.bfloat16, "x")
     B, h, w, C = x.shape
+    cin = C if cin is None else int(cin)
     if tuple(w2.shape) != (32, 9 * C) or w2.dtype != torch.bfloat16:
         raise ValueError(f"head_upconv: w2 must be bf16 [32, {9 * C}], got {tuple(w2.shape)} {w2.dtype}")
     if out is None:
         out = torch.empty((B, out_h, out_w), dtype=torch.float32, device=x.device)
-    flops = 2.0 * B * out_h * out_w * 32 * (9 * C + 1)
-    with _Timed("k_head_upconv", flops, 2.0 * B * h * w * C + 4.0 * B * out_h * out_w):
-        _lib.call("i2pc_head_upconv", _p(x), B, h, w, C, out_h, out_w, _p(w2.contiguous()), _p(b2), _p(w4),
+    flops = 2.0 * B * out_h * out_w * 32 * (9 * cin + 1)
+    with _Timed("k_head_upconv", flops, 2.0 * B * h * w * cin + 4.0 * B * out_h * out_w):
+        _lib.call("i2pc_head_upconv", _p(x), B, h, w, C, cin, out_h, out_w, _p(w2.contiguous()), _p(b2), _p(w4),
                   float(b4), _p(out), _stream())
     return out
 

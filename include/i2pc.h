@@ -468,11 +468,13 @@ int i2pc_head_out(const void* x, int64_t pixels, int c, const float* w, float bi
 /* Fused head tail (DPTDepthEstimationHead head[1..5], modeling_dpt.py:679-716, and the
  * Depth-Anything head after conv1): depth[b][y][x] = relu(b4 + sum_co w4[co] *
  * bf16(relu(b2[co] + conv3x3(resize_ac(x), w2)[co]))) where resize_ac is the bilinear
- * align_corners=True resize of x (bf16 NHWC [batch, h, w, c], c % 64 == 0) to
- * (out_h, out_w); w2: bf16 [32][9*c] packed (ky, kx, ci); b2, w4: fp32 [32]; depth fp32
- * [batch, out_h, out_w].  Replaces i2pc_resize_bilinear + a 3x3 conv + i2pc_head_out
- * without materialising the resized map. */
-int i2pc_head_upconv(const void* x, int batch, int h, int w, int c, int out_h, int out_w, const void* w2,
+ * align_corners=True resize of x (bf16 NHWC [batch, h, w, c], pitch c % 8 == 0, of which the
+ * first cin channels are used, cin % 32 == 0: Depth-Anything-V2-Small pads its 32 head
+ * channels to 64) to (out_h, out_w); w2: bf16 [32][9*c] packed (ky, kx, ci); b2, w4: fp32
+ * [32]; depth fp32 [batch, out_h, out_w].  Replaces i2pc_resize_bilinear + a 3x3 conv +
+ * i2pc_head_out without materialising the resized map.  The resize must not shrink by more
+ * than a tile's LDS source window holds (the heads enlarge: 2x for DPT, 1.75x for DA). */
+int i2pc_head_upconv(const void* x, int batch, int h, int w, int c, int cin, int out_h, int out_w, const void* w2,
                      const float* b2, const float* w4, float b4, float* depth, void* stream);
 
 /* Area-averaging downscale, cv2.resize(image, (out_w, out_h), interpolation=INTER_AREA)

@@ -216,7 +216,8 @@ def test_head_out(dev):
 
 
 @pytest.mark.parametrize("B,h,w,C,H,W", [(2, 24, 24, 128, 48, 48), (1, 37, 37, 64, 518, 518),
-                                         (2, 19, 23, 128, 38, 46), (1, 1, 1, 64, 7, 9)])
+                                         (2, 19, 23, 128, 38, 46), (1, 1, 1, 64, 7, 9), (1, 96, 150, 32, 192, 300),
+                                         (1, 40, 37, 96, 70, 65), (2, 64, 64, 128, 64, 64)])
 def test_head_upconv_matches_unfused_and_torch(dev, B, h, w, C, H, W):
     """Fused resize -> 3x3 conv + ReLU -> 1x1 conv + ReLU against (1) the unfused kernels
     (same bf16 rounding points; only the fp32 summation order differs) and (2) torch fp32."""
@@ -238,3 +239,28 @@ def test_head_upconv_matches_unfused_and_torch(dev, B, h, w, C, H, W):
     c = F.relu(F.conv2d(xr, w2.float().to(dev), b2, padding=1))
     ref = F.relu((c * w4.view(1, 32, 1, 1)).sum(1) + b4)
     _close(got, ref, rel=1.5e-2, mx=3e-2)
+
+
+@pytest.mark.parametrize("B,h,w,C,cin,H,W", [(2, 37, 37, 64, 32, 65, 65), (1, 48, 48, 128, 96, 96, 96)])
+def test_head_upconv_uses_only_cin_channels(dev, B, h, w, C, cin, H, W):
+    """A narrower head padded to a wider pitch (Depth-Anything-V2-Small: 32 head channels stored
+    as 64): the kernel reads the first `cin` channels only -- garbage in the padding changes
+    nothing, and the result is the unfused path's on the cin-channel slice."""
+    ops = _ops()
+    g = torch.Generator(device="cpu").manual_seed(cin + H)
+    x = _bf(torch.randn(B, h, w, C, generator=g)).to(dev)
+    w2 = _bf(torch.randn(32, C, 3, 3, generator=g) / math.sqrt(9 * cin))
+    w2p = w2.permute(0, 2, 3, 1).reshape(32, 9 * C).contiguous().to(dev)
+    b2 = (torch.randn(32, generator=g) * 0.1).to(dev)
+    w4 = (torch.randn(32, generator=g) / math.sqrt(32)).to(dev)
+    got = ops.head_upconv(x, H, W, w2p, b2, w4, 0.05, cin=cin)
+    x2 = x.clone()
+    x2[..., cin:] = float("nan")
+    again = ops.head_upconv(x2, H, W, w2p, b2, w4, 0.05, cin=cin)
+    assert torch.equal(got, again)
+    xs = x[..., :cin].contiguous()
+    ws = w2[:, :cin].permute(0, 2, 3, 1).reshape(32, 9 * cin).contiguous().to(dev)
+    want = ops.head_upconv(xs, H, W, ws, b2, w4, 0.05)
+    assert torch.equal(got, want)
+    unfused = ops.head_out(ops.conv2d(ops.resize_bilinear(xs, H, W, align_corners=True), ws, bias=b2, act="relu"), w4, 0.05)
+    _close(got, unfused, rel=2e-3, mx=5e-3)
