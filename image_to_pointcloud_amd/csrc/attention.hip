@@ -231,8 +231,30 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
 //    32-key half (T = 577 = 9*64 + 1: the tail was a whole wasted 64-key tile);
 //  * waves whose 32 query rows are all beyond T skip the MFMA/softmax work.
 __device__ __forceinline__ int v_swz(int row) { return ((row >> 1) & 1) << 2; }
+// K image: 16-B chunk c of key row r at c ^ ((r >> 1) & 7).  A ds_read_b128 serves 16 lanes per LDS
+// cycle (lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} and their +32 twins); a group's 16 keys
+// fall into 8 even and 8 odd rows, the parity picks the 128-B half of the 256-B bank row, and
+// (r >> 1) & 7 is a bijection on each parity class of a group -- conflict-free.  The r & 7 swizzle of
+// r04 mapped keys 20-27 onto the chunks of keys 0-3 / 12-15: every K read was 2-way conflicted.
+__device__ __forceinline__ int k_swz(int row) { return (row >> 1) & 7; }
 
 typedef short v4s __attribute__((ext_vector_type(4)));
+
+// 16 B per lane global -> LDS at lds_base + 16 * lane (buffer_load ... lds), issued by inline asm.
+// Through __builtin_amdgcn_raw_ptr_buffer_load_lds the compiler sees an LDS write it cannot prove
+// disjoint from the current tile's ds_reads, so it put s_waitcnt vmcnt(3..0) in front of this tile's
+// QK^T MFMAs -- each tile waited for the NEXT tile's K / V to land and the prefetch hid nothing.  The
+// kernel orders the DMA itself: vmcnt(0) + barrier before a buffer is read.  M0 carries the LDS base
+// (nothing the compiler generates in this kernel uses M0).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t lds_base, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rs), "s"(soff)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
 
 __device__ __forceinline__ v4s tr_read(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
@@ -245,6 +267,62 @@ __device__ __forceinline__ v4s tr_read(const uint8_t* p) {
 // them) instead of one v_pk_fma_f32 per pair -- packed FP32 ops cost extra issue cycles beside
 // MFMAs (MI355X_MICROARCH.md, filler prices) -- and the row max across the two lane halves by
 // v_permlane32_swap instead of ds_bpermute; the same operations, so bit-identical
+
+// The normalised output rows of one wave: bf16 out[row][D] or (F8OUT) the MX fp8 operand.
+template <bool F8OUT>
+__device__ __forceinline__ void store_rows(const f32x16 (&o)[2], float inv, int q, int T, int b, int h, int D, int lane,
+                                           bf16_t* __restrict__ out, uint8_t* __restrict__ out8,
+                                           uint8_t* __restrict__ out8s, int lds8) {
+  const int hh = lane >> 5;
+  if constexpr (F8OUT) {
+    // lane (lq, hh) holds d = 32 dt + 8 g + 4 hh + e of its query; the 32-d block dt is split over
+    // the lane pair (lq, lq + 32), which trade amax and bytes by v_permlane32_swap (both lanes of a
+    // pair share q, so both take this branch or neither)
+    if (q < T) {
+      const int64_t row = (int64_t)b * T + q;
+      uint32_t sbytes = 0;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        float v[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t w0 = pack_bf16(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+          const uint32_t w1 = pack_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+          v[4 * g + 0] = __uint_as_float(w0 << 16); v[4 * g + 1] = __uint_as_float(w0 & 0xffff0000u);
+          v[4 * g + 2] = __uint_as_float(w1 << 16); v[4 * g + 3] = __uint_as_float(w1 & 0xffff0000u);
+        }
+        float am = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) am = fmaxf(am, fabsf(v[e]));
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(am), __float_as_uint(am), false, false);
+        am = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        const int ex = mx::mx_exponent(am);
+        const float mul = mx::exp2i(-ex);
+        uint32_t d[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) d[g] = mx::pack_e4m3(v[4 * g] * mul, v[4 * g + 1] * mul, v[4 * g + 2] * mul, v[4 * g + 3] * mul);
+        // hh = 0 ends with bytes 0-15 of the block, hh = 1 with bytes 16-31
+        const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+        *reinterpret_cast<uint4*>(out8 + row * (int64_t)D + h * 64 + 32 * dt + 16 * hh) = make_uint4(s0[0], s0[1], s1[0], s1[1]);
+        sbytes |= (uint32_t)(ex + 127) << (8 * dt);
+      }
+      if (hh == 0) *reinterpret_cast<uint16_t*>(out8s + row * (int64_t)lds8 + 2 * h) = (uint16_t)sbytes;
+    }
+  } else if (q < T) {
+    bf16_t* orow = out + ((int64_t)b * T + q) * D + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * hh;
+        uint2 w;
+        w.x = pack_bf16(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        w.y = pack_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d) = w;
+      }
+  }
+}
 
 // F8OUT: the output is written as the MX fp8 operand of the next GEMM (C5's attention-out) instead of
 // bf16: e4m3 bytes out8[row][NH * 64] and one E8M0 scale byte per 32 d, out8s[row * lds8 + 2 h + dt],
@@ -300,17 +378,17 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
   for (int j = 0; j < 2; ++j) {
     const int row = (wid * 2 + j) * 8 + (lane >> 3);
     const int pchunk = lane & 7;
-    koff[j] = (uint32_t)((row * ld + (pchunk ^ (row & 7)) * 8) * 2);
+    koff[j] = (uint32_t)((row * ld + (pchunk ^ k_swz(row)) * 8) * 2);
     voff[j] = (uint32_t)((row * ld + (pchunk ^ v_swz(row)) * 8) * 2);
   }
   auto stage = [&](int buf, int kt) {
     uint8_t* sK = smem + buf * 2 * kTileBytes;
     uint8_t* sV = sK + kTileBytes;
-    const uint32_t t0 = (uint32_t)kt * tile_bytes;
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane((uint32_t)kt * tile_bytes);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(k_rs, (lds_ptr_t)(sK + (wid * 2 + j) * 8 * 128), 16, koff[j] + t0, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(v_rs, (lds_ptr_t)(sV + (wid * 2 + j) * 8 * 128), 16, voff[j] + t0, 0, 0, 0);
+      dma16(k_rs, __builtin_amdgcn_readfirstlane(lds_addr(sK + (wid * 2 + j) * 8 * 128)), koff[j], t0);
+      dma16(v_rs, __builtin_amdgcn_readfirstlane(lds_addr(sV + (wid * 2 + j) * 8 * 128)), voff[j], t0);
     }
   };
 
@@ -323,6 +401,11 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
   const int nt = (T + kKV - 1) / kKV;
   stage(0, 0);
+  // vmcnt(0) by the builtin, which the compiler's wait-count pass sees: the Q fragments are then known
+  // to have landed here.  (With no wait it knows of, it placed the Q waits at their first use INSIDE
+  // the loop -- vmcnt(3..0) in front of the QK^T MFMAs of every tile, which in hardware waited for the
+  // next tile's just-issued DMA.)
+  __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
   __syncthreads();
 
   for (int kt = 0; kt < nt; ++kt) {
@@ -342,7 +425,7 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int lchunk = 2 * s + hh;
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ (key & 7)) << 4));
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ k_swz(key)) << 4));
           // s == 0 starts from an inline-constant zero accumulator (no 16 v_movs per chain)
           st[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? f32x16{} : st[k2], 0, 0, 0);
         }
@@ -431,58 +514,200 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
         }
       }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's K / V landed (this wave's part)
+    __syncthreads();                                     // ... and every wave's
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  store_rows<F8OUT>(o, 1.0f / l_tot, q, T, b, h, D, lane, out, out8, out8s, lds8);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_attention_fast: k_attention_tr's tiling and staging with a shorter softmax per tile (r05).
+// What bounds k_attention_tr is vector issue, not the matrix pipe (PMC, profiles/r05_attention_pmc.txt:
+// ~190 VALU per 64-key tile per wave beside 16 MFMAs, MFMA busy ~29 %).  Per score it spent an FMA
+// (scale and max subtraction), half a v_max3 (tile max), an exp, an add and half a cvt.  Here:
+//  * Q arrives multiplied by scale * log2(e): the network folds that factor into the Q rows of its
+//    QKV weights and bias (fp32, before their one bf16 rounding -- so no extra rounding anywhere), and
+//    the scores come out of the MFMA in the exp2 domain (i2pc_attention_q2 / _q2_fp8);
+//  * the QK^T accumulators start from -m (a 16-register block holding minus the row's running max,
+//    rewritten only when the max moves), so the MFMA itself subtracts it: p = exp2(st), no FMA;
+//  * the running max moves only when it must (threshold rescale): a tile's probabilities are taken
+//    against the current m as long as none of them can grow large -- a lane's partial row sum below
+//    2^8 bounds every p below 2^8, harmless for the bf16 P operand and the fp32 O / l accumulators.
+//    Only when a lane's sum reaches 2^8 (a score above m + 3 at least) does the wave take the full
+//    path: the tile max, m += max(0, tile max - m), the tile's p again and the O / l rescale.  The
+//    first tile always takes it (m starts at that tile's max, so every row's l >= 1).
+// The result is the same softmax (O / l is invariant to the reference point m); it differs from
+// k_attention_tr by rounding only (P in bf16 against a different reference point).  (Scaling Q inside
+// the kernel instead -- bf16(q * c) -- would add a rounding of Q whose error grows with the score: 6 %
+// of the largest output on x4 scores against torch fp32, outside the 3 % bound; measured r05.)
+template <int OCC, bool F8OUT = false>
+__global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __restrict__ qkv, int B, int T, int NH,
+                                                             bf16_t* __restrict__ out,
+                                                             uint8_t* __restrict__ out8 = nullptr,
+                                                             uint8_t* __restrict__ out8s = nullptr, int lds8 = 0) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * 2 * kTileBytes];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qtiles = (T + kQ - 1) / kQ;
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, xq = nwg >> 3, xr = nwg & 7;
+  int bid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (blockIdx.x >> 3);
+  const int qt = bid % qtiles;
+  bid /= qtiles;
+  const int h = bid % NH;
+  const int b = bid / NH;
+  const int D = NH * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const bf16_t* Qg = qkv + (int64_t)b * T * ld + h * 64;
+  const bf16_t* Kg = Qg + D;
+  const bf16_t* Vg = Qg + 2 * D;
+
+  const int hh = lane >> 5;
+  const int lq = lane & 31;
+  const int q = qt * kQ + wid * 32 + lq;
+  const int qc = min(q, T - 1);
+  const bool wave_active = qt * kQ + wid * 32 < T;
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qg + qc * ld + 16 * s + 8 * hh);
+
+  const uint32_t span = (uint32_t)(((int64_t)(T - 1) * ld + 64) * 2);
+  const __amdgpu_buffer_rsrc_t k_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Kg), 0, span, 0x00020000);
+  const __amdgpu_buffer_rsrc_t v_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Vg), 0, span, 0x00020000);
+  const uint32_t tile_bytes = (uint32_t)(kKV * ld * 2);
+  uint32_t koff[2], voff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wid * 2 + j) * 8 + (lane >> 3);
+    const int pchunk = lane & 7;
+    koff[j] = (uint32_t)((row * ld + (pchunk ^ k_swz(row)) * 8) * 2);
+    voff[j] = (uint32_t)((row * ld + (pchunk ^ v_swz(row)) * 8) * 2);
+  }
+  auto stage = [&](int buf, int kt) {
+    uint8_t* sK = smem + buf * 2 * kTileBytes;
+    uint8_t* sV = sK + kTileBytes;
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane((uint32_t)kt * tile_bytes);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      dma16(k_rs, __builtin_amdgcn_readfirstlane(lds_addr(sK + (wid * 2 + j) * 8 * 128)), koff[j], t0);
+      dma16(v_rs, __builtin_amdgcn_readfirstlane(lds_addr(sV + (wid * 2 + j) * 8 * 128)), voff[j], t0);
+    }
+  };
+  stage(0, 0);
+  __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): Q and tile 0 landed (see k_attention_tr)
+  __syncthreads();
+
+  f32x16 o[2];
+  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+  f32x16 nm;                                     // -m of this lane's query, all 16 entries alike
+  for (int i = 0; i < 16; ++i) nm[i] = 0.f;
+  float l_run = 0.f;
+  constexpr float kThresh = 256.f;               // 2^8
+
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int nt = (T + kKV - 1) / kKV;
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) stage(cur ^ 1, kt + 1);
+    const uint8_t* sK = smem + cur * 2 * kTileBytes;
+    const uint8_t* sV = sK + kTileBytes;
+    const int nvalid = T - kt * kKV;
+    const bool half = nvalid <= 32;
+    if (wave_active) {
+      f32x16 st[2];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        if (k2 == 1 && half) break;
+        const int key = 32 * k2 + lq;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int lchunk = 2 * s + hh;
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ k_swz(key)) << 4));
+          st[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? nm : st[k2], 0, 0, 0);
+        }
+      }
+      if (half) for (int i = 0; i < 16; ++i) st[1][i] = -INFINITY;
+      if (nvalid < kKV) {
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = 32 * k2 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= nvalid) st[k2][r] = -INFINITY;
+          }
+      }
+      float ls = 0.f;
+      uint32_t pk[2][8];
+      auto probs = [&](float sub) {
+        ls = 0.f;
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const float p0 = __builtin_amdgcn_exp2f(st[k2][r] - sub);
+            const float p1 = __builtin_amdgcn_exp2f(st[k2][r + 1] - sub);
+            ls += p0 + p1;
+            pk[k2][r >> 1] = pack_bf16(p0, p1);
+          }
+      };
+      bool full = kt == 0;                                   // uniform
+      if (!full) {
+        probs(0.f);
+        full = __ballot(ls >= kThresh) != 0;
+      }
+      if (full) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[k2][r]);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        const float delta = kt == 0 ? mx : fmaxf(mx, 0.f);   // finite: tile 0 holds >= 1 key
+        probs(delta);
+        if (kt > 0) {
+          const float alpha = __builtin_amdgcn_exp2f(-delta);
+          l_run *= alpha;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) nm[i] -= delta;
+      }
+      l_run += ls;
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        if (k2 == 1 && half) break;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pf;
+          {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 u = {pk[k2][4 * s + 0], pk[k2][4 * s + 1], pk[k2][4 * s + 2], pk[k2][4 * s + 3]};
+            pf = __builtin_bit_cast(bf16x8, u);
+          }
+          const int kb = 32 * k2 + 16 * s + 4 * (tg >> 1);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int d0 = 32 * dt + 16 * (tg & 1) + 4 * tp;
+            const int lch = d0 >> 3, within = (d0 & 7) * 2;
+            const int r0 = kb + tq, r1 = kb + 8 + tq;
+            const v4s lo = tr_read(sV + r0 * 128 + ((lch ^ v_swz(r0)) << 4) + within);
+            const v4s hi = tr_read(sV + r1 * 128 + ((lch ^ v_swz(r1)) << 4) + within);
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32);
-  const float inv = 1.0f / l_tot;
-  if constexpr (F8OUT) {
-    // lane (lq, hh) holds d = 32 dt + 8 g + 4 hh + e of its query; the 32-d block dt is split over
-    // the lane pair (lq, lq + 32), which trade amax and bytes by v_permlane32_swap (both lanes of a
-    // pair share q, so both take this branch or neither)
-    if (q < T) {
-      const int64_t row = (int64_t)b * T + q;
-      uint32_t sbytes = 0;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        float v[16];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint32_t w0 = pack_bf16(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
-          const uint32_t w1 = pack_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-          v[4 * g + 0] = __uint_as_float(w0 << 16); v[4 * g + 1] = __uint_as_float(w0 & 0xffff0000u);
-          v[4 * g + 2] = __uint_as_float(w1 << 16); v[4 * g + 3] = __uint_as_float(w1 & 0xffff0000u);
-        }
-        float am = 0.f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) am = fmaxf(am, fabsf(v[e]));
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(am), __float_as_uint(am), false, false);
-        am = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-        const int ex = mx::mx_exponent(am);
-        const float mul = mx::exp2i(-ex);
-        uint32_t d[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) d[g] = mx::pack_e4m3(v[4 * g] * mul, v[4 * g + 1] * mul, v[4 * g + 2] * mul, v[4 * g + 3] * mul);
-        // hh = 0 ends with bytes 0-15 of the block, hh = 1 with bytes 16-31
-        const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
-        const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
-        *reinterpret_cast<uint4*>(out8 + row * (int64_t)D + h * 64 + 32 * dt + 16 * hh) = make_uint4(s0[0], s0[1], s1[0], s1[1]);
-        sbytes |= (uint32_t)(ex + 127) << (8 * dt);
-      }
-      if (hh == 0) *reinterpret_cast<uint16_t*>(out8s + row * (int64_t)lds8 + 2 * h) = (uint16_t)sbytes;
-    }
-  } else if (q < T) {
-    bf16_t* orow = out + ((int64_t)b * T + q) * D + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * hh;
-        uint2 w;
-        w.x = pack_bf16(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
-        w.y = pack_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(orow + d) = w;
-      }
-  }
+  store_rows<F8OUT>(o, 1.0f / l_tot, q, T, b, h, D, lane, out, out8, out8s, lds8);
 }
 
 }  // namespace attn
@@ -533,7 +758,7 @@ extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads,
     hipLaunchKernelGGL(attn::k_attention_tr<2>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   else if (occ == 4)
-    hipLaunchKernelGGL(attn::k_attention_tr<4>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL((attn::k_attention_tr<4, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   else if (g_scalar)
     hipLaunchKernelGGL((attn::k_attention_tr<3, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
@@ -542,4 +767,30 @@ extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads,
     hipLaunchKernelGGL(attn::k_attention_tr<3>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   return check_launch("attention");
+}
+
+extern "C" int i2pc_attention_q2(const void* qkv, int batch, int tokens, int heads, void* out, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(qkv && out, "NULL pointer");
+  I2PC_REQUIRE(batch > 0 && tokens > 0 && heads > 0, "attention_q2: empty shape");
+  const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
+  hipLaunchKernelGGL((attn::k_attention_fast<3>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, static_cast<uint16_t*>(out));
+  return check_launch("attention_q2");
+}
+
+extern "C" int i2pc_attention_q2_fp8(const void* qkv, int batch, int tokens, int heads, void* out, int64_t ldo,
+                                     void* out_scale, int64_t ldo_scale, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(qkv && out && out_scale, "NULL pointer");
+  I2PC_REQUIRE(batch > 0 && tokens > 0 && heads > 0, "attention_q2_fp8: empty shape");
+  I2PC_REQUIRE(ldo == (int64_t)heads * 64, "attention_q2_fp8: the fp8 rows are dense (ldo = heads * 64)");
+  I2PC_REQUIRE(ldo_scale * 128 >= (int64_t)heads * 64 && (reinterpret_cast<uintptr_t>(out) % 16) == 0 &&
+                   (reinterpret_cast<uintptr_t>(out_scale) % 4) == 0,
+               "attention_q2_fp8: scale rows of ldo_scale dwords cover heads * 2 blocks; 16-B aligned data");
+  const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
+  hipLaunchKernelGGL((attn::k_attention_fast<3, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, nullptr, static_cast<uint8_t*>(out),
+                     static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
+  return check_launch("attention_q2_fp8");
 }

@@ -150,7 +150,6 @@ static int forward_da(i2pc_model* m, const uint8_t* bgr, float* depth, bool plan
     TRY(gemm(m, d, plan, s));
   }
   if (!plan) TRY(i2pc_cls_pos(Wf("cls"), Wf("pos0"), B, T, D, static_cast<float*>(m->x), s));
-  const float scale = 1.0f / std::sqrt((float)(D / heads));
   // encoder on the shifted bf16 residual stream (depth_anything._encoder_stream)
   const void* res = m->x;
   bool res_f32 = true;
@@ -175,7 +174,7 @@ static int forward_da(i2pc_model* m, const uint8_t* bgr, float* depth, bool plan
       d.c = m->qkv; d.ldc = 3 * D;
     }
     TRY(gemm(m, d, plan, s));
-    if (!plan) TRY(i2pc_attention(m->qkv, B, T, heads, scale, m->att, s));
+    if (!plan) TRY(i2pc_attention_q2(m->qkv, B, T, heads, m->att, s));   // Q folded (file version 2)
     // attention-out + residual -> the stream (bf16, relative to sh0) + 32-column partials
     d = desc0();
     d.a = m->att; d.lda = D; d.m = M; d.n = D; d.k = D;
@@ -297,7 +296,8 @@ static int parse(const std::vector<char>& buf, int32_t* ints, float* floats, std
     return set_error(I2PC_EINVAL, "model: not an i2pc network file");
   std::memcpy(ints, buf.data() + 8, 32 * 4);
   std::memcpy(floats, buf.data() + 8 + 128, 16 * 4);
-  if (ints[I_VERSION] != 1) return set_error(I2PC_EUNSUPPORTED, "model: file version %d", ints[I_VERSION]);
+  // version 2: the Q rows of every QKV weight / bias carry the softmax scale * log2(e) (attention_q2)
+  if (ints[I_VERSION] != 2) return set_error(I2PC_EUNSUPPORTED, "model: file version %d (this library reads 2)", ints[I_VERSION]);
   const int nt = ints[I_NTENSORS];
   if (nt <= 0 || nt > 100000 || buf.size() < hdr + (size_t)nt * sizeof(Entry))
     return set_error(I2PC_EINVAL, "model: bad tensor table");

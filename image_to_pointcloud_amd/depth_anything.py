@@ -237,6 +237,10 @@ class DepthAnythingModel:
             p = f"backbone.encoder.layer.{i}."
             q = [sd[p + f"attention.attention.{n}.weight"] for n in ("query", "key", "value")]
             qb = [sd[p + f"attention.attention.{n}.bias"] for n in ("query", "key", "value")]
+            # softmax scale * log2(e) folded into the Q rows (fp32, before the bf16 rounding): the QKV GEMM
+            # writes Q in the exp2 domain that attention(..., q_log2=True) takes
+            wq, bq = ops.fold_q_scale(torch.cat(q, 0), torch.cat(qb, 0), 1.0 / math.sqrt(spec.hidden // spec.heads))
+            q, qb = [wq], [bq]
             l1 = sd[p + "layer_scale1.lambda1"]
             l2 = sd[p + "layer_scale2.lambda1"]
             L = dict(
@@ -390,7 +394,7 @@ class DepthAnythingModel:
         for i, L in enumerate(self.layers if not buf["ln_fold"] else ()):
             ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
             qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
-            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"], q_log2=True)
             ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
             ln = ops.layernorm(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])
             h = ops.linear(ln, L["w_1"], bias=L["b_1"], act="gelu", out=buf["mlp"])
@@ -435,7 +439,7 @@ class DepthAnythingModel:
             else:
                 qkv = ops.linear(a_in, L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
                                  out=buf["qkv"])
-            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"], q_log2=True)
             ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x, ln_part=buf["part"], out_bf16=buf["ln"],
                        ln_shift=buf["shift"], ln_chunk=LN_CHUNK)
             ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=buf["shift"], shift_out=buf["shift"],
@@ -472,7 +476,7 @@ class DepthAnythingModel:
             else:
                 qkv = ops.linear(buf["ln"], L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
                                  out=buf["qkv"])
-            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"], q_log2=True)
             ops.linear(att, L["w_o"], bias=L["b_o"], res=res, res_shift=rsh, out=buf["ln"], ln_part=buf["part"],
                        ln_shift=sh0, ln_chunk=LN_CHUNK)
             ops.ln_rowstats(buf["part"], s.eps, out=buf["rs"], shift_in=sh0, shift_out=sh1, chunk=LN_CHUNK)

@@ -239,6 +239,10 @@ class DPTDepthModel:
             p = f"dpt.encoder.layer.{i}."
             q = [sd[p + f"attention.attention.{n}.weight"] for n in ("query", "key", "value")]
             qb = [sd[p + f"attention.attention.{n}.bias"] for n in ("query", "key", "value")]
+            # softmax scale * log2(e) folded into the Q rows (fp32, before the bf16 rounding): the QKV GEMM
+            # writes Q in the exp2 domain that attention(..., q_log2=True) takes
+            wq, bq = ops.fold_q_scale(torch.cat(q, 0), torch.cat(qb, 0), 1.0 / math.sqrt(spec.hidden // spec.heads))
+            q, qb = [wq], [bq]
             L = dict(
                 ln1_g=f32(sd[p + "layernorm_before.weight"]), ln1_b=f32(sd[p + "layernorm_before.bias"]),
                 w_qkv=bf(torch.cat(q, 0)), b_qkv=f32(torch.cat(qb, 0)),
@@ -380,7 +384,7 @@ class DPTDepthModel:
             if not fold:
                 ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["ln"])
                 qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
-                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"], q_log2=True)
                 ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
                 ln = ops.layernorm(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])
                 h = ops.linear(ln, L["w_1"], bias=L["b_1"], act="gelu", out=buf["mlp"])
@@ -395,7 +399,7 @@ class DPTDepthModel:
             else:
                 qkv = ops.linear(a_in, L["w_qkv_f"], bias=L["b_qkv_f"], ln_rows=buf["rs"], col_sum=L["s_qkv"],
                                  out=buf["qkv"])
-            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+            att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"], q_log2=True)
             if BF16_STREAM:
                 a_in = self._stream_layer(i, L, att, a_in, buf)
                 continue

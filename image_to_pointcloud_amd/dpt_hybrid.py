@@ -283,6 +283,8 @@ class DPTHybridModel(DPTDepthModel):
             q = f"dpt.encoder.layer.{i}."
             wq = torch.cat([sd[q + f"attention.attention.{n}.weight"] for n in ("query", "key", "value")], 0)
             bq = torch.cat([sd[q + f"attention.attention.{n}.bias"] for n in ("query", "key", "value")], 0)
+            # softmax scale * log2(e) folded into the Q rows (fp32, before any rounding; see dpt.py)
+            wq, bq = ops.fold_q_scale(wq, bq, 1.0 / math.sqrt(spec.hidden // spec.heads))
             self.layers.append(dict(
                 ln1_g=f32(sd[q + "layernorm_before.weight"]), ln1_b=f32(sd[q + "layernorm_before.bias"]),
                 w_qkv=lin(wq, "qkv"), b_qkv=f32(bq),
@@ -369,10 +371,10 @@ class DPTHybridModel(DPTDepthModel):
                 ln = ops.layernorm(x, L["ln1_g"], L["ln1_b"], s.eps, out=buf["lnb"])
                 qkv = ops.linear(ln, L["w_qkv"], bias=L["b_qkv"], out=buf["qkv"])
             if f8("o"):       # the attention epilogue writes attention-out's fp8 operand directly
-                att8 = ops.attention(qkv, B, T, s.heads, scale, out=buf["att8"])
+                att8 = ops.attention(qkv, B, T, s.heads, scale, out=buf["att8"], q_log2=True)
                 ops.linear_fp8(att8, L["w_o"], bias=L["b_o"], res=x, out=x)
             else:
-                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"])
+                att = ops.attention(qkv, B, T, s.heads, scale, out=buf["att"], q_log2=True)
                 ops.linear(att, L["w_o"], bias=L["b_o"], res=x, out=x)
             if f8("fc1"):       # FC1's epilogue writes FC2's operand format
                 ln = ops.layernorm_fp8(x, L["ln2_g"], L["ln2_b"], s.eps, out=buf["ln"])

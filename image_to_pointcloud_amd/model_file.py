@@ -25,7 +25,7 @@ import struct
 
 MAGIC = b"I2PCNET1"
 FAMILY_DEPTH_ANYTHING = 1
-VERSION = 1
+VERSION = 2   # 2: the Q rows of the QKV weights carry the softmax scale * log2(e) (ops.fold_q_scale)
 # int header slots
 (I_FAMILY, I_VERSION, I_IN_H, I_IN_W, I_OUT_H, I_OUT_W, I_GH, I_GW, I_PATCH, I_HIDDEN, I_LAYERS, I_HEADS, I_MLP,
  I_FUSION, I_HEAD_HIDDEN, I_H1P, I_NECK0, I_FAC0, I_OUT0, I_NTENSORS, I_PITCH, I_STRIDE0) = (

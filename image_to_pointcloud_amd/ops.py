@@ -57,6 +57,9 @@ _lib.register("i2pc_layernorm", ctypes.c_int, [c_void_p, c_int64, c_void_p, c_vo
                                                ctypes.c_int, ctypes.c_int, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_attention", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_float, c_void_p, c_void_p])
+_lib.register("i2pc_attention_q2", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p])
+_lib.register("i2pc_attention_q2_fp8", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
+                                                      ctypes.c_int64, c_void_p, ctypes.c_int64, c_void_p])
 _lib.register("i2pc_attention_fp8", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                                    c_void_p, c_int64, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_upsample2x", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -441,10 +444,12 @@ def layernorm(x, gamma, beta, eps, out=None, mean_out=None):
     return out
 
 
-def attention(qkv, batch, tokens, heads, scale, out=None):
+def attention(qkv, batch, tokens, heads, scale, out=None, q_log2=False):
     """Fused self-attention (i2pc_attention).  out: bf16 [batch*tokens, heads*64], or an Fp8 of that
     shape: the MX fp8 operand of the next GEMM written by the kernel's epilogue (i2pc_attention_fp8;
-    the same bytes as quant_fp8 of the bf16 output)."""
+    the same bytes as quant_fp8 of the bf16 output).  q_log2: the Q block already holds
+    q * scale * log2(e) (folded into the QKV weights, `fold_q_scale`); scale is then ignored and the
+    threshold-rescale kernel runs (i2pc_attention_q2 / _q2_fp8)."""
     torch = _torch()
     _check(qkv, torch.bfloat16, "qkv")
     D = heads * 64
@@ -455,12 +460,35 @@ def attention(qkv, batch, tokens, heads, scale, out=None):
         if tuple(out.data.shape) != (batch * tokens, D):
             raise ValueError(f"attention fp8 out {tuple(out.data.shape)} != {(batch * tokens, D)}")
         with _Timed("k_attention", flops, 2.0 * 3 * batch * tokens * D + (1.0 + 1.0 / 32) * batch * tokens * D):
-            _lib.call("i2pc_attention_fp8", _p(qkv), batch, tokens, heads, float(scale), _p(out.data), D,
-                      _p(out.scale), out.scale.shape[-1] // 4, _stream())
+            if q_log2:
+                _lib.call("i2pc_attention_q2_fp8", _p(qkv), batch, tokens, heads, _p(out.data), D,
+                          _p(out.scale), out.scale.shape[-1] // 4, _stream())
+            else:
+                _lib.call("i2pc_attention_fp8", _p(qkv), batch, tokens, heads, float(scale), _p(out.data), D,
+                          _p(out.scale), out.scale.shape[-1] // 4, _stream())
         return out
     with _Timed("k_attention", flops, 2.0 * 4 * batch * tokens * D):
-        _lib.call("i2pc_attention", _p(qkv), batch, tokens, heads, float(scale), _p(out), _stream())
+        if q_log2:
+            _lib.call("i2pc_attention_q2", _p(qkv), batch, tokens, heads, _p(out), _stream())
+        else:
+            _lib.call("i2pc_attention", _p(qkv), batch, tokens, heads, float(scale), _p(out), _stream())
     return out
+
+
+LOG2E = 1.4426950408889634
+
+
+def fold_q_scale(w_qkv, b_qkv, scale):
+    """The QKV weights and bias (fp32, Q | K | V row blocks of equal size) with the Q rows multiplied by
+    scale * log2(e), in fp32 before any bf16 rounding: the product Q is then what
+    attention(..., q_log2=True) takes (the softmax scale and the exp2 base conversion ride on the GEMM)."""
+    c = float(scale) * LOG2E
+    d = w_qkv.shape[0] // 3
+    w = w_qkv.float().clone()
+    b = b_qkv.float().clone()
+    w[:d] *= c
+    b[:d] *= c
+    return w, b
 
 
 def upsample2x(x, add=None, out=None):

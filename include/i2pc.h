@@ -445,6 +445,16 @@ int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scal
  * equal i2pc_quant_fp8 of i2pc_attention's bf16 output (quantised from the bf16-rounded values). */
 int i2pc_attention_fp8(const void* qkv, int batch, int tokens, int heads, float scale, void* out, int64_t ldo,
                        void* out_scale, int64_t ldo_scale, void* stream);
+/* i2pc_attention with Q already in the exp2 domain: the Q block of qkv holds q * scale * log2(e) (the
+ * network folds that factor into the Q rows of its QKV weights and bias in fp32, before their bf16
+ * rounding), and out = softmax_2(Q K^T) V = softmax(q K^T * scale) V.  Runs the threshold-rescale
+ * kernel (k_attention_fast: no per-score scale FMA or tile max; the running max moves only when a
+ * tile's probabilities could reach 2^8).  Same argument rules as i2pc_attention. */
+int i2pc_attention_q2(const void* qkv, int batch, int tokens, int heads, void* out, void* stream);
+/* i2pc_attention_q2 writing the MX fp8 operand (as i2pc_attention_fp8; the bytes equal i2pc_quant_fp8
+ * of i2pc_attention_q2's bf16 output). */
+int i2pc_attention_q2_fp8(const void* qkv, int batch, int tokens, int heads, void* out, int64_t ldo,
+                          void* out_scale, int64_t ldo_scale, void* stream);
 
 /* Bilinear 2x upsample, align_corners = True, NHWC bf16 (nn.functional.interpolate,
  * modeling_dpt.py:504-506, 698), optional + add (bf16, output shape). */

@@ -193,6 +193,65 @@ def test_attention_lazy_rescale_bit_exact(dev, B, T, H, spike):
     _close(outs[1], ref, rel=1.2e-2, mx=3e-2)
 
 
+def _q2_inputs(B, T, H, mode, seed):
+    """qkv (bf16) for the attention tests, and its Q-in-the-exp2-domain form (the Q block times
+    0.125 * log2(e) in fp32, rounded once to bf16 -- what a QKV GEMM with fold_q_scale weights writes)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    qkv = torch.randn(B * T, 3, H, 64, generator=g) * 1.5
+    if mode == "spike":
+        q = qkv[:, 0]
+        for kt in (T // 3, (2 * T) // 3, T - 1):
+            qkv[kt::T, 1] = q[(kt * 7) % T::T] * 3.0
+    elif mode == "large":
+        qkv[:, :2] *= 4.0
+    elif mode == "negative":
+        qkv[:, 0] = qkv[:, 0].abs() + 2.0
+        qkv[:, 1] = -(qkv[:, 1].abs() + 2.0)
+    elif mode == "rising":
+        qkv[:, 0] = 1.0
+        qkv[:, 1] = (torch.arange(B * T) % T).float().view(-1, 1, 1) * 0.25
+    q2 = qkv.clone()
+    q2[:, 0] *= 0.125 * 1.4426950408889634
+    return _bf(qkv.reshape(B * T, 3 * H * 64)), _bf(q2.reshape(B * T, 3 * H * 64))
+
+
+@pytest.mark.parametrize("B,T,H,mode", [(2, 577, 16, "plain"), (2, 577, 16, "spike"), (1, 1370, 6, "spike"),
+                                         (2, 130, 12, "large"), (2, 577, 16, "large"), (1, 300, 4, "negative"),
+                                         (3, 1, 4, "large"), (1, 33, 2, "rising"), (1, 37, 6, "plain")])
+def test_attention_q2_threshold_rescale(dev, B, T, H, mode):
+    """i2pc_attention_q2 (Q in the exp2 domain, threshold rescale, -m folded into the QK^T
+    accumulators) against torch fp32 SDPA of the same bf16 operands (softmax_2(Q K^T) = SDPA with scale
+    ln 2), on inputs that drive its full path mid-sequence: spikes (late keys aligned with some
+    queries), large scores (x4: the running max moves by far more than 2^8 between tiles), uniformly
+    very negative scores (every p far below 1 against tile 0's reference point), and a rising
+    sequence (every 64-key tile raises every row's max).  The raw-Q kernel on the unscaled operands is
+    held to the same bound against its own reference."""
+    ops = _ops()
+    qkv, q2 = _q2_inputs(B, T, H, mode, T * 7 + H)
+    qkv, q2 = qkv.to(dev), q2.to(dev)
+    q, k, v = q2.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = F.scaled_dot_product_attention(q, k, v, scale=math.log(2.0)).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    got = ops.attention(q2, B, T, H, 0.125, q_log2=True)
+    assert torch.isfinite(got.float()).all()
+    _close(got, ref, rel=1.2e-2, mx=3e-2)
+    q, k, v = qkv.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    _close(ops.attention(qkv, B, T, H, 0.125), ref, rel=1.2e-2, mx=3e-2)
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 577, 12), (1, 37, 6), (3, 1, 4), (2, 130, 12)])
+def test_attention_q2_fp8_out_bit_exact(dev, B, T, H):
+    """i2pc_attention_q2_fp8 equals i2pc_quant_fp8 of i2pc_attention_q2's bf16 output byte for byte."""
+    ops = _ops()
+    _, q2 = _q2_inputs(B, T, H, "spike", T * 3 + H)
+    q2 = q2.to(dev)
+    ref = ops.quant_fp8(ops.attention(q2, B, T, H, 0.125, q_log2=True))
+    got = ops.attention(q2, B, T, H, 0.125, out=ops.empty_fp8((B * T, H * 64), dev), q_log2=True)
+    torch.cuda.synchronize()
+    assert torch.equal(got.data, ref.data)
+    assert torch.equal(got.scale, ref.scale)
+
+
 @pytest.mark.parametrize("B,H,W,C", [(2, 12, 12, 256), (1, 5, 7, 64), (1, 192, 192, 128)])
 def test_upsample2x_align_corners(dev, B, H, W, C):
     ops = _ops()

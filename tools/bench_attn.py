@@ -3,7 +3,9 @@ import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from image_to_pointcloud_amd import ops
-for B, T, H in [(32, 577, 16), (32, 1370, 6), (8, 1370, 6)]:
+SHAPES = [(32, 577, 16), (32, 1370, 6), (8, 1370, 6)]
+if os.environ.get("ATTN_SHAPE"): SHAPES = [SHAPES[int(os.environ["ATTN_SHAPE"])]]
+for B, T, H in SHAPES:
     qkv = (torch.randn(B * T, 3 * H * 64, device="cuda") * 1.5).to(torch.bfloat16)
     out = torch.empty(B * T, H * 64, dtype=torch.bfloat16, device="cuda")
     ops.attention(qkv, B, T, H, 0.125, out=out); torch.cuda.synchronize()
