@@ -569,10 +569,6 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
   const int qc = min(q, T - 1);
   const bool wave_active = qt * kQ + wid * 32 < T;
 
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qg + qc * ld + 16 * s + 8 * hh);
-
   const uint32_t span = (uint32_t)(((int64_t)(T - 1) * ld + 64) * 2);
   const __amdgpu_buffer_rsrc_t k_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Kg), 0, span, 0x00020000);
   const __amdgpu_buffer_rsrc_t v_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Vg), 0, span, 0x00020000);
@@ -595,8 +591,15 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
       dma16(v_rs, __builtin_amdgcn_readfirstlane(lds_addr(sV + (wid * 2 + j) * 8 * 128)), voff[j], t0);
     }
   };
+  const int nt = (T + kKV - 1) / kKV;
+  // tile 0's DMA, the Q fragments (compiler-visible loads), then a compiler-visible vmcnt(0), so no
+  // Q wait lands inside the loop (see k_attention_tr).  (A 3-slot ring prefetching two tiles ahead
+  // measured equal, r05.)
   stage(0, 0);
-  __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): Q and tile 0 landed (see k_attention_tr)
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Qg + qc * ld + 16 * s + 8 * hh);
+  __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
   __syncthreads();
 
   f32x16 o[2];
@@ -607,7 +610,6 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
   constexpr float kThresh = 256.f;               // 2^8
 
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
-  const int nt = (T + kKV - 1) / kKV;
 
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
@@ -617,19 +619,28 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
     const int nvalid = T - kt * kKV;
     const bool half = nvalid <= 32;
     if (wave_active) {
+      // the two 32-key halves' MFMA chains interleaved (each MFMA waits for its predecessor in the
+      // chain: back to back in one chain the matrix pipe idles between them), the K fragments of a
+      // d-step read for both halves ahead of its MFMAs
       f32x16 st[2];
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-        if (k2 == 1 && half) break;
-        const int key = 32 * k2 + lq;
+      if (!half) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int lchunk = 2 * s + hh;
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ k_swz(key)) << 4));
-          st[k2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? nm : st[k2], 0, 0, 0);
+          const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(sK + lq * 128 + ((lchunk ^ k_swz(lq)) << 4));
+          const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(sK + (32 + lq) * 128 + ((lchunk ^ k_swz(32 + lq)) << 4));
+          st[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[s], s == 0 ? nm : st[0], 0, 0, 0);
+          st[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[s], s == 0 ? nm : st[1], 0, 0, 0);
         }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int lchunk = 2 * s + hh;
+          const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(sK + lq * 128 + ((lchunk ^ k_swz(lq)) << 4));
+          st[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[s], s == 0 ? nm : st[0], 0, 0, 0);
+        }
+        for (int i = 0; i < 16; ++i) st[1][i] = -INFINITY;
       }
-      if (half) for (int i = 0; i < 16; ++i) st[1][i] = -INFINITY;
       if (nvalid < kKV) {
 #pragma unroll
         for (int k2 = 0; k2 < 2; ++k2)
@@ -703,8 +714,8 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's K / V landed (this wave's part)
+    __syncthreads();                                     // ... and every wave's
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   store_rows<F8OUT>(o, 1.0f / l_tot, q, T, b, h, D, lane, out, out8, out8s, lds8);
