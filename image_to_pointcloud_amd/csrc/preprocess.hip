@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #pragma clang fp contract(off)
@@ -109,6 +110,7 @@ struct DevPlan {
   const int* vy_min; const int* vy_cnt; const int* vy_k;
   const int* tile_lo; const int* tile_n;
   const int* col_a0; const int* col_wb;
+  const uint32_t* lut;    // [3][256]: channel c's output for uint8 u -- fp32 bits (layout 0), then bf16 (layout 1)
 };
 
 }  // namespace pre
@@ -122,6 +124,11 @@ struct i2pc_preprocess_plan {
 namespace i2pc {
 namespace pre {
 
+// Coefficients are < 2^23 in magnitude (22-bit fixed point of weights below 2): sign-extended from 24
+// bits the compiler knows it, and the taps become v_mad_i32_i24 (full rate) -- without it every tap
+// was a v_mad_u64_u32 (a quarter-rate 64-bit multiply), which bound the kernel
+__device__ __forceinline__ int k24(int k) { return (k << 8) >> 8; }
+
 __device__ __forceinline__ uint8_t clip8(int ss) {
   if (ss >= (1 << PB << 8)) return 255;
   if (ss <= 0) return 0;
@@ -130,6 +137,11 @@ __device__ __forceinline__ uint8_t clip8(int ss) {
 
 __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __restrict__ bgr, int layout, void* out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tmp[];   // [rows][CW][3] uint8 (BGR order)
+  // the rescale + normalise of a uint8 value depends on (channel, value) only: a 3 x 256 table (fp32 bits,
+  // or bf16 for the patch rows) built on the host with the same arithmetic replaces, per output value,
+  // an f64 multiply and a correctly rounded fp32 division (which made the vertical pass VALU-heavy)
+  __shared__ uint32_t lut[3 * 256];
+  for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) lut[i] = P.lut[(layout == 0 ? 0 : 3 * 256) + i];
   const int per_img = P.tiles * P.ctiles;
   const int b = blockIdx.x / per_img;
   const int rem = blockIdx.x - b * per_img;
@@ -187,7 +199,7 @@ __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __
       int s0 = 1 << (PB - 1), s1 = s0, s2 = s0;
       for (int x = 0; x < cnt; ++x) {
         const uint8_t* px = row + (xmin + x) * 3;
-        const int kv = k[x];
+        const int kv = k24(k[x]);
         s0 += px[0] * kv;
         s1 += px[1] * kv;
         s2 += px[2] * kv;
@@ -216,24 +228,21 @@ __global__ __launch_bounds__(256) void k_preprocess(DevPlan P, const uint8_t* __
     int s[3] = {1 << (PB - 1), 1 << (PB - 1), 1 << (PB - 1)};
     for (int y = 0; y < cnt; ++y) {
       const uint8_t* t = tmp + ((ymin + y) * CWt + xl) * 3;
-      const int kv = k[y];
+      const int kv = k24(k[y]);
       s[0] += t[0] * kv;
       s[1] += t[1] * kv;
       s[2] += t[2] * kv;
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {       // c = RGB channel; BGR source index 2 - c
-      const uint8_t u = clip8(s[2 - c]);
-      const float f = (float)((double)u * (1.0 / 255.0));
-      const float v = (f - P.mean[c]) / P.stdv[c];
+      const uint32_t v = lut[c * 256 + clip8(s[2 - c])];
       if (layout == 0) {
-        static_cast<float*>(out)[(((int64_t)b * 3 + c) * P.out_h + yy) * OW + xx] = v;
+        static_cast<uint32_t*>(out)[(((int64_t)b * 3 + c) * P.out_h + yy) * OW + xx] = v;
       } else {
         const int p = P.patch;
         const int prow = b * npatch + (yy / p) * np_x + xx / p;
         const int col = c * p * p + (yy % p) * p + (xx % p);
-        __bf16 h = (__bf16)v;
-        static_cast<uint16_t*>(out)[(int64_t)prow * P.pld + col] = *reinterpret_cast<uint16_t*>(&h);
+        static_cast<uint16_t*>(out)[(int64_t)prow * P.pld + col] = (uint16_t)v;
       }
     }
   }
@@ -309,10 +318,23 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
   I2PC_REQUIRE(max_rows * band_row <= kLdsBudget, "LDS band too large (%d rows x %d B)", max_rows, band_row);
   // every check is done: allocate.  One device buffer:
   // hx_min | hx_cnt | hx_k | vy_min | vy_cnt | vy_k | tile_lo | tile_n | col_a0 | col_wb
+  // output table: (float)((double)u / 255 in float64) then (f - mean) / std in float32 (the device formula
+  // of r04, image_transforms.py rescale + normalize), as fp32 bits and as RNE bf16
+  std::vector<int> lut(2 * 3 * 256);
+  for (int c = 0; c < 3; ++c)
+    for (int u = 0; u < 256; ++u) {
+      const float f = (float)((double)u * (1.0 / 255.0));
+      const float v = (f - mean[c]) / stdv[c];
+      uint32_t bits;
+      std::memcpy(&bits, &v, 4);
+      lut[c * 256 + u] = (int)bits;
+      const uint32_t rne = bits + 0x7FFFu + ((bits >> 16) & 1u);   // finite values only
+      lut[3 * 256 + c * 256 + u] = (int)(rne >> 16);
+    }
   std::vector<int> blob;
   auto put = [&](const std::vector<int>& v) { size_t off = blob.size(); blob.insert(blob.end(), v.begin(), v.end()); return off; };
   const size_t o0 = put(hx.xmin), o1 = put(hx.cnt), o2 = put(hx.k), o3 = put(vy.xmin), o4 = put(vy.cnt), o5 = put(vy.k),
-               o6 = put(tlo), o7 = put(tn), o8 = put(ca0), o9 = put(cwb);
+               o6 = put(tlo), o7 = put(tn), o8 = put(ca0), o9 = put(cwb), o10 = put(lut);
   void* dev = nullptr;
   if (hipMalloc(&dev, blob.size() * sizeof(int)) != hipSuccess) return set_error(I2PC_ELAUNCH, "hipMalloc failed");
   if (hipMemcpy(dev, blob.data(), blob.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
@@ -334,6 +356,7 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
   P.vy_min = base + o3; P.vy_cnt = base + o4; P.vy_k = base + o5;
   P.tile_lo = base + o6; P.tile_n = base + o7;
   P.col_a0 = base + o8; P.col_wb = base + o9;
+  P.lut = reinterpret_cast<const uint32_t*>(base + o10);
   *plan = pl;
   return I2PC_OK;
 }
