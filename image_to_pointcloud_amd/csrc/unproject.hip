@@ -2143,8 +2143,21 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
       const uint32_t lo = atomicMin(&sl[1], 0xffffffffu), hi = atomicMax(&sl[2], 0u);   // read at the coherence point
       s.kmin = min(s.kmin, lo);      // (with a fill, finish_targets already merged the median)
       s.kmax = max(s.kmax, hi);
-      if (finish_targets(s, true)) st[b] = s;
-      else { s.err = 1; s.phase = PH_SLOW; st[b] = s; }   // (not expected: the range was the only thing missing)
+      if (finish_targets(s, true)) {
+        st[b] = s;
+      } else {
+        // Not reachable by finish_targets as it stands (the range was the only thing missing); should a
+        // change ever make it so, the image is not left unresolved (no later launch of the chain takes
+        // PH_SLOW) but finishes LOUDLY as the all-NaN map does: NaN median and percentiles, every point
+        // NaN, stats p2 / p98 NaN -- never a silent output from stale selection state.
+        s.err = 2;
+        s.has_med = 1;
+        s.mode = 2;
+        s.med = __uint_as_float(0x7fc00000u);
+        s.p2 = s.p98 = (double)s.med;
+        s.phase = PH_DONE;
+        st[b] = s;
+      }
     }
     return;
   }
