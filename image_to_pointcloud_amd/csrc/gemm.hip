@@ -36,6 +36,20 @@ typedef uint16_t bf16_t;
 
 constexpr int BK = 64;
 
+// A-fragment look-ahead of the bf16 K-steps: m-subtiles whose LDS reads are issued ahead of their
+// MFMAs, the order pinned by scheduling groups (0 = the compiler's own schedule, which at 245 VGPRs
+// reused one fragment register: read -> lgkmcnt(0) -> 4 MFMAs per m-subtile, every LDS latency exposed
+// to the matrix pipe).  r05, in one box: persistent LN-fold QKV / FC1 7.23 -> 6.89 ms per C2 step
+// with 2 (3: equal), step 21.77 -> 21.34 ms, bit-identical.  The tile kernel (I2PC_GEMM_APF_TILE) got
+// slower with it: its 320 x 256 O / FC2 calls 6.21 -> 6.62 ms per step at 2 or 3 (DA-v2's 384 x 192
+// equal), so it keeps the compiler's schedule.  Variants: tools/build_variant.sh.
+#ifndef I2PC_GEMM_APF
+#define I2PC_GEMM_APF 2
+#endif
+#ifndef I2PC_GEMM_APF_TILE
+#define I2PC_GEMM_APF_TILE 0
+#endif
+
 __device__ __attribute__((aligned(16))) uint8_t g_zero[1024];  // conv zero padding / absent-bias source
 #ifdef I2PC_STAMPS
 // diagnostic build only: per-block s_memtime stamps (start, after prologue, after K loop, end)
@@ -571,6 +585,30 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
         const int row = wn * TN + j * 16 + frow;
         wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * ROWB + ((lchunk ^ swz(row)) << 4));
       }
+#if I2PC_GEMM_APF_TILE > 0
+      // A fragments I2PC_GEMM_APF_TILE m-subtiles ahead of their MFMAs (as the persistent engine)
+      constexpr int APF = I2PC_GEMM_APF_TILE < RM ? I2PC_GEMM_APF_TILE : RM;
+      bf16x8 afr[RM];
+      auto a_read = [&](int i) {
+        const int row = wm * TM + i * 16 + frow;
+        afr[i] = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((lchunk ^ swz(row)) << 4));
+      };
+#pragma unroll
+      for (int i = 0; i < APF; ++i) a_read(i);
+      __builtin_amdgcn_sched_group_barrier(0x100, RN + APF, 0);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        if (i + APF < RM) {
+          a_read(i + APF);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        bf16x8 af = afr[i];
+        if (RELU_A) af = relu8(af);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, RN, 0);
+      }
+#else
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int row = wm * TM + i * 16 + frow;
@@ -579,6 +617,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
 #pragma unroll
         for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
       }
+#endif
     }
     __syncthreads();
   }
@@ -1268,6 +1307,32 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
             const int row = wn * (BN / 4) + j * 16 + frow;
             wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * ROWB + ((lchunk ^ (row & 7)) << 4));
           }
+#if I2PC_GEMM_APF > 0
+          // A fragments read APF m-subtiles ahead of their MFMAs, the order pinned by scheduling groups
+          // (left to itself the compiler reused one fragment register: read -> lgkmcnt(0) -> 4 MFMAs per
+          // m-subtile, each LDS latency exposed to the matrix pipe)
+          constexpr int APF = I2PC_GEMM_APF < RM ? I2PC_GEMM_APF : RM;
+          bf16x8 afr[RM];
+          auto a_read = [&](int i) {
+            const int row = wm * TM + i * 16 + frow;
+            afr[i] = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((lchunk ^ (row & 7)) << 4));
+          };
+#pragma unroll
+          for (int i = 0; i < APF; ++i) a_read(i);
+          __builtin_amdgcn_sched_group_barrier(0x100, RN + APF, 0);
+#pragma unroll
+          for (int i = 0; i < RM; ++i) {
+            if (i + APF < RM) {
+              a_read(i + APF);
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            bf16x8 af = afr[i];
+            if (RELU_A) af = relu8(af);
+#pragma unroll
+            for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, RN, 0);
+          }
+#else
 #pragma unroll
           for (int i = 0; i < RM; ++i) {
             const int row = wm * TM + i * 16 + frow;
@@ -1276,6 +1341,7 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
 #pragma unroll
             for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
           }
+#endif
         }
       } else {
         const uint32_t* sS = reinterpret_cast<const uint32_t*>(sW + W_BYTES);
