@@ -42,7 +42,9 @@ constexpr int BK = 64;
 // to the matrix pipe).  r05, in one box: persistent LN-fold QKV / FC1 7.23 -> 6.89 ms per C2 step
 // with 2 (3: equal), step 21.77 -> 21.34 ms, bit-identical.  The tile kernel (I2PC_GEMM_APF_TILE) got
 // slower with it: its 320 x 256 O / FC2 calls 6.21 -> 6.62 ms per step at 2 or 3 (DA-v2's 384 x 192
-// equal), so it keeps the compiler's schedule.  Variants: tools/build_variant.sh.
+// equal), so it keeps the compiler's schedule.  The fp8 path of the persistent engine with one m-subtile
+// of look-ahead (two would spill) measured equal on C5 (26.40 vs 26.37 ms per step), not kept.
+// Variants: tools/build_variant.sh.
 #ifndef I2PC_GEMM_APF
 #define I2PC_GEMM_APF 2
 #endif
