@@ -197,83 +197,6 @@ const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
   }
 }
 
-// The same resize with a work item of XO consecutive output pixels of one row (one 8-channel chunk):
-// the row's source rows and weights and the index divisions are shared by the XO outputs, and their
-// 5 * XO loads (four taps and the add operand each) are all in flight before the arithmetic.
-// Output values are those of k_resize (the same per-output operations).
-template <int XO>
-__global__ __launch_bounds__(256) void k_resize_x(const bf16_t* __restrict__ x, int B, int h, int w, int c, int H, int W,
-                                                  int align, const bf16_t* __restrict__ add, bf16_t* __restrict__ y) {
-  const uint32_t cv = (uint32_t)(c / 8);
-  const uint32_t WG = (uint32_t)((W + XO - 1) / XO);
-  const uint32_t total = (uint32_t)B * (uint32_t)H * WG * cv;
-  float sh, sw;
-  if (align) {
-    sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
-    sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
-  } else {
-    sh = (float)h / (float)H;
-    sw = (float)w / (float)W;
-  }
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  auto g2 = [](uint32_t u) { return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; };
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int ch = (int)(i % cv);
-    uint32_t pix = i / cv;
-    const int ox0 = (int)(pix % WG) * XO;
-    pix /= WG;
-    const int oy = (int)(pix % (uint32_t)H);
-    const int b = (int)(pix / (uint32_t)H);
-    const float fy = align ? sh * oy : fmaxf(sh * (oy + 0.5f) - 0.5f, 0.f);
-    const int y0 = (int)fy;
-    const int y1 = y0 + (y0 < h - 1 ? 1 : 0);
-    const float ly1 = fy - y0, ly0 = 1.f - ly1;
-    const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
-    const bf16_t* r0 = base + (int64_t)y0 * w * c;
-    const bf16_t* r1 = base + (int64_t)y1 * w * c;
-    uint4 a00[XO], a01[XO], a10[XO], a11[XO], av[XO];
-    float lx0[XO], lx1[XO];
-#pragma unroll
-    for (int k = 0; k < XO; ++k) {
-      const int ox = min(ox0 + k, W - 1);    // (past the row end: recomputed, not stored)
-      const float fx = align ? sw * ox : fmaxf(sw * (ox + 0.5f) - 0.5f, 0.f);
-      const int x0 = (int)fx;
-      const int x1 = x0 + (x0 < w - 1 ? 1 : 0);
-      lx1[k] = fx - x0;
-      lx0[k] = 1.f - lx1[k];
-      a00[k] = *reinterpret_cast<const uint4*>(r0 + (int64_t)x0 * c);
-      a01[k] = *reinterpret_cast<const uint4*>(r0 + (int64_t)x1 * c);
-      a10[k] = *reinterpret_cast<const uint4*>(r1 + (int64_t)x0 * c);
-      a11[k] = *reinterpret_cast<const uint4*>(r1 + (int64_t)x1 * c);
-      av[k] = add ? *reinterpret_cast<const uint4*>(add + ((((int64_t)b * H + oy) * W + ox) * cv + ch) * 8)
-                  : make_uint4(0, 0, 0, 0);
-    }
-    const f32x2 vy0 = {ly0, ly0}, vy1 = {ly1, ly1};
-#pragma unroll
-    for (int k = 0; k < XO; ++k) {
-      if (ox0 + k >= W) break;
-      const uint32_t* p00 = reinterpret_cast<const uint32_t*>(&a00[k]);
-      const uint32_t* p01 = reinterpret_cast<const uint32_t*>(&a01[k]);
-      const uint32_t* p10 = reinterpret_cast<const uint32_t*>(&a10[k]);
-      const uint32_t* p11 = reinterpret_cast<const uint32_t*>(&a11[k]);
-      const uint32_t* pa = reinterpret_cast<const uint32_t*>(&av[k]);
-      const f32x2 vx0 = {lx0[k], lx0[k]}, vx1 = {lx1[k], lx1[k]};
-      uint4 out;
-      uint32_t* po = reinterpret_cast<uint32_t*>(&out);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x2 t0 = __builtin_elementwise_fma(vx1, g2(p01[q]), vx0 * g2(p00[q]));
-        const f32x2 t1 = __builtin_elementwise_fma(vx1, g2(p11[q]), vx0 * g2(p10[q]));
-        f32x2 r = __builtin_elementwise_fma(vy1, t1, vy0 * t0);
-        if (add) r += g2(pa[q]);
-        po[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
-      }
-      *reinterpret_cast<uint4*>(y + ((((int64_t)b * H + oy) * W + ox0 + k) * cv + ch) * 8) = out;
-    }
-  }
-}
-
 __global__ void k_cls_pos(const float* cls, const float* pos0, int B, int T, int D, float* x) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * D) return;
@@ -448,13 +371,10 @@ using namespace i2pc::misc;
 
 static thread_local int g_ln2 = 1;   // "ln_f2": the float2 row kernel for dim 384
 static thread_local int g_ln_apply_gs = 0;   // "ln_apply_gs": DIAGNOSTIC, the r04 grid-stride ln_apply
-// "resize_xo": 1 = k_resize_x<4> (four outputs of a row per work item; default), 0 = k_resize
-static thread_local int g_resize_xo = [] { const char* e = getenv("I2PC_RESIZE_XO"); return e ? atoi(e) : 1; }();
 
 bool i2pc_misc_tune(const char* name, int value) {
   if (std::strcmp(name, "ln_f2") == 0) { g_ln2 = value; return true; }
   if (std::strcmp(name, "ln_apply_gs") == 0) { g_ln_apply_gs = value; return true; }
-  if (std::strcmp(name, "resize_xo") == 0) { g_resize_xo = value; return true; }
   return false;
 }
 
@@ -555,14 +475,6 @@ extern "C" int i2pc_resize_bilinear(const void* x, int batch, int h, int w, int 
   I2PC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && out_h > 0 && out_w > 0,
                "resize_bilinear: bad shape (c %% 8 == 0)");
   const int64_t work = (int64_t)batch * out_h * out_w * (c / 8);
-  constexpr int XO = 4;
-  const int64_t work4 = (int64_t)batch * out_h * ((out_w + XO - 1) / XO) * (c / 8);
-  if (g_resize_xo && work4 + (int64_t)grid_for(work4) * 256 < ((int64_t)1 << 31)) {
-    hipLaunchKernelGGL(k_resize_x<XO>, dim3(grid_for(work4)), dim3(256), 0, as_stream(stream),
-                       static_cast<const bf16_t*>(x), batch, h, w, c, out_h, out_w, align_corners ? 1 : 0,
-                       static_cast<const bf16_t*>(add), static_cast<bf16_t*>(y));
-    return check_launch("resize_bilinear");
-  }
   // 32-bit indices when the flat index and its grid-stride successor stay below 2^31
   if (work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 31))
     hipLaunchKernelGGL(k_resize<uint32_t>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),

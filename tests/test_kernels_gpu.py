@@ -264,26 +264,6 @@ def test_upsample2x_align_corners(dev, B, H, W, C):
     _close(got, ref)
 
 
-@pytest.mark.parametrize("B,h,w,H,W,C,align,add", [(2, 12, 12, 24, 24, 256, 1, True), (1, 5, 7, 10, 14, 64, 1, False),
-                                                   (2, 24, 24, 48, 48, 256, 1, True), (1, 37, 41, 103, 77, 32, 0, True),
-                                                   (3, 9, 10, 9, 13, 16, 0, False)])
-def test_resize_xo_bit_identical(dev, B, h, w, H, W, C, align, add):
-    """k_resize_x<4> (four outputs of a row per work item, ragged row ends included) equals k_resize
-    bit for bit, with and without the fused add."""
-    ops = _ops()
-    g = torch.Generator(device="cpu").manual_seed(H * W + C)
-    x = _bf(torch.randn(B, h, w, C, generator=g)).to(dev)
-    a = _bf(torch.randn(B, H, W, C, generator=g)).to(dev) if add else None
-    outs = []
-    try:
-        for xo in (0, 1):
-            ops.set_tuning("resize_xo", xo)
-            outs.append(ops.resize_bilinear(x, H, W, align_corners=bool(align), add=a).clone())
-    finally:
-        ops.set_tuning("resize_xo", 1)
-    assert torch.equal(outs[0], outs[1])
-
-
 def test_head_out(dev):
     ops = _ops()
     g = torch.Generator(device="cpu").manual_seed(3)
