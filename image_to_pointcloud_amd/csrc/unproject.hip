@@ -82,6 +82,7 @@ constexpr int kMaxBandRanks = 256;
 // k_sel_slow (non-finite map); PH_DONE: p2 / p98 / mode final.
 // PH_SCR1 / PH_SCR2: the selection from scratch between its grid-wide radix levels (k_sel_slow ->
 // k_scratch<1> -> k_scratch<2>)
+constexpr uint32_t kLevelScratch = 16;   // SelState.level of an image selected from scratch (k_sel_slow)
 enum Phase : uint32_t { PH_INIT = 0, PH_SEL = 1, PH_SLOW = 2, PH_SCR1 = 3, PH_SCR2 = 4, PH_DONE = 5 };
 enum SlotMode : uint32_t { SM_HIST = 0, SM_COMPACT = 1 };
 constexpr uint32_t kNoSlot = 0xffffffffu;
@@ -1395,7 +1396,8 @@ __device__ void cand_select(const uint32_t* keys, uint32_t c, uint32_t lo, uint3
 __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t* mhist, uint32_t cap, int B,
                                                    int enable, int m, int nch) {
   __shared__ __attribute__((aligned(16))) uint32_t mh[kBins];
-  __shared__ uint32_t wsum[kBlock / 64], wb[6], tot;
+  __shared__ uint32_t wsum[kBlock / 64], wb[6], tot, wtot[3];
+  __shared__ double wlim[3];
   const int b = blockIdx.x;
   if (b >= B) return;
   SelState* S = st + b;
@@ -1457,10 +1459,13 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
     for (int i = 0; i < per; ++i) {
       const int bn = threadIdx.x * per + i;
       const double c1 = c + mh[bn];
-      // a bin that alone outgrows the window (a spike such as the zero floor) stays out of it
-      // unless it holds the rank itself (then no window can help; the levels take over)
-      const bool fits = (double)mh[bn] <= 2.0 * hk || (c <= r && r < c1);
-      if (c1 > r - hk && c <= r + hk && fits) { atomicMin(&wb[2 * k], (uint32_t)bn); atomicMax(&wb[2 * k + 1], (uint32_t)bn); }
+      // every bin overlapping the rank's uncertainty interval; one that alone outgrows the window (a
+      // spike such as the zero floor) can only sit at an end of it, where it is flagged below and
+      // counted with its min / max key.  (r04 left such a bin out unless the SAMPLE's rank fell in
+      // it: C2 image 5, whose ReLU floor holds 2.0x % of the pixels, had the sample's p2 rank just
+      // above the floor and the image's just inside it -- a rank outside every window, so the
+      // selection from scratch on every call, +0.64 ms per C2 step.)
+      if (c1 > r - hk && c <= r + hk) { atomicMin(&wb[2 * k], (uint32_t)bn); atomicMax(&wb[2 * k + 1], (uint32_t)bn); }
       c = c1;
     }
   }
@@ -1485,20 +1490,52 @@ __global__ __launch_bounds__(kBlock) void k_window(SelState* st, const uint32_t*
       }
     }
     for (int i = 0; i < 2 * nw; ++i) S->wbin[i] = w[i];
+    S->nwin = (uint32_t)nw;
+    for (int i = 0; i < 2 * nw; ++i) wb[i] = w[i];
+    for (int k = 0; k < nw; ++k) wlim[k] = lim[k];
+    for (int k = 0; k < 3; ++k) wtot[k] = 0;
+    tot = (uint32_t)nw;
+  }
+  __syncthreads();
+  // each window's sample count (the bins of a thread, added per window)
+  for (int k = 0; k < (int)tot; ++k) {
+    uint32_t part = 0;
+    for (int i = 0; i < per; ++i) {
+      const uint32_t bn = (uint32_t)(threadIdx.x * per + i);
+      if (bn >= wb[2 * k] && bn <= wb[2 * k + 1]) part += mh[bn];
+    }
+    part = wave_sum_u32(part);
+    if ((threadIdx.x & 63) == 0 && part) atomicAdd(&wtot[k], part);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
     // end bins expected to outgrow the window budget (the zero floor of a ReLU head, a saturated
     // maximum): counted with their min / max key by k_sweep_w instead of compacted; a window
     // holds such a bin only at an end (a bin larger than the window cannot have neighbours on
-    // both sides within the rank budget)
-    for (int k = 0; k < nw; ++k) {
-      const uint32_t lo = w[2 * k], hi = w[2 * k + 1];
+    // both sides within the rank budget).  Beyond a bin larger than the budget alone (lim: twice
+    // the half-width, at most 0.8 of a candidate list), a window whose compacted part would still
+    // exceed the budget has its larger remaining end bin split off too, when that bin holds at
+    // least a quarter of the budget: r05, a DPT-Large map whose ReLU zero floor (a bin holding the
+    // p2 rank itself, so kept in the window) was just under the budget while its neighbours brought
+    // the window past the list capacity -- the list overflowed and the image went to the selection
+    // from scratch every call (+0.64 ms per C2 step).
+    for (int k = 0; k < (int)tot; ++k) {
+      const uint32_t lo = wb[2 * k], hi = wb[2 * k + 1];
+      const double lk = wlim[k];
       uint32_t f = 0;
-      if ((double)mh[lo] > lim[k]) f |= 1u;
-      if (hi > lo && (double)mh[hi] > lim[k]) f |= 2u;
+      if ((double)mh[lo] > lk) f |= 1u;
+      if (hi > lo && (double)mh[hi] > lk) f |= 2u;
+      double rest = (double)wtot[k] - ((f & 1u) ? (double)mh[lo] : 0.0) - ((f & 2u) ? (double)mh[hi] : 0.0);
+      for (int it = 0; it < 2 && rest > lk && hi > lo; ++it) {
+        const double cl = (f & 1u) ? -1.0 : (double)mh[lo], ch = (f & 2u) ? -1.0 : (double)mh[hi];
+        const bool take_lo = cl >= ch;
+        const double c = take_lo ? cl : ch;
+        if (c < 0.25 * lk) break;
+        f |= take_lo ? 1u : 2u;
+        rest -= c;
+      }
       S->wspike[k] = f;
     }
-    S->nwin = (uint32_t)nw;
-    for (int i = 0; i < 2 * nw; ++i) wb[i] = w[i];
-    tot = (uint32_t)nw;
   }
   __syncthreads();
   // the windows as values for k_sweep_w: the first / last finite key of the window's bins, and of
@@ -2163,6 +2200,7 @@ __global__ __launch_bounds__(kSlowBlock) void k_sel_slow(Geo g, SelState* st, in
   }
   // from scratch, level 0 resolved by this (last) workgroup
   if (threadIdx.x == 0) {
+    s.level = kLevelScratch;          // diagnostics: this image's percentiles came from the fallback
     s.nan_count = atomicAdd(&sl[3], 0u);
     s.nonfinite_count = atomicAdd(&sl[4], 0u);
     s.ninf_neg = atomicAdd(&sl[5], 0u);

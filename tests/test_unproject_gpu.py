@@ -355,6 +355,30 @@ def test_selection_with_a_spike_of_equal_values(zero_frac, shape):
     assert _same_bits(whole.xyz[0].cpu().numpy(), ep), _first_diff(whole.xyz[0].cpu().numpy(), ep)
 
 
+def test_relu_floor_at_p2_stays_on_the_window_path():
+    """Image 5 of the C2 bench batch (DPT-Large, seeded weights; 3 % exact zeros of the head's ReLU
+    floor at model resolution, tests/golden/c2_relu_floor_depth.npz): the p2 rank falls on the zero
+    floor, whose level-0 bin was just under the window budget, so it stayed in the window and the
+    window's candidate list overflowed -- the image went to the selection from scratch on every call
+    (r05, +0.64 ms per C2 step).  k_window now splits the bin off as a spike: the selection must
+    resolve without the fallback (SelState.level != 16) and the points stay bit-exact vs the oracle."""
+    import os
+    from image_to_pointcloud_amd import geometry as G
+    dep = np.load(os.path.join(os.path.dirname(__file__), "golden", "c2_relu_floor_depth.npz"))["depth"]
+    dev = torch.device("cuda")
+    img = _rgb(1024, 1024, 105)
+    ws = torch.zeros(G.workspace_bytes(1, 1024, 1024, False), dtype=torch.uint8, device=dev)
+    pb = G.unproject_batch(torch.from_numpy(dep).to(dev)[None], torch.from_numpy(img).to(dev)[None], density="high",
+                           workspace=ws)
+    torch.cuda.synchronize()
+    state = ws[:624].cpu().numpy().view(np.uint32)
+    level = int(state[344 // 4 - 1])      # SelState.level: the uint32 before p2 (offset 344)
+    assert level != 16, "the ReLU-floor map went to the selection from scratch"
+    ep, ec = ref.depth_to_point_cloud(img, dep, density="high", loop=False)
+    assert _same_bits(pb.xyz[0].cpu().numpy(), ep), _first_diff(pb.xyz[0].cpu().numpy(), ep)
+    assert _same_bits(pb.rgb[0].cpu().numpy().astype(np.float32), ec)
+
+
 @pytest.mark.parametrize("density", ["high", "low"])
 def test_equirect_projection_matches_oracle_and_bands(density):
     """Equirectangular mode (C4 panoramas; not in the reference, so parity is against the

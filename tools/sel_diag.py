@@ -22,7 +22,9 @@ SEL = np.dtype([("phase", u4), ("n", u4), ("nan_count", u4), ("nonfinite_count",
                 ("bbox_key", u4, 6), ("pad3", u4, 2), ("rden64", np.float64), ("pad4", np.float64),
                 ("wspike", u4, 3), ("wbelow", u4, 3), ("wcntF", u4, 3), ("wminF", u4, 3), ("wmaxF", u4, 3),
                 ("wcntL", u4, 3), ("wminL", u4, 3), ("wmaxL", u4, 3), ("wvlo", np.float32, 3),
-                ("wvhi", np.float32, 3), ("wvF", np.float32, 3), ("wvL", np.float32, 3), ("twin", u4, 10)])
+                ("wvhi", np.float32, 3), ("wvF", np.float32, 3), ("wvL", np.float32, 3), ("twin", u4, 10),
+                ("pad5", u4, 2)])   # alignas(16): sizeof(SelState) == 624 (unproject.hip static_assert)
+assert SEL.itemsize == 624
 
 
 def show(tag, ws):
