@@ -468,6 +468,13 @@ def main():
                     "achieved": round(geo_bytes / geo_t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(geo_bytes / geo_t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                     "ms": round(geo_t * 1e3, 3), "bytes_per_step": geo_bytes}
+        # images whose percentiles the last call took from the selection from scratch (the exact
+        # fallback, ~0.2-0.6 ms; SelState.level == 16 in the pipeline's workspace, unproject.hip)
+        try:
+            st = pipe._ws[:624 * B].view(torch.int32).view(B, 156).cpu()
+            roof_geo["selection_from_scratch"] = int((st[:, 85] == 16).sum())
+        except Exception:   # (diagnostic only)
+            pass
         rooflines = {"unproject_stage": roof_geo}
         if unp_t:
             a_unp = geo_bytes / unp_t / 1e9
