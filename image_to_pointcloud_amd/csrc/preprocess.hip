@@ -316,6 +316,11 @@ extern "C" int i2pc_preprocess_plan_create(int in_h, int in_w, int out_h, int ou
     max_rows = std::max(max_rows, hi - lo);
   }
   I2PC_REQUIRE(max_rows * band_row <= kLdsBudget, "LDS band too large (%d rows x %d B)", max_rows, band_row);
+  {
+    const size_t lds = align_up((size_t)max_rows * band_row, 16) +
+                       align_up((size_t)std::max(1, kStageBytes / max_wb) * max_wb, 16);
+    I2PC_REQUIRE(lds + 3 * 256 * 4 <= 160 * 1024, "preprocess plan needs %zu B of LDS", lds);
+  }
   // every check is done: allocate.  One device buffer:
   // hx_min | hx_cnt | hx_k | vy_min | vy_cnt | vy_k | tile_lo | tile_n | col_a0 | col_wb
   // output table: (float)((double)u / 255 in float64) then (f - mean) / std in float32 (the device formula
@@ -376,8 +381,9 @@ extern "C" int i2pc_preprocess(const i2pc_preprocess_plan* plan, const uint8_t* 
   if (P.lds_bytes > 64 * 1024) {
     static bool attr = false;
     if (!attr) {
+      // (the kernel's static LDS -- the 3 x 256 output table -- counts against the 160 KB too)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_preprocess), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
+                                160 * 1024 - 3 * 256 * 4);
       attr = true;
     }
   }
