@@ -3,6 +3,7 @@
 // All are HBM-bound: 16-byte vector loads/stores, one wave per row where a row
 // reduction is needed.
 #include "common.h"
+#include "mx.h"
 
 #include <cstdlib>
 
@@ -194,6 +195,74 @@ const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
       po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
     }
     *reinterpret_cast<uint4*>(y + (int64_t)i * 8) = out;
+  }
+}
+
+// 2x bilinear upsample (align_corners, as k_resize) written as MX fp8 rows -- i2pc_gemm_fp8's operand:
+// e4m3 bytes [pixel][c] + one E8M0 scale byte per 32 channels (scale dwords [pixel][ldys / 4]).  One
+// thread per (output pixel, 32-channel block): the four taps' 64-B runs, the same bf16 rounding of each
+// value as k_resize, then the block quantised exactly as k_quant_rows quantises a bf16 row (so the bytes
+// equal quant_fp8(upsample2x(x))) and stored as 32 B + 1 scale byte; the bf16 map is never written.
+__global__ __launch_bounds__(256) void k_upsample2x_fp8(const bf16_t* __restrict__ x, int B, int h, int w, int c,
+                                                        const bf16_t* __restrict__ add, uint8_t* __restrict__ y8,
+                                                        int64_t ldy8, uint8_t* __restrict__ ys, int64_t ldys) {
+  const int H = 2 * h, W = 2 * w;
+  const uint32_t nb = (uint32_t)(c / 32);
+  const uint32_t total = (uint32_t)B * (uint32_t)H * (uint32_t)W * nb;
+  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  auto g2 = [](uint32_t u) { return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; };
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int blk = (int)(i % nb);
+    uint32_t pix = i / nb;
+    const int ox = (int)(pix % (uint32_t)W);
+    const uint32_t t = pix / (uint32_t)W;
+    const int oy = (int)(t % (uint32_t)H);
+    const int b = (int)(t / (uint32_t)H);
+    const float fy = sh * oy, fx = sw * ox;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly1 = fy - y0, lx1 = fx - x0;
+    const f32x2 vx0 = {1.f - lx1, 1.f - lx1}, vx1 = {lx1, lx1}, vy0 = {1.f - ly1, 1.f - ly1}, vy1 = {ly1, ly1};
+    const bf16_t* base = x + (int64_t)b * h * w * c + blk * 32;
+    const uint4* p00 = reinterpret_cast<const uint4*>(base + ((int64_t)y0 * w + x0) * c);
+    const uint4* p01 = reinterpret_cast<const uint4*>(base + ((int64_t)y0 * w + x1) * c);
+    const uint4* p10 = reinterpret_cast<const uint4*>(base + ((int64_t)y1 * w + x0) * c);
+    const uint4* p11 = reinterpret_cast<const uint4*>(base + ((int64_t)y1 * w + x1) * c);
+    const uint4* pa = add ? reinterpret_cast<const uint4*>(add + (int64_t)pix * c + blk * 32) : nullptr;
+    float v[32];
+    float am = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 a00 = p00[q], a01 = p01[q], a10 = p10[q], a11 = p11[q];
+      const uint4 aa = pa ? pa[q] : make_uint4(0, 0, 0, 0);
+      const uint32_t w00[4] = {a00.x, a00.y, a00.z, a00.w}, w01[4] = {a01.x, a01.y, a01.z, a01.w};
+      const uint32_t w10[4] = {a10.x, a10.y, a10.z, a10.w}, w11[4] = {a11.x, a11.y, a11.z, a11.w};
+      const uint32_t wa[4] = {aa.x, aa.y, aa.z, aa.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x2 t0 = __builtin_elementwise_fma(vx1, g2(w01[k]), vx0 * g2(w00[k]));
+        const f32x2 t1 = __builtin_elementwise_fma(vx1, g2(w11[k]), vx0 * g2(w10[k]));
+        f32x2 r = __builtin_elementwise_fma(vy1, t1, vy0 * t0);
+        if (pa) r += g2(wa[k]);
+        const f32x2 rb = g2(__builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2)));   // k_resize's bf16 value
+        v[8 * q + 2 * k] = rb.x;
+        v[8 * q + 2 * k + 1] = rb.y;
+        am = fmaxf(am, fmaxf(fabsf(rb.x), fabsf(rb.y)));
+      }
+    }
+    const int ex = ::i2pc::mx::mx_exponent(am);
+    const float mul = ::i2pc::mx::exp2i(-ex);
+    uint32_t d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      d[q] = ::i2pc::mx::pack_e4m3(v[4 * q] * mul, v[4 * q + 1] * mul, v[4 * q + 2] * mul, v[4 * q + 3] * mul);
+    uint4* out = reinterpret_cast<uint4*>(y8 + (int64_t)pix * ldy8 + blk * 32);
+    out[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    out[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    ys[(int64_t)pix * ldys + blk] = (uint8_t)(ex + 127);
   }
 }
 
@@ -489,6 +558,21 @@ extern "C" int i2pc_resize_bilinear(const void* x, int batch, int h, int w, int 
 
 extern "C" int i2pc_upsample2x(const void* x, int batch, int h, int w, int c, const void* add, void* y, void* stream) {
   return i2pc_resize_bilinear(x, batch, h, w, c, 2 * h, 2 * w, 1, add, y, stream);
+}
+
+extern "C" int i2pc_upsample2x_fp8(const void* x, int batch, int h, int w, int c, const void* add, void* y, int64_t ldy,
+                                   void* y_scale, int64_t ldy_scale, void* stream) {
+  clear_error();
+  I2PC_REQUIRE(x && y && y_scale, "NULL pointer");
+  I2PC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && c % 32 == 0, "upsample2x_fp8: bad shape (c %% 32 == 0)");
+  I2PC_REQUIRE(ldy % 16 == 0 && ldy >= c && ldy_scale * 128 >= c, "upsample2x_fp8: ldy %% 16, ldy >= c, ldy_scale >= c/128");
+  const int H = 2 * h, W = 2 * w;
+  const int64_t work = (int64_t)batch * H * W * (c / 32);
+  I2PC_REQUIRE(work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 32), "upsample2x_fp8: map too large for 32-bit indexing");
+  hipLaunchKernelGGL(k_upsample2x_fp8, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                     static_cast<const bf16_t*>(x), batch, h, w, c, static_cast<const bf16_t*>(add),
+                     static_cast<uint8_t*>(y), ldy, static_cast<uint8_t*>(y_scale), ldy_scale * 4);
+  return check_launch("upsample2x_fp8");
 }
 
 extern "C" int i2pc_cls_pos(const float* cls, const float* pos0, int batch, int tokens, int dim, float* x, void* stream) {

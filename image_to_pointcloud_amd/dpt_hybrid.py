@@ -398,9 +398,10 @@ class DPTHybridModel(DPTDepthModel):
         feats += [self._reassemble_vit(j, buf, B) for j in (2, 3)]
         hidden = None
         for j, feat in enumerate(reversed(feats)):
-            hidden = self._fuse(self.fusion[j], feat, hidden)
+            # the last stage's output feeds only the head: its upsample writes the head's fp8 operand
+            hidden = self._fuse(self.fusion[j], feat, hidden, head_fp8=j == len(feats) - 1 and f8("head"))
         if f8("head"):
-            t = ops.conv2d_fp8(ops.quant_fp8(hidden), self.w_h0, bias=self.b_h0)
+            t = ops.conv2d_fp8(hidden if isinstance(hidden, ops.Fp8) else ops.quant_fp8(hidden), self.w_h0, bias=self.b_h0)
         else:
             t = ops.conv2d(hidden, self.w_h0, bias=self.b_h0)
         return ops.head_upconv(t, 2 * t.shape[1], 2 * t.shape[2], self.w_h2, self.b_h2, self.w_h4, self.b_h4)
@@ -469,7 +470,7 @@ class DPTHybridModel(DPTDepthModel):
                 proj = ops.quant_fp8(proj)
         return ops.conv2d_fp8(proj, st["w_neck"]) if f8n else ops.conv2d(proj, st["w_neck"])
 
-    def _fuse(self, fl, feat, hidden):
+    def _fuse(self, fl, feat, hidden, head_fp8=False):
         if not self._f8("fusion"):
             return super()._fuse(fl, feat, hidden)
         if hidden is None:
@@ -486,4 +487,4 @@ class DPTHybridModel(DPTDepthModel):
         h2 = ops.conv2d_fp8(t, fl["residual_layer2.convolution2.w"], bias=fl["residual_layer2.convolution2.b"], res=h)
         B, H, W, F = h2.shape
         p = ops.linear(h2.view(B * H * W, F), fl["w_proj"], bias=fl["b_proj"]).view(B, H, W, F)
-        return ops.upsample2x(p)
+        return ops.upsample2x(p, out_fp8=head_fp8 and F % 128 == 0)

@@ -64,6 +64,8 @@ _lib.register("i2pc_attention_fp8", ctypes.c_int, [c_void_p, ctypes.c_int, ctype
                                                    c_void_p, c_int64, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_upsample2x", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, c_void_p, c_void_p, c_void_p])
+_lib.register("i2pc_upsample2x_fp8", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p])
 _lib.register("i2pc_resize_bilinear", ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                      c_void_p, c_void_p, c_void_p])
@@ -491,10 +493,19 @@ def fold_q_scale(w_qkv, b_qkv, scale):
     return w, b
 
 
-def upsample2x(x, add=None, out=None):
+def upsample2x(x, add=None, out=None, out_fp8=False):
+    """Bilinear 2x (align_corners) of NHWC bf16 x (+ add); out_fp8: returned as Fp8 rows [B, 2H, 2W, C]
+    (i2pc_upsample2x_fp8, the bytes quant_fp8 of the bf16 result would give)."""
     torch = _torch()
     _check(x, torch.bfloat16, "x")
     B, H, W, C = x.shape
+    if out_fp8:
+        if out is None:
+            out = empty_fp8((B, 2 * H, 2 * W, C), x.device)
+        with _Timed("k_resize_fp8", 0.0, 2.0 * B * H * W * C + 4.0 * B * H * W * C * (1 + 1 / 32 + (2 if add is not None else 0))):
+            _lib.call("i2pc_upsample2x_fp8", _p(x), B, H, W, C, _p(add), _p(out.data), out.data.shape[-1],
+                      _p(out.scale), out.scale.shape[-1] // 4, _stream())
+        return out
     if out is None:
         out = torch.empty((B, 2 * H, 2 * W, C), dtype=torch.bfloat16, device=x.device)
     with _Timed("k_resize", 0.0, 2.0 * B * H * W * C * (1 + 4 + (4 if add is not None else 0))):

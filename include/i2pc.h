@@ -459,6 +459,12 @@ int i2pc_attention_q2_fp8(const void* qkv, int batch, int tokens, int heads, voi
 /* Bilinear 2x upsample, align_corners = True, NHWC bf16 (nn.functional.interpolate,
  * modeling_dpt.py:504-506, 698), optional + add (bf16, output shape). */
 int i2pc_upsample2x(const void* x, int batch, int h, int w, int c, const void* add, void* y, void* stream);
+/* The same upsample written as the MX fp8 operand of i2pc_gemm_fp8 (e4m3 [pixels][ldy] bytes + E8M0 scale
+ * dwords [pixels][ldy_scale]): the bytes equal i2pc_quant_fp8 of i2pc_upsample2x's bf16 output, without
+ * that bf16 map (DPT-Hybrid fp8: the last fusion stage's output feeds only the head's first conv).
+ * c % 32 == 0, ldy % 16 == 0. */
+int i2pc_upsample2x_fp8(const void* x, int batch, int h, int w, int c, const void* add, void* y, int64_t ldy,
+                        void* y_scale, int64_t ldy_scale, void* stream);
 
 /* General bilinear resize of an NHWC bf16 map to out_h x out_w with torch's
  * upsample_bilinear2d index rules (align_corners 1: the DPT/Depth-Anything fusion and

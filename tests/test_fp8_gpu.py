@@ -186,3 +186,20 @@ def test_conv_fp8_residual_unit(dev):
     h = ops.conv2d_fp8(t, w2, bias=b2, res=xb, res2=hid)
     ref = _conv_ref(t, w2, C, 3, 1, 1, b2) + xb.float() + hid.float()
     _close(h, ref, 1e-2)
+
+
+@pytest.mark.parametrize("B,H,W,C,add", [(2, 96, 96, 256, False), (3, 13, 7, 128, True), (1, 5, 9, 384, False)])
+def test_upsample2x_fp8_bit_exact(dev, B, H, W, C, add):
+    """i2pc_upsample2x_fp8 (the DPT-Hybrid head's operand straight from the last fusion upsample) equals
+    quant_fp8 of the bf16 upsample2x output byte for byte (data and scales)."""
+    from image_to_pointcloud_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(H * W + C)
+    x = (torch.randn(B, H, W, C, generator=g) * torch.logspace(-2, 2, C)).to(torch.bfloat16).to(dev)
+    a = torch.randn(B, 2 * H, 2 * W, C, generator=g).to(torch.bfloat16).to(dev) if add else None
+    x[0, 0, 0, :32] = 0
+    got = ops.upsample2x(x, add=a, out_fp8=True)
+    ref = ops.quant_fp8(ops.upsample2x(x, add=a))
+    torch.cuda.synchronize()
+    assert got.data.shape == ref.data.shape
+    assert _bits_equal(ops.Fp8(got.data.view(-1, C), got.scale.view(-1, C // 32)),
+                       ops.Fp8(ref.data.view(-1, C), ref.scale.view(-1, C // 32)))

@@ -189,8 +189,11 @@ def test_dpt_large_ln_fold_matches_unfused_forward():
     rel = ((d1 - d0).norm() / d0.norm()).item()
     from test_dpt_gpu import _report
     _report("dpt-large ln-fold vs LN kernels", rel_l2=rel)
-    # two bf16 paths, each ~1e-2 from transformers fp32 (test_dpt_gpu.py) on this random network
-    assert rel <= 2e-2, rel
+    # two bf16 paths, each bounded against transformers fp32 by max(1.5e-2, 1.5 x the torch-bf16 control)
+    # (test_dpt_gpu.py: 1.0-1.7e-2 achieved, control up to 1.7e-2 at 1024^2), so they may differ by up to
+    # the sum; measured 0.0197 (r05, first attention form) and 0.0210 after the split-half attention, whose
+    # own error against fp64 attention did not move (2.3e-3 relative L2 either way, tools/attn_accuracy.py)
+    assert rel <= 3e-2, rel
 
 
 def test_depth_anything_ln_fold_matches_unfused_forward():
