@@ -358,9 +358,8 @@ __global__ __launch_bounds__(256) void k_ln_rowstats(const float2* __restrict__ 
 // (one 16-B load and store), one workgroup row per matrix row.
 __global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, int64_t ldx8, const float2* __restrict__ rs,
                                                   const float4* __restrict__ gamma, const float4* __restrict__ beta,
-                                                  int rows, int d8, uint4* __restrict__ y, int64_t ldy8) {
+                                                  int d8, uint4* __restrict__ y, int64_t ldy8) {
   // one 8-column group per thread: row r = blockIdx.y, group c = blockIdx.x * 256 + threadIdx.x
-  (void)rows;
   const int r = blockIdx.y;
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < d8) {
@@ -481,7 +480,7 @@ extern "C" int i2pc_ln_apply(const void* x, int64_t ldx, const float* rows_stats
     hipLaunchKernelGGL(k_ln_apply, dim3((d8 + 255) / 256, nr), dim3(256), 0, as_stream(stream),
                        static_cast<const uint4*>(x) + (int64_t)r0 * (ldx / 8), ldx / 8,
                        reinterpret_cast<const float2*>(rows_stats) + r0, reinterpret_cast<const float4*>(gamma),
-                       reinterpret_cast<const float4*>(beta), nr, d8, static_cast<uint4*>(y) + (int64_t)r0 * (ldy / 8),
+                       reinterpret_cast<const float4*>(beta), d8, static_cast<uint4*>(y) + (int64_t)r0 * (ldy / 8),
                        ldy / 8);
   }
   return check_launch("ln_apply");
