@@ -217,15 +217,18 @@ def _q2_inputs(B, T, H, mode, seed):
 
 @pytest.mark.parametrize("B,T,H,mode", [(2, 577, 16, "plain"), (2, 577, 16, "spike"), (1, 1370, 6, "spike"),
                                          (2, 130, 12, "large"), (2, 577, 16, "large"), (1, 300, 4, "negative"),
-                                         (3, 1, 4, "large"), (1, 33, 2, "rising"), (1, 37, 6, "plain")])
+                                         (3, 1, 4, "large"), (1, 33, 2, "rising"), (1, 37, 6, "plain"),
+                                         (1, 96, 4, "rising"), (1, 64, 4, "spike"), (2, 160, 8, "large"),
+                                         (1, 95, 3, "negative")])
 def test_attention_q2_threshold_rescale(dev, B, T, H, mode):
     """i2pc_attention_q2 (Q in the exp2 domain, threshold rescale, -m folded into the QK^T
     accumulators) against torch fp32 SDPA of the same bf16 operands (softmax_2(Q K^T) = SDPA with scale
     ln 2), on inputs that drive its full path mid-sequence: spikes (late keys aligned with some
     queries), large scores (x4: the running max moves by far more than 2^8 between tiles), uniformly
     very negative scores (every p far below 1 against tile 0's reference point), and a rising
-    sequence (every 64-key tile raises every row's max).  The raw-Q kernel on the unscaled operands is
-    held to the same bound against its own reference."""
+    sequence (every 64-key tile raises every row's max).  Sequence lengths put the last key tile's valid
+    keys below, at and above the 32-key half the kernel works in (T % 64 = 1, 26, 2, 44, 33, 37, 32, 0,
+    31).  The raw-Q kernel on the unscaled operands is held to the same bound against its own reference."""
     ops = _ops()
     qkv, q2 = _q2_inputs(B, T, H, mode, T * 7 + H)
     qkv, q2 = qkv.to(dev), q2.to(dev)
