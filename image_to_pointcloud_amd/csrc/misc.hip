@@ -198,6 +198,92 @@ const bf16_t* base = x + (int64_t)b * h * w * c + ch * 8;
   }
 }
 
+// k_resize / k_upsample2x_fp8 mapped by output row (r05): a workgroup walks output rows (b, oy), and
+// inside a row each thread keeps one 8-channel chunk (ch = thread % (c / 8), c a power of two) and
+// steps over the pixels -- no per-output index divisions (≈ 20 VALU per value in the flat-index
+// kernels, PMC), one row's vertical taps computed once, and every tap load lane-consecutive (the
+// 32-channel-block form put 8 lanes 64 B apart).  Same arithmetic as k_resize (bit-identical).  F8:
+// the block's four lanes (a quad) share the amax by DPP and write k_quant_rows' bytes.
+template <bool F8>
+__global__ __launch_bounds__(256) void k_resize_rowmap(const bf16_t* __restrict__ x, int B, int h, int w, int c,
+                                                       int lgcv, int H, int W, int align,
+                                                       const bf16_t* __restrict__ add, bf16_t* __restrict__ y,
+                                                       uint8_t* __restrict__ y8, int64_t ldy8,
+                                                       uint8_t* __restrict__ ys, int64_t ldys) {
+  const int cv = 1 << lgcv;
+  const int ch = threadIdx.x & (cv - 1);
+  const int px0 = threadIdx.x >> lgcv, pstep = 256 >> lgcv;
+  float sh, sw;
+  if (align) {
+    sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+    sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  } else {
+    sh = (float)h / (float)H;
+    sw = (float)w / (float)W;
+  }
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  auto g2 = [](uint32_t u) { return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; };
+  for (int row = blockIdx.x; row < B * H; row += gridDim.x) {
+    const int b = row / H, oy = row - (row / H) * H;
+    const float fy = align ? sh * oy : fmaxf(sh * (oy + 0.5f) - 0.5f, 0.f);
+    const int y0 = (int)fy;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0);
+    const float ly1 = fy - y0, ly0 = 1.f - ly1;
+    const f32x2 vy0 = {ly0, ly0}, vy1 = {ly1, ly1};
+    const bf16_t* r0 = x + ((int64_t)b * h + y0) * w * c + ch * 8;
+    const bf16_t* r1 = x + ((int64_t)b * h + y1) * w * c + ch * 8;
+    for (int ox = px0; ox < W; ox += pstep) {
+      const float fx = align ? sw * ox : fmaxf(sw * (ox + 0.5f) - 0.5f, 0.f);
+      const int x0 = (int)fx;
+      const int x1 = x0 + (x0 < w - 1 ? 1 : 0);
+      const float lx1 = fx - x0, lx0 = 1.f - lx1;
+      const f32x2 vx0 = {lx0, lx0}, vx1 = {lx1, lx1};
+      const uint4 a00 = *reinterpret_cast<const uint4*>(r0 + (int64_t)x0 * c);
+      const uint4 a01 = *reinterpret_cast<const uint4*>(r0 + (int64_t)x1 * c);
+      const uint4 a10 = *reinterpret_cast<const uint4*>(r1 + (int64_t)x0 * c);
+      const uint4 a11 = *reinterpret_cast<const uint4*>(r1 + (int64_t)x1 * c);
+      const int64_t o = ((int64_t)row * W + ox) * c + ch * 8;
+      uint4 addv = make_uint4(0, 0, 0, 0);
+      if (add) addv = *reinterpret_cast<const uint4*>(add + o);
+      const uint32_t p00[4] = {a00.x, a00.y, a00.z, a00.w}, p01[4] = {a01.x, a01.y, a01.z, a01.w};
+      const uint32_t p10[4] = {a10.x, a10.y, a10.z, a10.w}, p11[4] = {a11.x, a11.y, a11.z, a11.w};
+      const uint32_t pa[4] = {addv.x, addv.y, addv.z, addv.w};
+      uint32_t po[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x2 t0 = __builtin_elementwise_fma(vx1, g2(p01[k]), vx0 * g2(p00[k]));
+        const f32x2 t1 = __builtin_elementwise_fma(vx1, g2(p11[k]), vx0 * g2(p10[k]));
+        f32x2 r = __builtin_elementwise_fma(vy1, t1, vy0 * t0);
+        if (add) r += g2(pa[k]);
+        po[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+      }
+      if constexpr (!F8) {
+        *reinterpret_cast<uint4*>(y + o) = make_uint4(po[0], po[1], po[2], po[3]);
+      } else {
+        float v[8];
+        float am = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] = __uint_as_float(po[k] << 16);
+          v[2 * k + 1] = __uint_as_float(po[k] & 0xffff0000u);
+          am = fmaxf(am, fmaxf(fabsf(v[2 * k]), fabsf(v[2 * k + 1])));
+        }
+        // the 32-channel block = this quad of lanes (ch & ~3 .. ch | 3): max by quad_perm xor 1, xor 2
+        am = fmaxf(am, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(am), 0xB1, 0xF, 0xF, true)));
+        am = fmaxf(am, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(am), 0x4E, 0xF, 0xF, true)));
+        const int ex = ::i2pc::mx::mx_exponent(am);
+        const float mul = ::i2pc::mx::exp2i(-ex);
+        const int64_t pix = (int64_t)row * W + ox;
+        *reinterpret_cast<uint2*>(y8 + pix * ldy8 + ch * 8) =
+            make_uint2(::i2pc::mx::pack_e4m3(v[0] * mul, v[1] * mul, v[2] * mul, v[3] * mul),
+                       ::i2pc::mx::pack_e4m3(v[4] * mul, v[5] * mul, v[6] * mul, v[7] * mul));
+        if ((ch & 3) == 0) ys[pix * ldys + (ch >> 2)] = (uint8_t)(ex + 127);
+      }
+    }
+  }
+}
+
 // 2x bilinear upsample (align_corners, as k_resize) written as MX fp8 rows -- i2pc_gemm_fp8's operand:
 // e4m3 bytes [pixel][c] + one E8M0 scale byte per 32 channels (scale dwords [pixel][ldys / 4]).  One
 // thread per (output pixel, 32-channel block): the four taps' 64-B runs, the same bf16 rounding of each
@@ -438,11 +524,14 @@ using namespace i2pc;
 using namespace i2pc::misc;
 
 static thread_local int g_ln2 = 1;   // "ln_f2": the float2 row kernel for dim 384
+static thread_local int g_resize_rows = 1;   // "resize_rows": k_resize_rowmap where it applies (0 = the flat kernels)
+static int pow2_log(int v) { return v > 0 && (v & (v - 1)) == 0 ? __builtin_ctz((unsigned)v) : -1; }
 static thread_local int g_ln_apply_gs = 0;   // "ln_apply_gs": DIAGNOSTIC, the r04 grid-stride ln_apply
 
 bool i2pc_misc_tune(const char* name, int value) {
   if (std::strcmp(name, "ln_f2") == 0) { g_ln2 = value; return true; }
   if (std::strcmp(name, "ln_apply_gs") == 0) { g_ln_apply_gs = value; return true; }
+  if (std::strcmp(name, "resize_rows") == 0) { g_resize_rows = value; return true; }
   return false;
 }
 
@@ -542,6 +631,14 @@ extern "C" int i2pc_resize_bilinear(const void* x, int batch, int h, int w, int 
   I2PC_REQUIRE(x && y, "NULL pointer");
   I2PC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && out_h > 0 && out_w > 0,
                "resize_bilinear: bad shape (c %% 8 == 0)");
+  const int lgcv = pow2_log(c / 8);
+  if (g_resize_rows && lgcv >= 0 && lgcv <= 8 && (int64_t)batch * out_h < (1ll << 31)) {
+    const int rows = batch * out_h;
+    hipLaunchKernelGGL(k_resize_rowmap<false>, dim3(std::min(rows, 16384)), dim3(256), 0, as_stream(stream),
+                       static_cast<const bf16_t*>(x), batch, h, w, c, lgcv, out_h, out_w, align_corners ? 1 : 0,
+                       static_cast<const bf16_t*>(add), static_cast<bf16_t*>(y), nullptr, 0, nullptr, 0);
+    return check_launch("resize_bilinear");
+  }
   const int64_t work = (int64_t)batch * out_h * out_w * (c / 8);
   // 32-bit indices when the flat index and its grid-stride successor stay below 2^31
   if (work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 31))
@@ -568,6 +665,14 @@ extern "C" int i2pc_upsample2x_fp8(const void* x, int batch, int h, int w, int c
   const int H = 2 * h, W = 2 * w;
   const int64_t work = (int64_t)batch * H * W * (c / 32);
   I2PC_REQUIRE(work + (int64_t)grid_for(work) * 256 < ((int64_t)1 << 32), "upsample2x_fp8: map too large for 32-bit indexing");
+  const int lgcv = pow2_log(c / 8);
+  if (g_resize_rows && lgcv >= 2 && lgcv <= 8) {
+    const int rows = batch * H;
+    hipLaunchKernelGGL(k_resize_rowmap<true>, dim3(std::min(rows, 16384)), dim3(256), 0, as_stream(stream),
+                       static_cast<const bf16_t*>(x), batch, h, w, c, lgcv, H, W, 1, static_cast<const bf16_t*>(add),
+                       nullptr, static_cast<uint8_t*>(y), ldy, static_cast<uint8_t*>(y_scale), ldy_scale * 4);
+    return check_launch("upsample2x_fp8");
+  }
   hipLaunchKernelGGL(k_upsample2x_fp8, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
                      static_cast<const bf16_t*>(x), batch, h, w, c, static_cast<const bf16_t*>(add),
                      static_cast<uint8_t*>(y), ldy, static_cast<uint8_t*>(y_scale), ldy_scale * 4);

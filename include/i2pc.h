@@ -418,6 +418,9 @@ int i2pc_gemm_set_engine(int mode);
  *                 the r04 grid-stride kernel (row statistics by vector loads), 2 / 3 / 4 / 5 = the same with an
  *                 agent-scope acquire first / agent-scope loads / a vector-L1 invalidate first / agent-scope
  *                 loads of the row statistics only; 0 = the product kernel (default)
+ *   "resize_rows" 1 = bilinear resizes / 2x upsamples whose channel count is a power of two (8..2048)
+ *                 run row-mapped (k_resize_rowmap: no per-output index divisions, lane-consecutive
+ *                 taps; bit-identical), 0 = the flat-index kernels; default 1
  * Defaults: the I2PC_GEMM_TAIL / _GEMM_BN128 / _GEMM_SPLITK / _GEMM_SPLIT_TILE / _GEMM_TILE192 /
  * _GEMM_LNP_P / _GEMM_TAIL160 / _GEMM_STAGGER / _UNP_ROWS / _UNP_NT / _UNP_RPT / _SEL_WIN / _ATTN_LAZY /
  * _ATTN_SCALAR environment variables, else 1, 1, 1, 0, 1, 0, 1, 1, 1, 1, 8, 1, 1, 1; sel_parts 0, sel_rows 16, sel_lband -1, ln_f2 1.  A HIP graph keeps

@@ -326,3 +326,37 @@ def test_head_upconv_uses_only_cin_channels(dev, B, h, w, C, cin, H, W):
     assert torch.equal(got, want)
     unfused = ops.head_out(ops.conv2d(ops.resize_bilinear(xs, H, W, align_corners=True), ws, bias=b2, act="relu"), w4, 0.05)
     _close(got, unfused, rel=2e-3, mx=5e-3)
+
+
+@pytest.mark.parametrize("B,h,w,C,H,W,align,add", [(2, 96, 96, 256, 192, 192, True, False), (3, 24, 24, 256, 48, 48, True, True),
+                                                    (2, 37, 53, 64, 74, 106, True, False), (2, 30, 41, 128, 64, 90, False, True),
+                                                    (1, 12, 12, 256, 24, 24, True, False), (1, 9, 7, 8, 20, 15, False, False)])
+def test_resize_rowmap_bit_identical(B, h, w, C, H, W, align, add):
+    """k_resize_rowmap (knob resize_rows 1: output rows per workgroup, a fixed 8-channel chunk per thread)
+    against the flat-index kernels (knob 0) bit for bit -- bf16, and the fp8 upsample with its per-quad
+    amax -- and against torch's upsample_bilinear2d within the bf16 rounding."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(h * w + C)
+    x = torch.randn(B, h, w, C, generator=g).to(torch.bfloat16).to(dev)
+    a = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(dev) if add else None
+    up2 = align and (H, W) == (2 * h, 2 * w) and C % 128 == 0
+    try:
+        ops.set_tuning("resize_rows", 1)
+        y1 = ops.resize_bilinear(x, H, W, align_corners=align, add=a)
+        f1 = ops.upsample2x(x, add=a, out_fp8=True) if up2 else None
+        ops.set_tuning("resize_rows", 0)
+        y0 = ops.resize_bilinear(x, H, W, align_corners=align, add=a)
+        f0 = ops.upsample2x(x, add=a, out_fp8=True) if up2 else None
+    finally:
+        ops.set_tuning("resize_rows", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16))
+    if up2:
+        assert torch.equal(f1.data, f0.data) and torch.equal(f1.scale, f0.scale)
+    ref = F.interpolate(x.permute(0, 3, 1, 2).float(), size=(H, W), mode="bilinear",
+                        align_corners=align).permute(0, 2, 3, 1)
+    if a is not None:
+        ref = ref + a.float()
+    err = (y1.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
