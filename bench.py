@@ -45,6 +45,21 @@ def _peak(label: str) -> float:
     return FP8_PEAK_TFLOPS if label.startswith("k_gemm_f8") else BF16_PEAK_TFLOPS
 
 
+class ByteAccountingError(RuntimeError):
+    """A kernel label's algorithmic bytes / measured time exceed the HBM peak: its byte formula
+    (ops.py `_Timed`) charges more than 'every operand read once, every output written once'."""
+
+
+def check_byte_accounting(kernels: dict, peak_gbs: float = HBM_PEAK_GBS) -> dict:
+    """Raise ByteAccountingError naming every kernel whose algorithmic rate is above the HBM peak
+    (k_resize once charged four input taps per output and read 13 TB/s)."""
+    over = {k: v["gbs"] for k, v in kernels.items() if v.get("gbs") and v["gbs"] > peak_gbs}
+    if over:
+        raise ByteAccountingError(f"algorithmic GB/s above the {peak_gbs:.0f} GB/s HBM peak: {over}")
+    return {"ok": True, "max_gbs": max([v["gbs"] for v in kernels.values() if v.get("gbs")] or [0.0]),
+            "peak_gbs": peak_gbs}
+
+
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -65,6 +80,12 @@ def _args():
     ap.add_argument("--no-all-gather", action="store_true",
                     help="world > 1: skip the C3 all-gather of every rank's point buffers (RCCL over xGMI), "
                          "which by default runs inside every step, overlapped with the next step's compute")
+    ap.add_argument("--no-medium", action="store_true",
+                    help="N = 1, density high: skip the density-medium sub-record (the reference's default "
+                         "density, a second pipeline on the same model, timed after the headline steps)")
+    ap.add_argument("--strict-accounting", action="store_true",
+                    help="raise ByteAccountingError when a kernel's algorithmic GB/s exceeds the HBM peak "
+                         "(default: report it in the line's byte_accounting field)")
     ap.add_argument("--model", default="dpt-large", choices=["dpt-large", "dpt-hybrid", "depth-anything-v2"])
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp8"],
                     help="network arithmetic (fp8 = MX e4m3 on the scaled MFMA; DPT-Hybrid only). "
@@ -133,6 +154,43 @@ def _kernel_profile(pipe, images, reps=5):
         d["bytes"] += nbytes
     geo_t = sorted(geo)[len(geo) // 2] * 1e-3
     return per, geo_t, (unp_ms * 1e-3 if unp_ms > 0 else None)
+
+
+def _density_record(a, spec, pipe, images, device, density):
+    """The same workload at another density step on the same model (s = 2, the reference's
+    default `medium`, app.py:52,226, beside the headline s = 1): a second captured pipeline, `a.warmup`
+    untimed and `a.steps` timed replays, then the geometry stage / unprojection kernel by HIP events."""
+    import torch
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    B, S = a.batch, a.size
+    p = PointCloudPipeline(B, S, S, spec=spec, density=density, device=device, model=pipe.model, dtype=a.dtype)
+    if a.no_graph:
+        step = lambda: p.run(images)       # noqa: E731
+    else:
+        p.capture(images)
+        step = p.replay
+    for _ in range(max(a.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    rec = {"density": density, "points_per_image": p.points_per_image,
+           "value": round(B * p.points_per_image * a.steps / el / 1e6, 2), "unit": "Mpoints/s",
+           "ms_per_step": round(el / a.steps * 1e3, 3), "steps": a.steps}
+    if not a.no_kernel_profile:
+        _, geo_t, unp_t = _kernel_profile(p, images)
+        geo_bytes = B * (4.0 * p.pre.out_h * p.pre.out_w + 18.0 * p.points_per_image)
+        rec["unproject_stage"] = {"ms": round(geo_t * 1e3, 3), "achieved_gbs": round(geo_bytes / geo_t / 1e9, 1),
+                                  "frac": round(geo_bytes / geo_t / 1e9 / HBM_PEAK_GBS, 4),
+                                  "bytes_per_step": geo_bytes}
+        if unp_t:
+            rec["unproject_kernel"] = {"us": round(unp_t * 1e6, 1), "achieved_gbs": round(geo_bytes / unp_t / 1e9, 1),
+                                       "frac": round(geo_bytes / unp_t / 1e9 / HBM_PEAK_GBS, 4)}
+    del p
+    return rec
 
 
 def kernels_sha16() -> str:
@@ -417,7 +475,7 @@ def main():
     ms = elapsed / a.steps * 1e3
 
     roofline = roof_geo = rooflines = None
-    kernels = None
+    kernels = accounting = None
     _log(f"timed {a.steps} steps: {ms:.3f} ms per step")
     if rank == 0 and not a.no_kernel_profile:
         _log("kernel profile (eager, HIP events)")
@@ -512,6 +570,18 @@ def main():
                        "tflops": round(v["flops"] / v["t"] / 1e12, 1) if v["flops"] else None,
                        "gbs": round(v["bytes"] / v["t"] / 1e9, 1) if v["bytes"] else None}
                    for k, v in sorted(per.items(), key=lambda kv: -kv[1]["t"])}
+        try:
+            accounting = check_byte_accounting(kernels)
+        except ByteAccountingError as e:
+            if a.strict_accounting:
+                raise
+            _log(f"ByteAccountingError: {e}")
+            accounting = {"ok": False, "error": f"ByteAccountingError: {e}"}
+
+    medium = None
+    if rank == 0 and world == 1 and a.density == "high" and not a.no_medium:
+        _log("density medium (the reference's default, app.py:52,226) on the same model")
+        medium = _density_record(a, spec, pipe, images, device, "medium")
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -545,6 +615,8 @@ def main():
             "rooflines": rooflines,
             "cpu_baseline": cpu,
             "multi_gpu": multi,
+            "density_medium": medium,
+            "byte_accounting": accounting,
             "kernels": kernels,
         }
         print(json.dumps(out))

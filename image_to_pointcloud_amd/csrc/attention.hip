@@ -245,12 +245,12 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 // disjoint from the current tile's ds_reads, so it put s_waitcnt vmcnt(3..0) in front of this tile's
 // QK^T MFMAs -- each tile waited for the NEXT tile's K / V to land and the prefetch hid nothing.  The
 // kernel orders the DMA itself: vmcnt(0) + barrier before a buffer is read.  M0 carries the LDS base
-// (nothing the compiler generates in this kernel uses M0).
+// and is declared clobbered, so the compiler saves / restores any M0 value of its own around it.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t lds_base, uint32_t voff, uint32_t soff) {
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                :
                : "s"(lds_base), "v"(voff), "s"(rs), "s"(soff)
-               : "memory");
+               : "memory", "m0");
 }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
@@ -732,9 +732,17 @@ extern "C" int i2pc_attention_fp8(const void* qkv, int batch, int tokens, int he
                "attention_fp8: scale rows of ldo_scale dwords cover heads * 2 blocks; 16-B aligned data");
   const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
   const float scale_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL((attn::k_attention_tr<3, true, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, nullptr, g_lazy,
-                     static_cast<uint8_t*>(out), static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
+  // the same exponent form as i2pc_attention's default dispatch (occupancy 3; scalar or packed
+  // exponent FMAs by the "attn_scalar" knob), so the bytes equal quant_fp8 of its bf16 output under
+  // the same knobs (I2PC_ATTN_OCC / I2PC_ATTN_OLD select bf16-only variants and are not mirrored here)
+  if (g_scalar)
+    hipLaunchKernelGGL((attn::k_attention_tr<3, true, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, nullptr, g_lazy,
+                       static_cast<uint8_t*>(out), static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
+  else
+    hipLaunchKernelGGL((attn::k_attention_tr<3, false, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, nullptr, g_lazy,
+                       static_cast<uint8_t*>(out), static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
   return check_launch("attention_fp8");
 }
 
@@ -753,7 +761,7 @@ extern "C" int i2pc_attention(const void* qkv, int batch, int tokens, int heads,
   else if (occ == 2)
     hipLaunchKernelGGL(attn::k_attention_tr<2>, dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
-  else if (occ == 4)
+  else if (occ == 4)   // four waves per SIMD: the scalar-FMA form only (r05)
     hipLaunchKernelGGL((attn::k_attention_tr<4, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
                        static_cast<const uint16_t*>(qkv), batch, tokens, heads, scale_log2, static_cast<uint16_t*>(out), g_lazy);
   else if (g_scalar)

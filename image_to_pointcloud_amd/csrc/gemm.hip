@@ -225,8 +225,9 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       const int m = mrow0 + i0 * 16 + r;
       if ((LPR * RPP < 64 && (rr >= RPP || r >= ni * 16)) || m >= p.M) continue;
       const int orow = remap(m, p.o_g, p.o_gs, p.o_o);
-      if (p.rsh) pre_rs[it] = p.rsh[orow];
-      if (p.lnsh) pre_sh[it] = p.lnsh[m];
+      // per-call row shifts, written by the launch before: agent-scope loads
+      if (p.rsh) pre_rs[it] = __hip_atomic_load(p.rsh + orow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.lnsh) pre_sh[it] = __hip_atomic_load(p.lnsh + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // bias depends on the column only: load it once, all loads in flight together
@@ -312,7 +313,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
         if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
-          const float rs = PRE_SH && pre ? pre_rs[PRE_SH ? it : 0] : p.rsh[orow];
+          const float rs = PRE_SH && pre ? pre_rs[PRE_SH ? it : 0]
+                                          : __hip_atomic_load(p.rsh + orow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             v[2 * t] += __uint_as_float(q[t] << 16) + rs;
@@ -341,7 +343,9 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         if (p.lnp) {
           // LayerNorm producer: the bf16 copy of out - shift[m], and (mean, M2) of each 64-column
           // chunk (= 8 lanes) of it, or of each 32-column chunk (4 lanes; lnc = 32)
-          const float shf = p.lnsh ? (PRE_SH && pre ? pre_sh[PRE_SH ? it : 0] : p.lnsh[m]) : 0.f;
+          const float shf = p.lnsh ? (PRE_SH && pre ? pre_sh[PRE_SH ? it : 0]
+                                                   : __hip_atomic_load(p.lnsh + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                    : 0.f;
           float u[8];
 #pragma unroll
           for (int t = 0; t < 8; ++t) u[t] = v[t] - shf;
@@ -1151,6 +1155,10 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     }
   };
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  // cache policy of the LDS-DMA loads of the per-call row statistics / row shifts (written by the
+  // k_ln_rowstats launch or the producer GEMM right before this one): sc1 = agent scope, past any
+  // non-coherent line another XCD's L2 may hold (the bias and column sums are weights)
+  constexpr int kAgentScope = 16;
   // one K-stage (A BM x KSTEP, W BN x KSTEP [+ their scale dwords]) into LDS buffer `buf`;
   // with `bias_par` >= 0 wave 0 first stages the tile's BN bias values into bias slot bias_par
   const rsrc_t cs_rs_ln = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.csum), 0, EPI == EPI_LNF ? p.N * 4 : 0,
@@ -1173,13 +1181,13 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
                                                   (nn0 + lane * 4) * 4, 0, 0, 0);
       if (bias_par >= 0 && (wid == 2 || (wid == 3 && lane < (BM - 128) / 2)))
         __builtin_amdgcn_raw_ptr_buffer_load_lds(lr_rs, (lds_ptr_t)(smem + ROWS_OFF + bias_par * BM * 8 + (wid - 2) * 1024),
-                                                  16, (nm0 + (wid - 2) * 128 + lane * 2) * 8, 0, 0, 0);
+                                                  16, (nm0 + (wid - 2) * 128 + lane * 2) * 8, 0, 0, kAgentScope);
     }
     if constexpr (EPI == EPI_LNP) {
       // the tile's BM row shifts (wave 1; rows past M and a NULL shift read as zero)
       if (bias_par >= 0 && wid == 1 && lane < BM / 4)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(sh_rs, (lds_ptr_t)(smem + SHIFT_OFF + bias_par * 1024), 16,
-                                                  (nm0 + lane * 4) * 4, 0, 0, 0);
+                                                  (nm0 + lane * 4) * 4, 0, 0, kAgentScope);
     }
     int kk = 0, ky = 0, kx = 0, ci0 = 0;
     if constexpr (CONV) {

@@ -80,12 +80,12 @@ __device__ __forceinline__ void hlerp(const uint8_t* s_row, int p0, int p1, int 
 // not see these writes, so it inserts no waits for them (it would put a vmcnt(0) -- which also
 // drains the weight loads meant to stay in flight -- in front of every LDS access it cannot prove
 // disjoint); the kernel orders them itself with a counted vmcnt and a barrier.  M0 carries the LDS
-// base (no compiler-generated code in this kernel uses M0).
+// base and is declared clobbered (the compiler keeps any M0 value of its own around it).
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t lds_base, uint32_t voff, uint32_t soff) {
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                :
                : "s"(lds_base), "v"(voff), "s"(rs), "s"(soff)
-               : "memory");
+               : "memory", "m0");
 }
 
 // keep = all ones inside the image, 0 on the conv's zero padding

@@ -450,7 +450,14 @@ __global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, i
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c < d8) {
     const uint4 v = x[r * ldx8 + c];
-    const float2 s = rs[r];
+    // the row statistics are rewritten by the k_ln_rowstats launch right before this one: read them
+    // with agent-scope loads (sc1: past any non-coherent line another XCD's L2 may hold), by
+    // construction rather than by the compiler's choice of a scalar load (the r04
+    // two-process nondeterminism)
+    const float* sp = reinterpret_cast<const float*>(rs + r);
+    float2 s;
+    s.x = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s.y = __hip_atomic_load(sp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const float4 g0 = gamma[2 * c], g1 = gamma[2 * c + 1], b0 = beta[2 * c], b1 = beta[2 * c + 1];
     const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
     const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};

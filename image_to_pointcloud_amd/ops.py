@@ -520,7 +520,9 @@ def resize_bilinear(x, out_h, out_w, align_corners=True, add=None, out=None):
     B, H, W, C = x.shape
     if out is None:
         out = torch.empty((B, out_h, out_w, C), dtype=torch.bfloat16, device=x.device)
-    with _Timed("k_resize", 0.0, 2.0 * B * out_h * out_w * C * (1 + 4 + (1 if add is not None else 0))):
+    # algorithmic bytes: the input read once, the output written once, the addend read once (the
+    # per-output taps re-read the input through the caches; that is traffic, not algorithm)
+    with _Timed("k_resize", 0.0, 2.0 * B * C * (H * W + out_h * out_w * (1 + (1 if add is not None else 0)))):
         _lib.call("i2pc_resize_bilinear", _p(x), B, H, W, C, out_h, out_w, int(bool(align_corners)), _p(add),
                   _p(out), _stream())
     return out

@@ -445,7 +445,9 @@ int i2pc_attention(const void* qkv, int batch, int tokens, int heads, float scal
 /* i2pc_attention writing the MX fp8 operand of the next GEMM (DPT-Hybrid's attention-out on the fp8
  * engine) instead of bf16: out e4m3fn [batch*tokens][ldo = heads*64], out_scale E8M0 bytes, row r's
  * 32-column block j at byte r * ldo_scale * 4 + j (ldo_scale in dwords, >= heads*64/128).  The bytes
- * equal i2pc_quant_fp8 of i2pc_attention's bf16 output (quantised from the bf16-rounded values). */
+ * equal i2pc_quant_fp8 of i2pc_attention's bf16 output (quantised from the bf16-rounded values) under
+ * the same "attn_scalar" / "attn_lazy" knobs; the diagnostic I2PC_ATTN_OCC / I2PC_ATTN_OLD variants of
+ * i2pc_attention have no fp8 twin. */
 int i2pc_attention_fp8(const void* qkv, int batch, int tokens, int heads, float scale, void* out, int64_t ldo,
                        void* out_scale, int64_t ldo_scale, void* stream);
 /* i2pc_attention with Q already in the exp2 domain: the Q block of qkv holds q * scale * log2(e) (the

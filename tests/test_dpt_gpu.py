@@ -191,6 +191,61 @@ def test_c3_dpt_large_512_batch():
         assert pb.rgb[i].cpu().numpy().astype(np.float32).tobytes() == ec.tobytes(), i
 
 
+def test_c2_benchmarked_graph_32x1024():
+    """The headline workload exactly as bench.py times it (BASELINE configs[1]):
+    PointCloudPipeline(32, 1024, 1024, DPT_LARGE, seed 0) on bench._images, captured into one HIP
+    graph and replayed (bench.py main()).  Reference per-image path: backend/app.py:460-476.
+    * two replays are bit-identical to each other and to an eager run() of the same pipeline
+      (xyz, rgb, bbox, stats and the model-resolution depth);
+    * the depth is finite and non-degenerate for every image;
+    * images 0, 15 and 31 unproject bit-exact vs oracle.unproject_ref on the device depth
+      (points, colours, bounds);
+    * no image took the exact selection from scratch (SelState.level != 16: the bench's fast path)."""
+    import bench
+    from image_to_pointcloud_amd.dpt import DPT_LARGE
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    from oracle import unproject_ref as oref
+    dev = torch.device("cuda")
+    B, S = 32, 1024
+    pipe = PointCloudPipeline(B, S, S, spec=DPT_LARGE, density="high", device=dev, seed=0)
+    images = bench._images(B, S, 0, dev)
+    out = pipe.capture(images)
+
+    def snap():
+        return [t.clone() for t in (out.xyz, out.rgb, out.bbox, out.stats, pipe.depth)]
+
+    pipe.replay()
+    torch.cuda.synchronize()
+    r1 = snap()
+    pipe.replay()
+    torch.cuda.synchronize()
+    r2 = snap()
+    names = ("xyz", "rgb", "bbox", "stats", "depth")
+    for n, a, b in zip(names, r1, r2):
+        assert torch.equal(a, b), f"replay 1 vs replay 2 differ in {n}"
+    st = pipe._ws[:624 * B].view(torch.int32).view(B, 156)[:, 85].cpu()
+    assert int((st == 16).sum()) == 0, f"selection from scratch on images {torch.nonzero(st == 16).flatten().tolist()}"
+    eo = pipe.run(images)
+    torch.cuda.synchronize()
+    for n, a, b in zip(names, r1, (eo.xyz, eo.rgb, eo.bbox, eo.stats, pipe.depth)):
+        assert torch.equal(a, b), f"replay vs eager run() differ in {n}"
+    depth = r1[4].cpu().numpy()
+    assert depth.shape == (B, 384, 384) and np.isfinite(depth).all()
+    per_std = depth.reshape(B, -1).std(axis=1)
+    assert (per_std > 1e-3 * np.abs(depth).max()).all(), "degenerate depth in some image"
+    imgs = images.cpu().numpy()
+    bbox = r1[2].cpu().numpy()
+    for i in (0, 15, 31):
+        ep, ec = oref.depth_to_point_cloud(imgs[i], depth[i], density="high", loop=False)
+        assert r1[0][i].cpu().numpy().tobytes() == ep.tobytes(), i
+        assert r1[1][i].cpu().numpy().astype(np.float32).tobytes() == ec.tobytes(), i
+        eb = oref.gis_bounds(ep)                                  # app.py:393-400
+        exp = np.array([eb["minX"], eb["maxX"], eb["minY"], eb["maxY"], eb["minZ"], eb["maxZ"]], np.float64)
+        assert np.array_equal(bbox[i], exp), (i, bbox[i], exp)
+    _report("c2 benchmarked graph 32x1024^2", replays_identical=1, eager_identical=1,
+            selection_from_scratch=int((st == 16).sum()))
+
+
 def test_dpt_any_grid_pos_interpolation_and_fusion_resize():
     """DPT on an odd patch grid (112 x 112 network input -> 7 x 7 patches against the checkpoint's
     8 x 8): the position table is interpolated (DPTViTEmbeddings._resize_pos_embed) and the

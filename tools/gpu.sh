@@ -20,7 +20,7 @@
 #   c4                         tools/c4_panorama.py on one rank: window / levels / smooth / equirect / network stream
 #   clock [tag] [bench args]   effective shader clock per kernel (GRBM_GUI_ACTIVE / 8 / wall) -> profiles/<round>_<tag>_clock.json
 set -o pipefail
-R=${ROUND:-r05}
+R=${ROUND:-r06}
 TASK=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out profiles
@@ -56,11 +56,11 @@ profile() {
   local D=gpurun_out/prof_$TAG
   rm -rf "$D"; mkdir -p "$D"
   timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$D/stats" -o run --output-format csv -- \
-    python bench.py --steps 10 --warmup 3 --no-cpu-baseline "$@" > "$D/bench.json" 2> "$D/bench.err" \
+    python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-medium --strict-accounting "$@" > "$D/bench.json" 2> "$D/bench.err" \
     || { echo "stats run failed"; tail -5 "$D/bench.err"; return 1; }
   for grp in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$D/pmc" -o $grp --output-format csv -- \
-      python bench.py --steps 1 --warmup 0 --no-graph --no-kernel-profile --no-cpu-baseline "$@" > "$D/pmc_$grp.txt" 2>&1 \
+      python bench.py --steps 1 --warmup 0 --no-graph --no-kernel-profile --no-cpu-baseline --no-medium "$@" > "$D/pmc_$grp.txt" 2>&1 \
       || { echo "pmc pass $grp failed"; tail -5 "$D/pmc_$grp.txt"; return 1; }
   done
   python tools/pmc_traffic.py "$D/pmc" "profiles/${R}_${TAG}_pmc_traffic.json" || return 1
@@ -80,7 +80,7 @@ sq() {
   for grp in "$P1" "$P2"; do
     i=$((i + 1))
     timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$D/p$i" -o p$i --output-format csv -- \
-      python bench.py --steps 1 --warmup 0 --no-graph --no-kernel-profile --no-cpu-baseline "$@" > "$D/p$i.txt" 2>&1 \
+      python bench.py --steps 1 --warmup 0 --no-graph --no-kernel-profile --no-cpu-baseline --no-medium "$@" > "$D/p$i.txt" 2>&1 \
       || { echo "pass $i failed"; tail -5 "$D/p$i.txt"; return 1; }
   done
   { for f in attention gemm_p; do python tools/pmc_summary.py "$D/p1" $f; python tools/pmc_summary.py "$D/p2" $f; done; } \
