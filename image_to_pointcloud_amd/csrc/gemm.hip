@@ -2231,6 +2231,20 @@ extern "C" int i2pc_gemm_ws(const i2pc_gemm_desc* d, void* workspace, size_t wor
 
 extern "C" int i2pc_gemm(const i2pc_gemm_desc* d, void* stream) { return i2pc_gemm_ws(d, nullptr, 0, stream); }
 
+// Planning pass of a caller that builds its descriptors ahead of the launches (model.cpp): the same
+// validation and plan as i2pc_gemm_ws, without a launch; sets the thread's error like the launch would.
+int i2pc_gemm_check(const i2pc_gemm_desc* d, size_t* workspace_bytes) {
+  gemm::Args p;
+  const int rc = make_args(d, p);
+  if (rc != I2PC_OK) return rc;
+  const gemm::Plan pl = gemm::plan_for(p, d->conv != 0, d->conv_relu_in != 0);
+  if (pl.kind == -2) return set_error(I2PC_EUNSUPPORTED, "gemm: LayerNorm fold not available for this call");
+  if (pl.kind == -1) return set_error(I2PC_EUNSUPPORTED, "gemm: N=%d must be a multiple of 32", p.N);
+  const gemm::SplitPlan sp = gemm::split_for(p, pl);
+  if (workspace_bytes) *workspace_bytes = sp.splits > 1 ? (size_t)sp.bytes : 0;
+  return I2PC_OK;
+}
+
 extern "C" size_t i2pc_gemm_workspace_bytes(const i2pc_gemm_desc* d) {
   gemm::Args p;
   if (make_args(d, p) != I2PC_OK) return 0;

@@ -115,10 +115,20 @@ static i2pc_gemm_desc conv_desc(const Map& x, const void* w, const float* bias, 
   return d;
 }
 
-// plan pass: record the largest split-K workspace; run pass: launch
+}  // namespace model
+}  // namespace i2pc
+int i2pc_gemm_check(const i2pc_gemm_desc* d, size_t* workspace_bytes);   // gemm.hip (no launch)
+namespace i2pc {
+namespace model {
+
+// plan pass: every descriptor validated and planned as the launch would (an error here fails
+// i2pc_model_create before any kernel runs), and the largest split-K workspace recorded; run pass: launch
 static int gemm(i2pc_model* m, const i2pc_gemm_desc& d, bool plan, hipStream_t s) {
   if (plan) {
-    m->ws_bytes = std::max(m->ws_bytes, i2pc_gemm_workspace_bytes(&d));
+    size_t ws = 0;
+    const int rc = i2pc_gemm_check(&d, &ws);
+    if (rc != I2PC_OK) return rc;
+    m->ws_bytes = std::max(m->ws_bytes, ws);
     return I2PC_OK;
   }
   return i2pc_gemm_ws(&d, m->ws, m->ws_bytes, s);
@@ -276,6 +286,74 @@ static int forward_da(i2pc_model* m, const uint8_t* bgr, float* depth, bool plan
   return I2PC_OK;
 }
 
+// Every tensor forward_da reads, with the dtype (0 fp32, 1 bf16) and element count the header's
+// dimensions imply (model_file.py _tensors): a file whose table disagrees is rejected before any
+// upload, so a truncated or mismatched file cannot reach a kernel.
+struct Want { std::string name; int dtype; int64_t elems; };
+static int expected_tensors(const int32_t* I, std::vector<Want>& want) {
+  const int64_t D = I[I_HIDDEN], L = I[I_LAYERS], mlp = I[I_MLP], F = I[I_FUSION], h1p = I[I_H1P], kp = I[I_PITCH];
+  const int64_t np_ = (int64_t)I[I_GH] * I[I_GW];
+  want = {{"pe.w", 1, D * kp}, {"pe.b", 0, D}, {"cls", 0, D}, {"pos0", 0, D}, {"pos.table", 0, np_ * D}};
+  for (int i = 0; i < L; ++i) {
+    const std::string p = "L" + std::to_string(i) + ".";
+    want.insert(want.end(), {{p + "ln1_g", 0, D}, {p + "ln1_b", 0, D}, {p + "w_qkv", 1, 3 * D * D}, {p + "b_qkv", 0, 3 * D},
+                             {p + "w_qkv_f", 1, 3 * D * D}, {p + "b_qkv_f", 0, 3 * D}, {p + "s_qkv", 0, 3 * D},
+                             {p + "w_o", 1, D * D}, {p + "b_o", 0, D}, {p + "w_1_f", 1, mlp * D}, {p + "b_1_f", 0, mlp},
+                             {p + "s_1", 0, mlp}, {p + "w_2", 1, D * mlp}, {p + "b_2", 0, D}});
+  }
+  want.insert(want.end(), {{"ln_g", 0, D}, {"ln_b", 0, D}});
+  for (int j = 0; j < 4; ++j) {
+    const std::string p = "S" + std::to_string(j) + ".";
+    const int64_t c = I[I_NECK0 + j], fac = I[I_FAC0 + j];
+    want.insert(want.end(), {{p + "w_proj", 1, c * D}, {p + "b_proj", 0, c}, {p + "w_neck", 1, F * 9 * c}});
+    if (fac > 1) want.insert(want.end(), {{p + "w_rs", 1, fac * fac * c * c}, {p + "b_rs", 0, fac * fac * c}});
+    if (fac < 0) want.insert(want.end(), {{p + "w_rs", 1, c * 9 * c}, {p + "b_rs", 0, c}});
+  }
+  for (int j = 0; j < 4; ++j) {
+    const std::string p = "F" + std::to_string(j) + ".";
+    want.insert(want.end(), {{p + "w_proj", 1, F * F}, {p + "b_proj", 0, F}});
+    for (const char* rc : {"r1c1", "r1c2", "r2c1", "r2c2"})
+      want.insert(want.end(), {{p + rc + ".w", 1, F * 9 * F}, {p + rc + ".b", 0, F}});
+  }
+  want.insert(want.end(), {{"H.w1", 1, h1p * 9 * F}, {"H.b1", 0, h1p}, {"H.w2", 1, 32 * 9 * h1p}, {"H.b2", 0, 32},
+                           {"H.w3", 0, 32}});
+  return I2PC_OK;
+}
+
+static int validate(const int32_t* I, const std::vector<Entry>& tab) {
+  // out_indices: four distinct layers, each of which the encoder loop meets once (else hs[] would
+  // be left unwritten and the neck would read uninitialised hidden states)
+  for (int k = 0; k < 4; ++k) {
+    if (I[I_OUT0 + k] < 1 || I[I_OUT0 + k] > I[I_LAYERS])
+      return set_error(I2PC_EINVAL, "model: out index %d = %d outside 1..%d", k, I[I_OUT0 + k], I[I_LAYERS]);
+    for (int q = 0; q < k; ++q)
+      if (I[I_OUT0 + q] == I[I_OUT0 + k]) return set_error(I2PC_EINVAL, "model: out indices repeat layer %d", I[I_OUT0 + k]);
+  }
+  for (int j = 0; j < 4; ++j)
+    if (I[I_NECK0 + j] <= 0 || I[I_FAC0 + j] == 0 || I[I_FAC0 + j] > 16 || I[I_FAC0 + j] < -16)
+      return set_error(I2PC_EINVAL, "model: reassemble stage %d (channels %d, factor %d)", j, I[I_NECK0 + j], I[I_FAC0 + j]);
+  if (I[I_GH] <= 0 || I[I_GW] <= 0 || I[I_PITCH] < 3 * I[I_PATCH] * I[I_PATCH] || I[I_H1P] <= 0 || I[I_FUSION] <= 0 ||
+      I[I_MLP] <= 0 || I[I_HIDDEN] <= 0 || I[I_LAYERS] <= 0 || I[I_LAYERS] > 1024 || I[I_PATCH] <= 0)
+    return set_error(I2PC_EINVAL, "model: header dimensions out of range");
+  std::map<std::string, const Entry*> by;
+  for (const Entry& e : tab) by[std::string(e.name)] = &e;
+  std::vector<Want> want;
+  TRY(expected_tensors(I, want));
+  for (const Want& w : want) {
+    auto it = by.find(w.name);
+    if (it == by.end()) return set_error(I2PC_EINVAL, "model: tensor %s missing", w.name.c_str());
+    const Entry& e = *it->second;
+    const int64_t esz = w.dtype ? 2 : 4;
+    int64_t dims = 1;
+    for (int k = 0; k < 4; ++k) dims *= k < e.ndim ? e.dims[k] : 1;
+    if (e.dtype != w.dtype || e.ndim < 1 || e.ndim > 4 || e.nbytes != w.elems * esz || dims != w.elems)
+      return set_error(I2PC_EINVAL, "model: tensor %s is %s x %lld elements (%lld bytes), the header implies %s x %lld",
+                       w.name.c_str(), e.dtype == 1 ? "bf16" : e.dtype == 0 ? "fp32" : "?", (long long)dims,
+                       (long long)e.nbytes, w.dtype ? "bf16" : "fp32", (long long)w.elems);
+  }
+  return I2PC_OK;
+}
+
 static int read_file(const char* path, std::vector<char>& buf) {
   FILE* f = std::fopen(path, "rb");
   if (!f) return set_error(I2PC_EINVAL, "model: cannot open %s", path);
@@ -326,6 +404,7 @@ extern "C" int i2pc_model_file_info(const char* path, int32_t* ints32, float* fl
   std::vector<Entry> tab;
   size_t data0 = 0;
   TRY(parse(buf, ints32, floats16, tab, data0));
+  if (ints32[I_FAMILY] == kFamilyDepthAnything) TRY(validate(ints32, tab));
   *ntensors = (int)tab.size();
   return I2PC_OK;
 }
@@ -363,6 +442,7 @@ extern "C" int i2pc_model_create(const char* path, int batch, int in_h, int in_w
   if (I[I_IN_H] != in_h || I[I_IN_W] != in_w)
     return bail(set_error(I2PC_EINVAL, "model: the file is made for %dx%d input images, not %dx%d", I[I_IN_H], I[I_IN_W],
                           in_h, in_w));
+  if ((rc = validate(I, tab)) != I2PC_OK) return bail(rc);
   const int D = I[I_HIDDEN], gh = I[I_GH], gw = I[I_GW], np_ = gh * gw, T = np_ + 1, F = I[I_FUSION];
   if (D <= 0 || D % 64 || I[I_MLP] % 64 || I[I_HEADS] * 64 != D || gh <= 0 || gw <= 0 || F % 64 || I[I_H1P] % 64 ||
       I[I_PITCH] % 64 || I[I_LAYERS] <= 0 || I[I_HEAD_HIDDEN] != 32 || D % kLnChunk)
@@ -428,10 +508,7 @@ extern "C" int i2pc_model_create(const char* path, int batch, int in_h, int in_w
   }
   ok = ok && alloc_map(m, m->head_t, batch, m->fuse[3].up.h, m->fuse[3].up.w, I[I_H1P]);
   if (!ok) return bail(set_error(I2PC_ELAUNCH, "model: activation allocation failed"));
-  // every name the forward reads must be present
-  const char* need[] = {"pe.w", "pe.b", "cls", "pos0", "pos.table", "ln_g", "ln_b", "H.w1", "H.b1", "H.w2", "H.b2", "H.w3"};
-  for (const char* n : need)
-    if (!get(m, n)) return bail(set_error(I2PC_EINVAL, "model: tensor %s missing", n));
+  // (every tensor the forward reads was checked by validate() above: name, dtype, byte count)
   // plan pass: the largest split-K workspace any call of the forward asks for
   if ((rc = forward_da(m, nullptr, nullptr, true, nullptr)) != I2PC_OK) return bail(rc);
   if (m->ws_bytes && !(m->ws = dalloc(m, m->ws_bytes))) return bail(set_error(I2PC_ELAUNCH, "model: workspace allocation failed"));

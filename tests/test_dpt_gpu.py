@@ -12,8 +12,8 @@ DPTImageProcessorPil.
 End to end (`test_end_to_end_points_vs_fp32_reference`): transformers-fp32 depth -> oracle
 unprojection against HIP bf16 depth -> HIP unprojection.  The north star's 1e-4 relative XYZ
 bound holds for the unprojection given identical depth (bit-exact, test_unproject_gpu.py); with a
-bf16 network in front it cannot hold point for point (D9), so this test measures and prints the
-fraction of points within 1e-4 and the median / p99 relative XYZ error, and bounds the median.
+bf16 network in front it cannot hold point for point (D9), so this test splits the points into
+clip / far / interior classes, reports each class's error, and bounds the interior class.
 """
 import json
 import os
@@ -106,12 +106,26 @@ def _report(case, **vals):
 
 
 def test_end_to_end_points_vs_fp32_reference():
-    """bf16 HIP depth -> HIP points vs transformers-fp32 depth -> oracle points (DPT-Large, 2 x 384^2)."""
+    """bf16 HIP depth -> HIP points vs transformers-fp32 depth -> oracle points (DPT-Large, 2 x 384^2),
+    the point error split by cause (app.py:197-206 normalises the depth to
+    n = (clip(depth, p2, p98) - p2) / (p98 - p2) and z = depth_scale * (1 - n)):
+    * `clip`: pixels at or outside [p2, p98] in either path -- their n is pinned to 0 / 1 by one path
+      and free in the other, or both are pinned to percentiles that moved;
+    * `far`: interior pixels with z < 0.1 * depth_scale (n > 0.9, near the p98 clip) -- relative XYZ
+      error is |dn| / (1 - n), so a small absolute error is a large relative one there;
+    * `interior`: the rest -- the bulk of the cloud.
+    Per class the p50 / p99 of the relative XYZ error and of the absolute error in units of
+    depth_scale are reported.  The north star's 1e-4 relative XYZ holds for the unprojection given
+    identical depth (bit-exact, test_unproject_gpu.py); behind a bf16 network it is the
+    network's depth error that moves the points: the interior class is bounded through the
+    absolute error |dz| / depth_scale (the normalised-depth error itself), the relative error of the
+    other two classes is reported, not bounded (it divides by z -> 0 or by a clip decision)."""
     from image_to_pointcloud_amd import geometry
     from image_to_pointcloud_amd.dpt import DPT_LARGE, DPTDepthModel, synthetic_state_dict
     from image_to_pointcloud_amd.preprocess import Preprocessor, ProcessorSpec
     from oracle import unproject_ref as oref
     spec, B, hw = DPT_LARGE, 2, (384, 384)
+    scale = 10.0
     dev = torch.device("cuda")
     sd = synthetic_state_dict(spec, seed=0)
     ours = DPTDepthModel(spec, sd, dev)
@@ -122,21 +136,43 @@ def test_end_to_end_points_vs_fp32_reference():
     with torch.no_grad():
         exp_depth = ref(pixel_values=prep(timgs, layout="nchw")).predicted_depth.float().cpu().numpy()
     depth = ours(prep(timgs, layout="patches"), B)
-    pb = geometry.unproject_batch(depth, timgs, density="high")
+    pb = geometry.unproject_batch(depth, timgs, density="high", depth_scale=scale)
     torch.cuda.synchronize()
-    fracs, meds, p99s = [], [], []
+    got_depth = depth.cpu().numpy()
+    stats = pb.stats.cpu().numpy()
+    acc = {c: {"rel": [], "abs": []} for c in ("clip", "far", "interior")}
+    fracs = []
     for i in range(B):
-        ep, ec = oref.depth_to_point_cloud(imgs[i], exp_depth[i], density="high", loop=False)
+        ep, ec = oref.depth_to_point_cloud(imgs[i], exp_depth[i], density="high", depth_scale=scale, loop=False)
         got = pb.xyz[i].cpu().numpy().astype(np.float64)
         assert np.array_equal(pb.rgb[i].cpu().numpy().astype(np.float32), ec)   # integer outputs: exact
-        scale = np.maximum(np.abs(ep).max(axis=1), 10.0 * 1e-5)                  # floor: depth_scale * 1e-5
-        rel = (np.abs(got - ep).max(axis=1) / scale)
+        _, est = oref.normalize_depth(exp_depth[i], True)
+        dg, de = got_depth[i].astype(np.float32).ravel(), exp_depth[i].astype(np.float32).ravel()
+        clip = ((dg <= stats[i, 0]) | (dg >= stats[i, 1]) | (de <= est["p2"]) | (de >= est["p98"]))
+        far = ~clip & (np.minimum(np.abs(got[:, 2]), np.abs(ep[:, 2])) < 0.1 * scale)
+        inner = ~clip & ~far
+        den = np.maximum(np.abs(ep).max(axis=1), scale * 1e-5)                  # floor: depth_scale * 1e-5
+        err = np.abs(got - ep).max(axis=1)
+        rel, ab = err / den, err / scale
         fracs.append(float((rel <= 1e-4).mean()))
-        meds.append(float(np.median(rel)))
-        p99s.append(float(np.quantile(rel, 0.99)))
-    _report("e2e dpt-large 2x384^2 high: bf16 network + HIP unproject vs fp32 network + oracle",
-            frac_within_1e4=np.mean(fracs), median_rel=np.mean(meds), p99_rel=np.mean(p99s))
-    assert np.mean(meds) <= 5e-2, (fracs, meds, p99s)
+        for c, msk in (("clip", clip), ("far", far), ("interior", inner)):
+            acc[c]["rel"].append(rel[msk])
+            acc[c]["abs"].append(ab[msk])
+    out = {"frac_within_1e4": float(np.mean(fracs))}
+    n_all = sum(len(np.concatenate(v["rel"])) for v in acc.values())
+    for c, v in acc.items():
+        r, a = np.concatenate(v["rel"]), np.concatenate(v["abs"])
+        out[f"{c}_share"] = len(r) / n_all
+        if len(r):
+            out.update({f"{c}_rel_p50": float(np.median(r)), f"{c}_rel_p99": float(np.quantile(r, 0.99)),
+                        f"{c}_abs_p50": float(np.median(a)), f"{c}_abs_p99": float(np.quantile(a, 0.99))})
+    _report("e2e dpt-large 2x384^2 high: bf16 network + HIP unproject vs fp32 network + oracle", **out)
+    # the bulk of the cloud: the normalised-depth error the bf16 network leaves (its depth is within
+    # ~1-2 % rel L2 of fp32, test_dpt_forward_matches_transformers_fp32; p98 - p2 spans a fraction of
+    # the depth, so the normalised error is a few times that)
+    assert out["interior_share"] >= 0.5, out
+    assert out["interior_abs_p50"] <= 2e-2 and out["interior_abs_p99"] <= 1e-1, out
+    assert out["interior_rel_p50"] <= 5e-2, out
 
 
 def test_captured_pipeline_survives_workspace_regrow():

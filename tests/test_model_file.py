@@ -61,3 +61,52 @@ def test_bad_file_is_an_error(tmp_path):
     p.write_bytes(b"not a network")
     with pytest.raises(_lib.I2PCError, match="not an i2pc network file"):
         mf.file_info(str(p))
+
+
+def _patched(path, tmp_path, fn, tag):
+    """A copy of the file at `path` with its tensor table / header edited by fn(raw bytearray, header)."""
+    from image_to_pointcloud_amd import model_file as mf
+    raw = bytearray(open(path, "rb").read())
+    fn(raw, mf.read_header(path))
+    out = tmp_path / f"{tag}.i2pcnet"
+    out.write_bytes(bytes(raw))
+    return str(out)
+
+
+def _entry_pos(h, name):
+    from image_to_pointcloud_amd import model_file as mf
+    return 8 + 128 + 64 + mf.ENTRY.size * list(h["tensors"]).index(name)
+
+
+@pytest.mark.parametrize("case", ["nbytes", "dtype", "missing", "out_repeat", "out_range"])
+def test_mismatched_file_is_rejected(da_file, tmp_path, case):
+    """the reader checks every tensor the executor's forward reads (name, dtype, byte
+    count implied by the header) and the out indices, so a mismatched file fails at create / info time
+    instead of reading past a tensor on the GPU."""
+    import struct
+    from image_to_pointcloud_amd import _lib, model_file as mf
+    _, path = da_file
+
+    def edit(raw, h):
+        if case in ("nbytes", "dtype", "missing"):
+            pos = _entry_pos(h, "L1.w_o")
+            name, dt, nd, d0, d1, d2, d3, off, nb = mf.ENTRY.unpack(bytes(raw[pos:pos + mf.ENTRY.size]))
+            if case == "nbytes":
+                nb, d0 = nb // 2, d0 // 2            # a truncated tensor, consistent with itself
+            elif case == "dtype":
+                dt = 0
+            else:
+                name = b"L1.w_o_renamed"
+            raw[pos:pos + mf.ENTRY.size] = mf.ENTRY.pack(name, dt, nd, d0, d1, d2, d3, off, nb)
+        else:
+            ints = list(h["ints"])
+            if case == "out_repeat":
+                ints[mf.I_OUT0 + 3] = ints[mf.I_OUT0 + 2]
+            else:
+                ints[mf.I_OUT0] = ints[mf.I_LAYERS] + 1
+            raw[8:8 + 128] = struct.pack("<32i", *ints)
+    bad = _patched(path, tmp_path, edit, case)
+    msg = {"nbytes": "header implies", "dtype": "header implies", "missing": "missing", "out_repeat": "repeat",
+           "out_range": "outside"}[case]
+    with pytest.raises(_lib.I2PCError, match=msg):
+        mf.file_info(bad)
