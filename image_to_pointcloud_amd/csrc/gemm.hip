@@ -193,9 +193,16 @@ __device__ __forceinline__ void epi_passes(F&& f) {
   }
 }
 
-template <int RM, int RN, int NI>
+// Spatial output tile of the halo convolution (k_conv3_halo): local row r of the tile is pixel
+// (ty0 + r / tw, tx0 + r % tw) of image b; rows outside the output map are skipped.
+struct SpTile {
+  int base;          // b * oh * ow
+  int ty0, tx0, tw, oh, ow;
+};
+
+template <int RM, int RN, int NI, bool SPAT = false>
 __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int mrow0,
-                                              int ncol0, float* lds) {
+                                              int ncol0, float* lds, SpTile sp = SpTile{}) {
   constexpr int ni = NI;
   constexpr int TN = RN * 16;
   constexpr int U = TN / 4;                 // 16-B units per LDS row
@@ -278,7 +285,11 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
     const int r = r0 + rr;
     // TN = 96: 12 lanes per row, 5 rows per pass (60 lanes), and 48 rows are not a multiple of 5
     if (LPR * RPP < 64 && (rr >= RPP || r >= rows)) continue;
-    const int m = mrow0 + i0 * 16 + r;
+    int m = mrow0 + i0 * 16 + r;
+    if constexpr (SPAT) {   // mrow0: the wave's first local row of the spatial tile
+      const int py = m / sp.tw, px = m - py * sp.tw;
+      m = (sp.ty0 + py < sp.oh && sp.tx0 + px < sp.ow) ? sp.base + (sp.ty0 + py) * sp.ow + sp.tx0 + px : p.M;
+    }
     const int u0 = (2 * c8) ^ (r & SW), u1 = (2 * c8 + 1) ^ (r & SW);
     const float4 a = *reinterpret_cast<const float4*>(lds + r * TN + u0 * 4);
     const float4 b = *reinterpret_cast<const float4*>(lds + r * TN + u1 * 4);
@@ -688,6 +699,141 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(Args p, const float* __re
 }
 
 // ---------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 convolution of a 64-channel NHWC bf16 map with an LDS input halo
+// (k_conv3_halo; the 64-channel fusion / head convs of Depth-Anything-V2-Small,
+// modeling_depth_anything.py DepthAnythingPreActResidualLayer / DepthAnythingDepthEstimationHead).
+// The implicit-GEMM tile kernel stages every tap's A rows by LDS-DMA -- nine 128-B rows per output
+// pixel per 64 channels -- and with N = 64 its K-step is bound by that DMA issue (24 wave-instructions
+// for 8 MFMAs per wave, measured 0.56 PF at M = 701 K).  Here a workgroup owns TH x TW output pixels
+// of one image: their (TH + 2) x (TW + 2) input pixels (64 channels = one 128-B row each, zero
+// outside the image) land in LDS once, and the nine taps read their A fragments from that halo at
+// row (py + ky) * (TW + 2) + px + kx; only the tap's BN x 64 weight tile is double-buffered per
+// K-step.  K order = tap-major, as the implicit GEMM's (k = tap * 64 + ci, two 32-k MFMA sub-steps
+// per tap), so the result is bit-identical to it.  Epilogue: the tile kernel's (bias, act,
+// residuals, bf16 / fp32 out) through a spatial row map.
+template <int TH, int TW, int BN, int WM, int WN, bool RELU_A>
+__global__ __launch_bounds__(64 * WM * WN) void k_conv3_halo(Args p) {
+  constexpr int NW = WM * WN, BM = TH * TW, TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
+  constexpr int HW_ = TW + 2, HR = (TH + 2) * HW_;
+  constexpr int HR8 = (HR + 7) / 8;                 // halo DMA wave-instructions (8 rows of 128 B each)
+  constexpr int HALO_BYTES = HR8 * 8 * 128;
+  constexpr int WBYTES = BN * 128;                  // one tap's weight tile
+  constexpr int W_LOADS = BN / (8 * NW);
+  static_assert(RM >= 1 && RN >= 1 && W_LOADS >= 1 && W_LOADS * 8 * NW == BN, "tile");
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* sH = smem;
+  uint8_t* sWb = smem + HALO_BYTES;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_x = (p.cow + TW - 1) / TW, tiles_y = (p.coh + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int b = t / tiles_y;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int n0 = blockIdx.y * BN;
+
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.A), 0, (uint32_t)((int64_t)p.cb * p.ch * p.cw * 128), 0x00020000);
+  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p.W), 0, (uint32_t)((int64_t)p.N * p.ldw * 2), 0x00020000);
+  const int lrow = lane >> 3, pchunk = lane & 7;
+
+  // the halo: row R = hy * HW_ + hx <- input pixel (y0 - 1 + hy, x0 - 1 + hx); 16-B chunk pchunk of
+  // the LDS row holds logical chunk pchunk ^ (R & 7) (the source-address swizzle of the engines)
+  for (int j = wid; j < HR8; j += NW) {
+    const int R = j * 8 + lrow;
+    const int hy = R / HW_, hx = R - hy * HW_;
+    const int yi = y0 - 1 + hy, xi = x0 - 1 + hx;
+    const bool ok = R < HR && (unsigned)yi < (unsigned)p.ch && (unsigned)xi < (unsigned)p.cw;
+    const int off = ok ? ((b * p.ch + yi) * p.cw + xi) * 128 + ((pchunk ^ (R & 7)) << 4) : 0x7FFFFFF0;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rs, (lds_ptr_t)(sH + j * 1024), 16, off, 0, 0, 0);
+  }
+  // tap t's weights: rows n0 .. n0 + BN of W [N][9 * 64], columns t * 64 .. + 64
+  const int w_voff = (n0 + wid * W_LOADS * 8 + lrow) * (int)p.ldw * 2 + ((pchunk ^ lrow) << 4);
+  auto stage_w = [&](int buf, int tap) {
+#pragma unroll
+    for (int j = 0; j < W_LOADS; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rs, (lds_ptr_t)(sWb + buf * WBYTES + (wid * W_LOADS + j) * 1024), 16,
+                                                w_voff + j * 8 * (int)p.ldw * 2, tap * 128, 0, 0);
+  };
+  stage_w(0, 0);
+
+  const int frow = lane & 15, fq = lane >> 4;
+  int hb[RM];                         // halo row of tap (0, 0) for each m-subtile of this lane
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int r = wm * TM + i * 16 + frow;
+    const int py = r / TW, px = r - py * TW;
+    hb[i] = py * HW_ + px;
+  }
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();   // (vmcnt(0)) the halo and tap 0's weights landed
+
+  for (int tap = 0; tap < 9; ++tap) {
+    const int cur = tap & 1;
+    if (tap + 1 < 9) stage_w(cur ^ 1, tap + 1);
+    const uint8_t* sW = sWb + cur * WBYTES;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    const int hoff = ky * HW_ + kx;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int lchunk = 4 * s + fq;
+      bf16x8 wf[RN];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int row = wn * TN + j * 16 + frow;
+        wf[j] = *reinterpret_cast<const bf16x8*>(sW + row * 128 + ((lchunk ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int R = hb[i] + hoff;
+        bf16x8 af = *reinterpret_cast<const bf16x8*>(sH + R * 128 + ((lchunk ^ (R & 7)) << 4));
+        if (RELU_A) af = relu8(af);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // (vmcnt(0)) the next tap's weights landed; this tap's buffer may be refilled
+  }
+
+  // epilogue through this wave's LDS region (the halo and weight buffers are dead)
+  constexpr int LDS_ALL = HALO_BYTES + 2 * WBYTES;
+  constexpr int EP_RM0 = LDS_ALL / (NW * TN * 4 * 16);
+  constexpr int EP_RM1 = EP_RM0 < RM ? EP_RM0 : RM;
+  constexpr int EP_RM = RM % EP_RM1 == 0 ? EP_RM1 : RM % (EP_RM1 - 1) == 0 ? EP_RM1 - 1 : 1;
+  static_assert(EP_RM >= 1 && RM % EP_RM == 0, "epilogue LDS");
+  const SpTile sp{b * p.coh * p.cow, y0, x0, TW, p.coh, p.cow};
+  epi_passes<RM / EP_RM>([&](int pass) {
+    tile_epilogue<RM, RN, EP_RM, true>(p, acc, pass * EP_RM, wm * TM, n0 + wn * TN,
+                                       reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN, sp);
+    __builtin_amdgcn_wave_barrier();
+  });
+}
+
+template <int TH, int TW, int BN, int WM, int WN, bool RELU_A>
+static void launch_halo(const Args& p, hipStream_t s) {
+  constexpr int HR8 = ((TH + 2) * (TW + 2) + 7) / 8;
+  const int smem = HR8 * 8 * 128 + 2 * BN * 128;
+  auto kern = k_conv3_halo<TH, TW, BN, WM, WN, RELU_A>;
+  static bool attr = false;
+  if (!attr && smem > 64 * 1024) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = p.cb * ((p.coh + TH - 1) / TH) * ((p.cow + TW - 1) / TW);
+  hipLaunchKernelGGL(kern, dim3(tiles, p.N / BN), dim3(64 * WM * WN), smem, s, p);
+}
+
+// ---------------------------------------------------------------------------
 // Persistent 256-column GEMM (BM x 256 x 64 tiles, BM = 256 or 320, 8 waves as
 // 2 M x 4 N, wave tile (BM/2) x 64).  One workgroup per CU walks a strided list
 // of tiles (XCD-contiguous slots, GROUP_M order inside a round).  What it hides
@@ -708,7 +854,8 @@ namespace pers {
 
 using namespace ::i2pc::mx;
 
-enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4, EPI_Q8 = 5, EPI_LNF = 6, EPI_LNP = 7 };
+enum { EPI_PLAIN = 0, EPI_RESF32 = 1, EPI_RESBF16 = 2, EPI_RES2 = 3, EPI_CT = 4, EPI_Q8 = 5, EPI_LNF = 6, EPI_LNP = 7,
+       EPI_LNPB = 8 };
 constexpr int OOB = 0x7FFFFFF0;   // buffer range; offsets >= OOB are dropped / read as 0
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -780,9 +927,11 @@ __device__ __forceinline__ int out_elem(const Args& p, int m, int n, int64_t ld,
   } while (0)
 
 template <int EPI> struct EpiCount {
-  static constexpr int loads = EPI == EPI_RESF32 || EPI == EPI_RESBF16 || EPI == EPI_LNP ? 4 : EPI == EPI_RES2 ? 8 : 0;
-  // EPI_LNP: 4 fp32 rows + 2 bf16 (shifted copy) + 1 chunk-partials store per m-subtile
-  static constexpr int stores = EPI == EPI_RESF32 ? 4 : EPI == EPI_Q8 ? 5 : EPI == EPI_LNP ? 7 : 2;
+  static constexpr int loads = EPI == EPI_RESF32 || EPI == EPI_RESBF16 || EPI == EPI_LNP || EPI == EPI_LNPB ? 4
+                               : EPI == EPI_RES2 ? 8 : 0;
+  // EPI_LNP: 4 fp32 rows + 2 bf16 (shifted copy) + 1 chunk-partials store per m-subtile;
+  // EPI_LNPB (bf16 residual stream): 2 bf16 (the stream, in place) + 1 chunk-partials store
+  static constexpr int stores = EPI == EPI_RESF32 ? 4 : EPI == EPI_Q8 ? 5 : EPI == EPI_LNP ? 7 : EPI == EPI_LNPB ? 3 : 2;
 };
 
 // Register-direct tile epilogue of the persistent engines for one wave: rows mw0 + i*16 + (lane & 15),
@@ -791,11 +940,17 @@ template <int EPI> struct EpiCount {
 // the fp8 engine, plain row-bias / table loads the counted waits tolerate (extra, older-first).
 // EPI_LNF (LayerNorm fold, i2pc.h): t = rs.x * acc + rs.y * col_sum + bias with the wave's row
 // scales rs (float2, from LDS at rows_lds[local row]) and column sums (LDS, like the bias).
+// EPI_LNPB (LayerNorm-fold producer on the shifted bf16 residual stream, i2pc.h res_shift): the
+// tile kernel's bf16-output producer -- v = act(acc + bias) + (res + res_shift[row]), the stream
+// written back in place as bf16(v - ln_shift[row]) with the chunk partials of v - ln_shift
+// (rows_lds: the ln shifts, rsh_lds: the res shifts, both staged in LDS with the tile's bias).
 template <int RM, int RN, int EPI, bool F8>
 __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], int mw0, int ncol, const float* bias_lds,
                                            rsrc_t c_rs, rsrc_t r_rs, rsrc_t r2_rs, rsrc_t cs_rs,
-                                           const float* csum_lds = nullptr, const float* rows_lds = nullptr) {
-    static_assert(EPI != EPI_LNP || RN == 4, "EPI_LNP: a wave's 64 columns are one LayerNorm chunk (or two of 32)");
+                                           const float* csum_lds = nullptr, const float* rows_lds = nullptr,
+                                           const float* rsh_lds = nullptr) {
+    static_assert((EPI != EPI_LNP && EPI != EPI_LNPB) || RN == 4,
+                  "EPI_LNP / EPI_LNPB: a wave's 64 columns are one LayerNorm chunk (or two of 32)");
     constexpr int NRL = EpiCount<EPI>::loads, NS = EpiCount<EPI>::stores;
     static_assert(RN == 2 || RN == 4, "RN");
     const int lane = threadIdx.x & 63;
@@ -823,7 +978,7 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
           const int off = m < p.M ? (remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldr + n) * 4 : OOB;
           asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(rf[slot][j]) : "v"(off), "s"(r_rs) : "memory");
         }
-        if constexpr (EPI == EPI_RESBF16 || EPI == EPI_RES2) {
+        if constexpr (EPI == EPI_RESBF16 || EPI == EPI_RES2 || EPI == EPI_LNPB) {
           const int off = m < p.M ? (remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldr + n) * 2 : OOB;
           asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(rb[slot][j]) : "v"(off), "s"(r_rs) : "memory");
         }
@@ -849,7 +1004,7 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
                          : "i"(after) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(%c2)" : "+v"(rf[slot][0]), "+v"(rf[slot][1]) : "i"(after) : "memory");
-        } else if constexpr (EPI == EPI_RESBF16) {
+        } else if constexpr (EPI == EPI_RESBF16 || EPI == EPI_LNPB) {
           if constexpr (RN == 4)
             asm volatile("s_waitcnt vmcnt(%c4)" : "+v"(rb[slot][0]), "+v"(rb[slot][1]), "+v"(rb[slot][2]), "+v"(rb[slot][3])
                          : "i"(after) : "memory");
@@ -905,6 +1060,11 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
           v[j][0] += __uint_as_float(rb[slot][j].x << 16); v[j][1] += __uint_as_float(rb[slot][j].x & 0xffff0000u);
           v[j][2] += __uint_as_float(rb[slot][j].y << 16); v[j][3] += __uint_as_float(rb[slot][j].y & 0xffff0000u);
         }
+        if constexpr (EPI == EPI_LNPB) {   // the tile kernel's order: v + (stored + shift)
+          const float rsv = rsh_lds[i * 16 + frow];
+          v[j][0] += __uint_as_float(rb[slot][j].x << 16) + rsv; v[j][1] += __uint_as_float(rb[slot][j].x & 0xffff0000u) + rsv;
+          v[j][2] += __uint_as_float(rb[slot][j].y << 16) + rsv; v[j][3] += __uint_as_float(rb[slot][j].y & 0xffff0000u) + rsv;
+        }
         if constexpr (EPI == EPI_RES2) {
           v[j][0] += __uint_as_float(rb2[slot][j].x << 16); v[j][1] += __uint_as_float(rb2[slot][j].x & 0xffff0000u);
           v[j][2] += __uint_as_float(rb2[slot][j].y << 16); v[j][3] += __uint_as_float(rb2[slot][j].y & 0xffff0000u);
@@ -940,19 +1100,22 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
         const int soff = (ok && fq == 0) ? remap(m, p.o_g, p.o_gs, p.o_o) * (int)p.ldcs * 4 + ncol / 32 : OOB;
         if constexpr (NB == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)sbytes, cs_rs, soff, 0, 0);
         else __builtin_amdgcn_raw_buffer_store_b8((uint8_t)sbytes, cs_rs, soff, 0, 0);
-      } else if constexpr (EPI == EPI_LNP) {
+      } else if constexpr (EPI == EPI_LNP || EPI == EPI_LNPB) {
         // LayerNorm-fold producer (the tile kernel's tile_epilogue, same values bit for bit): the fp32
-        // output, a bf16 copy of u = out - shift[m], and per 64 (or 32) columns (mean, M2) of u summed
-        // in the tile kernel's order -- there a lane holds 8 consecutive columns of a row and the chunk
-        // is reduced over lane groups by xor 1, 2, 4; here a lane holds 4 columns of each 16-column
-        // group j, so 8-column group g = 2 j + (fq >> 1) is split over lanes fq = 2 h, 2 h + 1 (lane
-        // xor 16), g ^ 1 is lane xor 32, g ^ 2 is j ^ 1 and g ^ 4 is j ^ 2 (fp32 addition commutes).
+        // output (EPI_LNP; the bf16 stream has none), a bf16 copy of u = out - shift[m], and per 64 (or
+        // 32) columns (mean, M2) of u summed in the tile kernel's order -- there a lane holds 8
+        // consecutive columns of a row and the chunk is reduced over lane groups by xor 1, 2, 4; here a
+        // lane holds 4 columns of each 16-column group j, so 8-column group g = 2 j + (fq >> 1) is split
+        // over lanes fq = 2 h, 2 h + 1 (lane xor 16), g ^ 1 is lane xor 32, g ^ 2 is j ^ 1 and g ^ 4 is
+        // j ^ 2 (fp32 addition commutes).
+        if constexpr (EPI == EPI_LNP) {
 #pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          const int off = ok ? out_elem(p, m, ncol + j * 16 + fq * 4, p.ldc, false) * 4 : OOB;
-          const u32x4 d = {__float_as_uint(v[j][0]), __float_as_uint(v[j][1]), __float_as_uint(v[j][2]),
-                           __float_as_uint(v[j][3])};
-          __builtin_amdgcn_raw_buffer_store_b128(d, c_rs, off, 0, 0);
+          for (int j = 0; j < RN; ++j) {
+            const int off = ok ? out_elem(p, m, ncol + j * 16 + fq * 4, p.ldc, false) * 4 : OOB;
+            const u32x4 d = {__float_as_uint(v[j][0]), __float_as_uint(v[j][1]), __float_as_uint(v[j][2]),
+                             __float_as_uint(v[j][3])};
+            __builtin_amdgcn_raw_buffer_store_b128(d, c_rs, off, 0, 0);
+          }
         }
         const float sh = rows_lds[i * 16 + frow];
         float u[RN][4];
@@ -1075,13 +1238,15 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   constexpr int BIAS_OFF = 2 * STAGE;
   constexpr int CSUM_OFF = BIAS_OFF + 2048;          // EPI_LNF: column sums [2][1 KB], row scales [2][BM * 8]
   constexpr int ROWS_OFF = CSUM_OFF + 2048;
-  constexpr int SHIFT_OFF = BIAS_OFF + 2048;         // EPI_LNP: row shifts [2][1 KB] (BM <= 256 floats)
+  constexpr int SHIFT_OFF = BIAS_OFF + 2048;         // EPI_LNP(B): row shifts [2][1 KB] (BM <= 256 floats)
+  constexpr int RSH_OFF = SHIFT_OFF + 2048;          // EPI_LNPB: the stream's row shifts (res_shift) [2][1 KB]
   constexpr int NRL = EpiCount<EPI>::loads * RN / 4, NS = EpiCount<EPI>::stores;
   constexpr int E_ALL = RM * (NRL + NS);
   static_assert(BM == 256 || BM == 320 || BM == 160, "BM");
   static_assert(BM % 64 == 0 || (!F8 && !CONV), "BM = 160: dense bf16 A");
   static_assert(EPI != EPI_LNF || ((BM == 256 || BM == 160) && !F8 && !CONV), "EPI_LNF: dense bf16 A, BM 256 or 160");
-  static_assert(EPI != EPI_LNP || (BN == 256 && BM <= 256 && !F8 && !CONV), "EPI_LNP: dense bf16 A, BN 256");
+  static_assert((EPI != EPI_LNP && EPI != EPI_LNPB) || (BN == 256 && BM <= 256 && !F8 && !CONV),
+                "EPI_LNP / EPI_LNPB: dense bf16 A, BN 256");
   static_assert(BN == 256 || BN == 128, "BN");
   static_assert(!F8 || BM == 256, "fp8 engine: BM 256 (scale loads: one wave per 64 rows)");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1166,7 +1331,10 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
   const rsrc_t lr_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.lnr), 0, EPI == EPI_LNF ? p.M * 8 : 0,
                                                          0x00020000);
   const rsrc_t sh_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.lnsh), 0,
-                                                         EPI == EPI_LNP && p.lnsh ? p.M * 4 : 0, 0x00020000);
+                                                         (EPI == EPI_LNP || EPI == EPI_LNPB) && p.lnsh ? p.M * 4 : 0,
+                                                         0x00020000);
+  const rsrc_t rsh_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.rsh), 0,
+                                                          EPI == EPI_LNPB && p.rsh ? p.M * 4 : 0, 0x00020000);
   auto stage = [&](int buf, int k0, int bias_par) {
     uint8_t* sA = smem + buf * STAGE;
     uint8_t* sW = sA + A_BYTES;
@@ -1183,10 +1351,16 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(lr_rs, (lds_ptr_t)(smem + ROWS_OFF + bias_par * BM * 8 + (wid - 2) * 1024),
                                                   16, (nm0 + (wid - 2) * 128 + lane * 2) * 8, 0, 0, kAgentScope);
     }
-    if constexpr (EPI == EPI_LNP) {
+    if constexpr (EPI == EPI_LNP || EPI == EPI_LNPB) {
       // the tile's BM row shifts (wave 1; rows past M and a NULL shift read as zero)
       if (bias_par >= 0 && wid == 1 && lane < BM / 4)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(sh_rs, (lds_ptr_t)(smem + SHIFT_OFF + bias_par * 1024), 16,
+                                                  (nm0 + lane * 4) * 4, 0, 0, kAgentScope);
+    }
+    if constexpr (EPI == EPI_LNPB) {
+      // ... and the shifts the stream rows are stored relative to (wave 2)
+      if (bias_par >= 0 && wid == 2 && lane < BM / 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsh_rs, (lds_ptr_t)(smem + RSH_OFF + bias_par * 1024), 16,
                                                   (nm0 + lane * 4) * 4, 0, 0, kAgentScope);
     }
     int kk = 0, ky = 0, kx = 0, ci0 = 0;
@@ -1238,9 +1412,10 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
 
   const rsrc_t c_rs = p.dbg_drop ? __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0, 0x00020000) : make_rsrc(p.C);
   const rsrc_t r_rs = make_rsrc(p.res);
-  // EPI_LNP: the bf16 copy and the chunk partials take the second-residual / fp8-scale slots
-  const rsrc_t r2_rs = make_rsrc(EPI == EPI_LNP ? static_cast<const void*>(p.cbf) : static_cast<const void*>(p.res2));
-  const rsrc_t cs_rs = make_rsrc(EPI == EPI_LNP ? static_cast<const void*>(p.lnp) : static_cast<const void*>(p.Cs));
+  // EPI_LNP(B): the bf16 copy and the chunk partials take the second-residual / fp8-scale slots
+  constexpr bool LNPX = EPI == EPI_LNP || EPI == EPI_LNPB;
+  const rsrc_t r2_rs = make_rsrc(LNPX ? static_cast<const void*>(p.cbf) : static_cast<const void*>(p.res2));
+  const rsrc_t cs_rs = make_rsrc(LNPX ? static_cast<const void*>(p.lnp) : static_cast<const void*>(p.Cs));
   const int nk = p.K / KSTEP;
 
   setup(t);
@@ -1397,8 +1572,9 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
     epilogue_p<RM, RN, EPI, F8>(p, acc, m0 + wm * TM, n0 + wn * (BN / 4),
                                 reinterpret_cast<const float*>(smem + BIAS_OFF + tpar * 1024) + wn * (BN / 4), c_rs, r_rs,
                                 r2_rs, cs_rs, reinterpret_cast<const float*>(smem + CSUM_OFF + tpar * 1024) + wn * (BN / 4),
-                                EPI == EPI_LNP ? reinterpret_cast<const float*>(smem + SHIFT_OFF + tpar * 1024) + wm * TM
-                                               : reinterpret_cast<const float*>(smem + ROWS_OFF + tpar * BM * 8) + wm * TM * 2);
+                                LNPX ? reinterpret_cast<const float*>(smem + SHIFT_OFF + tpar * 1024) + wm * TM
+                                     : reinterpret_cast<const float*>(smem + ROWS_OFF + tpar * BM * 8) + wm * TM * 2,
+                                reinterpret_cast<const float*>(smem + RSH_OFF + tpar * 1024) + wm * TM);
     PSTAMP(tord, 3);
     ++tord;
     if (!has_next) break;
@@ -1671,7 +1847,7 @@ static void launch_p(const Args& p, hipStream_t s) {
   q.tiles_n = p.N / BN;
   q.group_m = group_m_for(q.tiles_m);
   const int smem = 2 * ((BM + BN) * 128 + (F8 ? (BM + BN) * 4 : 0)) + 2048 + (EPI == pers::EPI_LNF ? 2048 + 2 * BM * 8 : 0) +
-                   (EPI == pers::EPI_LNP ? 2048 : 0);
+                   (EPI == pers::EPI_LNP ? 2048 : 0) + (EPI == pers::EPI_LNPB ? 4096 : 0);
   auto kern = pers::k_gemm_p<BM, CONV, RELU_A, EPI, BN, F8>;
   static bool attr = false;
   if (!attr) {
@@ -1708,7 +1884,7 @@ static void launch_8p(const Args& p, hipStream_t s) {
 // Which kernel a call runs: the persistent 256-column engine when the epilogue is one it
 // implements and every byte offset fits its 31-bit buffer range; else the tile kernel.
 struct Plan {
-  int kind;      // 0 tile kernel, 1 persistent engine, 2 ping-pong persistent engine
+  int kind;      // 0 tile kernel, 1 persistent engine, 2 ping-pong persistent engine, 3 halo 3x3 conv
   int bm, bn, epi;
 };
 
@@ -1741,6 +1917,20 @@ static thread_local int g_split_tile = [] { const char* e = getenv("I2PC_GEMM_SP
 // 320 x 256 -- a 160-row K-step costs 0.79 of a 256-row one for 0.625 of its MFMAs, and the register-direct
 // producer epilogue's shuffle tree is slower than the tile kernel's LDS-staged one; off by default)
 static thread_local int g_lnp_p = [] { const char* e = getenv("I2PC_GEMM_LNP_P"); return e ? atoi(e) : 0; }();
+// LayerNorm-fold producers on the shifted bf16 residual stream (attention-out / FC2 with a bf16 res and
+// output, i2pc.h res_shift) on the persistent engine's EPI_LNPB: full rounds of 256 x 256 tiles plus
+// the remaining rows as one round of 160 x 256 tiles (tail_split), so one tile's producer epilogue
+// overlaps the next tile's K-loop instead of a single round's epilogues all running exposed together
+// (I2PC_GEMM_LNP_STREAM / "gemm_lnp_stream": 0 = the tile kernel, 1 = where K <= 2048 (DPT-Large's
+// attention-out; FC2's K = 4096 keeps the tile kernel's one round of 320 x 256), 2 = every such call)
+// 3x3 stride-1 convs of 64-channel maps on k_conv3_halo (I2PC_CONV_HALO / "conv_halo"; 0 = the implicit GEMM)
+// variants 1-4 (launch in run_plan); measured r06 on DA-v2's shapes (tools/bench_conv_halo.py, batch 32):
+// 148^2 + res 106 / 87 / 85 / 104 us, 296^2 295 / 274 / 282 / 302 us against the implicit GEMM's 123 / 422 us
+static thread_local int g_halo = [] { const char* e = getenv("I2PC_CONV_HALO"); return e ? atoi(e) : 3; }();
+// Measured r06 in one process (tools/ab_pipeline.py, C2): tile kernel 20.68 ms per step, attention-out on
+// EPI_LNPB 20.81, attention-out and FC2 21.22 -- the producer epilogue's register-direct shuffle tree and
+// the 1 + 0.6-round schedule do not beat the tile kernel's single round, so the default is 0 (bit-identical).
+static thread_local int g_lnp_stream = [] { const char* e = getenv("I2PC_GEMM_LNP_STREAM"); return e ? atoi(e) : 0; }();
 
 static int64_t max_row(const Args& p) {
   const int64_t m = p.M - 1;
@@ -1755,12 +1945,25 @@ static Plan plan_for(const Args& p, bool conv, bool relu) {
   int epi = -1;
   // N a multiple of 128 only (e.g. the DPT head's first conv, 256 -> 128): 256 x 128 tiles
   const int pbn = p.N % 256 == 0 ? 256 : (p.N % 128 == 0 && g_bn128) ? 128 : 0;
+  if (conv && g_halo && force == 0 && pforce != 1 && p.cc == 64 && p.ck == 3 && p.cs == 1 && p.cp == 1 &&
+      p.coh == p.ch && p.cow == p.cw && p.N % 64 == 0 && !p.rbias && !p.tbl && !p.lnp && !p.lnr && p.ct_s == 0 &&
+      p.o_g == 0 && p.o_o == 0 && (int64_t)p.cb * p.ch * p.cw * 128 < pers::OOB && (int64_t)p.N * p.ldw * 2 < pers::OOB &&
+      p.ldw >= 9 * 64)
+    return Plan{3, 256, 64, g_halo};
   if (p.lnr) {
     // LayerNorm-fold consumer: the persistent engine's EPI_LNF only (dense A, bf16 out, no extras)
     const bool ok = pbn && !conv && !relu && !p.rbias && !p.tbl && !p.res && !p.res2 && !p.c_f32 && p.ct_s == 0 &&
                     p.a_g == 0 && (int64_t)(p.M + 320) * p.lda * 2 < pers::OOB && (int64_t)p.N * p.ldw * 2 < pers::OOB &&
                     (max_row(p) * p.ldc + p.N) * 2 < pers::OOB;
     return ok ? Plan{1, 256, pbn, pers::EPI_LNF} : Plan{-2, 0, 0, 0};
+  }
+  if (p.lnp && !p.c_f32 && g_lnp_stream && force == 0 && pforce != 1) {
+    const bool ok = p.N % 256 == 0 && !conv && !relu && !p.rbias && !p.tbl && p.res && !p.res_f32 && !p.res2 &&
+                    p.ct_s == 0 && p.a_g == 0 && p.o_g == 0 && p.o_o == 0 && (g_lnp_stream >= 2 || p.K <= 2048) &&
+                    (int64_t)(p.M + 320) * p.lda * 2 < pers::OOB && (int64_t)p.N * p.ldw * 2 < pers::OOB &&
+                    ((int64_t)p.M * p.ldc + p.N) * 2 < pers::OOB && ((int64_t)p.M * p.ldr + p.N) * 2 < pers::OOB &&
+                    ((int64_t)p.M * p.ldcb + p.N) * 2 < pers::OOB && (int64_t)p.M * (p.N / p.lnc) * 8 < pers::OOB;
+    if (ok) return Plan{1, 256, 256, pers::EPI_LNPB};
   }
   if (p.lnp && g_lnp_p && force == 0 && pforce != 1) {
     // LayerNorm-fold producer on the persistent engine (EPI_LNP): a wave's 64 columns are one chunk
@@ -1955,6 +2158,10 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
     return set_error(I2PC_EUNSUPPORTED, "gemm: no persistent BN=128 variant with ReLU on A");
   }
   if constexpr (!CONV && !RELU_A) {
+    if (pl.epi == EPI_LNPB) {
+      launch_p<256, false, false, EPI_LNPB>(p, s);
+      return check_launch("gemm (LN producer, bf16 stream)");
+    }
     if (pl.epi == EPI_LNP) {
       if (pl.bm == 160) launch_p<160, false, false, EPI_LNP>(p, s);
       else launch_p<256, false, false, EPI_LNP>(p, s);
@@ -1989,7 +2196,7 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
 // (r04; a 160-row K-step costs ~0.79 of a 256-row one, tools/stamps_p.py) instead of a fifth round.
 // Returns 0 (no split), 1 (BN = 128 persistent remainder) or 2 (BM = 160 remainder).
 static thread_local int g_tail160 = [] { const char* e = getenv("I2PC_GEMM_TAIL160"); return e ? atoi(e) : 1; }();
-static int tail_split(const Args& p, int& ma) {
+static int tail_split(const Args& p, int& ma, bool bn128_ok = true) {
   if (!g_tail || p.o_g != 0 || p.a_g != 0 || p.ct_s > 0 || p.N % 256 != 0) return 0;
   const int64_t tn = p.N / 256, tm = (p.M + 255) / 256, T = tm * tn, G = num_cus();
   const int64_t rounds = T / G;
@@ -2000,7 +2207,7 @@ static int tail_split(const Args& p, int& ma) {
   if (mt >= tm) return 0;
   ma = (int)(mt * 256);
   const int64_t half_tiles = (tm - mt) * 2 * tn;
-  if (half_tiles <= G) return 1;
+  if (bn128_ok && half_tiles <= G) return 1;
   const int64_t t160 = (p.M - ma + 159) / 160 * tn;
   return g_tail160 && t160 <= G ? 2 : 0;
 }
@@ -2009,15 +2216,29 @@ template <bool CONV, bool RELU_A>
 static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
   if constexpr (!CONV && !RELU_A) {
     int ma = 0;
-    const bool lnf = pl.epi == pers::EPI_LNF;
-    const int ts = (pl.kind == 1 || pl.kind == 2) && (pl.epi == pers::EPI_PLAIN || lnf) && pl.bn == 256
-                       ? tail_split(p, ma) : 0;
+    const bool lnf = pl.epi == pers::EPI_LNF, lnpb = pl.epi == pers::EPI_LNPB;
+    // (EPI_LNPB: a 64-column partial chunk is one wave's 64 columns, so its remainder takes 160-row tiles)
+    const int ts = (pl.kind == 1 || pl.kind == 2) && (pl.epi == pers::EPI_PLAIN || lnf || lnpb) && pl.bn == 256
+                       ? tail_split(p, ma, !lnpb) : 0;
     if (ts) {
       Args pa = p, pb = p;
       pa.M = ma;
       pb.M = p.M - ma;
       pb.a_o = p.a_o + ma;
       pb.o_o = p.o_o + ma;
+      if (lnpb) {
+        // every per-row operand of the producer follows the rows (its output row map stays linear)
+        pb.o_o = p.o_o;
+        pb.C = static_cast<bf16_t*>(p.C) + (int64_t)ma * p.ldc;
+        pb.cbf = p.cbf + (int64_t)ma * p.ldcb;
+        pb.res = static_cast<const bf16_t*>(p.res) + (int64_t)ma * p.ldr;
+        pb.lnp = p.lnp + (int64_t)ma * (p.N / p.lnc) * 2;
+        if (p.lnsh) pb.lnsh = p.lnsh + ma;
+        if (p.rsh) pb.rsh = p.rsh + ma;
+        launch_p<256, false, false, pers::EPI_LNPB>(pa, s);
+        launch_p<160, false, false, pers::EPI_LNPB>(pb, s);
+        return check_launch("gemm (LN producer, bf16 stream, tail split)");
+      }
       if (lnf) {
         pb.lnr = p.lnr + (int64_t)ma * 2;      // row scales follow the rows
         launch_p<256, false, false, pers::EPI_LNF>(pa, s);
@@ -2041,6 +2262,18 @@ static int run_plan(const Plan& pl, const Args& p, hipStream_t s) {
     return set_error(I2PC_EUNSUPPORTED, "gemm: no ping-pong variant");
   }
   if (pl.kind == 1) return run_persistent<CONV, RELU_A>(pl, p, s);
+  if (pl.kind == 3) {
+    if constexpr (CONV) {
+      // variants (knob conv_halo): 1 = 16 x 16 pixels, 4 waves; 2 = 16 x 16, 8 waves; 3 = 8 x 16, 4 waves;
+      // 4 = 8 x 32, 4 waves
+      if (pl.epi == 2) launch_halo<16, 16, 64, 8, 1, RELU_A>(p, s);
+      else if (pl.epi == 3) launch_halo<8, 16, 64, 4, 1, RELU_A>(p, s);
+      else if (pl.epi == 4) launch_halo<8, 32, 64, 4, 1, RELU_A>(p, s);
+      else launch_halo<16, 16, 64, 4, 1, RELU_A>(p, s);
+      return check_launch("conv (halo)");
+    }
+    return set_error(I2PC_EUNSUPPORTED, "gemm: halo plan without a conv");
+  }
   if (pl.kind == -2) return set_error(I2PC_EUNSUPPORTED, "gemm: LayerNorm fold not available for this call");
   if (pl.kind < 0) return set_error(I2PC_EUNSUPPORTED, "gemm: N=%d must be a multiple of 32", p.N);
   if (pl.bm == 256 && pl.epi == 64) launch<256, 256, 2, 4, 64, CONV, RELU_A>(p, s);
@@ -2065,10 +2298,14 @@ static const char* plan_name(const Plan& pl, bool conv, bool relu, const SplitPl
   }
   const char* c = conv ? "true" : "false";
   const char* r = relu ? "true" : "false";
-  if (pl.kind == 2) {
+  if (pl.kind == 3) {
+    static const int th[] = {16, 16, 16, 8, 8}, tw[] = {16, 16, 16, 16, 32}, wv[] = {4, 4, 8, 4, 4};
+    const int v = pl.epi >= 1 && pl.epi <= 4 ? pl.epi : 1;
+    snprintf(buf, sizeof buf, "k_conv3_halo<%d, %d, 64, %d, 1, %s>", th[v], tw[v], wv[v], r);
+  } else if (pl.kind == 2) {
     snprintf(buf, sizeof buf, "k_gemm_8p<%s>", pl.epi == pers::EPI_PLAIN ? "plain" : "res_f32");
   } else if (pl.kind == 1) {
-    static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8", "ln_fold", "ln_prod"};
+    static const char* epis[] = {"plain", "res_f32", "res_bf16", "res2", "convT", "q8", "ln_fold", "ln_prod", "ln_stream"};
     if (pl.bn == 128) snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s, 128>", pl.bm, c, r, epis[pl.epi]);
     else snprintf(buf, sizeof buf, "k_gemm_p<%d, %s, %s, %s>", pl.bm, c, r, epis[pl.epi]);
   } else if (pl.kind == 0) {
@@ -2320,6 +2557,8 @@ bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_split_tile") == 0) { i2pc::gemm::g_split_tile = value; return true; }
   if (std::strcmp(name, "gemm_tile192") == 0) { i2pc::gemm::g_tile192 = value; return true; }
   if (std::strcmp(name, "gemm_lnp_p") == 0) { i2pc::gemm::g_lnp_p = value; return true; }
+  if (std::strcmp(name, "gemm_lnp_stream") == 0) { i2pc::gemm::g_lnp_stream = value; return true; }
+  if (std::strcmp(name, "conv_halo") == 0) { i2pc::gemm::g_halo = value; return true; }
   if (std::strcmp(name, "gemm_tail160") == 0) { i2pc::gemm::g_tail160 = value; return true; }
   if (std::strcmp(name, "gemm_stagger") == 0) { i2pc::gemm::g_stagger = value; return true; }
   return false;

@@ -392,6 +392,14 @@ int i2pc_gemm_set_engine(int mode);
  *   "gemm_tile192" 1 = 384 x 192 tiles for N % 192 == 0 calls that fit one round
  *   "gemm_lnp_p"  1 = LayerNorm-fold producers (ln_part) on the persistent engine (160 x 256 or
  *                 256 x 256 tiles, N % 256 == 0), 0 = on the tile kernel (default: measured faster)
+ *   "gemm_lnp_stream" bf16-stream producers (bf16 res + res_shift, bf16 out) on the persistent engine
+ *                 (full rounds of 256 x 256 tiles + a 160-row remainder round; N % 256 == 0):
+ *                 0 = the tile kernel (default: measured faster, r06), 1 = where K <= 2048, 2 = every K;
+ *                 bit-identical
+ *   "conv_halo"   3x3 stride-1 pad-1 convs of 64-channel NHWC maps (N % 64 == 0) on the LDS-halo kernel
+ *                 (one input halo per spatial output tile, the nine taps read from LDS): 1 = 16 x 16
+ *                 pixels / 4 waves, 2 = 16 x 16 / 8 waves, 3 = 8 x 16 / 4 waves (default), 4 = 8 x 32 /
+ *                 4 waves; 0 = the implicit GEMM.  Bit-identical (same K order)
  *   "gemm_tail160" 1 = a persistent GEMM's last partial round as 160 x 256 tiles where 256 x 128
  *                 tiles do not fit one round (DPT-Large FC1)
  *   "gemm_stagger" 1 = in the 8-wave GEMM kernels waves 4-7 issue the next K-stage's loads half-way

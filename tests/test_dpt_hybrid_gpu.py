@@ -205,10 +205,10 @@ def test_c5_batch64_pipeline_fp8_to_coloured_ply(tmp_path):
     * images 0, 31 and 63 of the batch against transformers' fp32 forward of the same three images
       on the same weights: relative L2 <= max(5e-2, 1.5 x the MX-fp8 control), max <= 3e-1 x max|ref|
       (the bound of the B = 2 test, test_dpt_hybrid_matches_transformers_fp32);
-    * the same three images as a batch of 3 through the same model, reported beside it: the fp8
-      network amplifies the fp32 summation-order differences of other schedules (split-K, tails)
-      through flipped e4m3 roundings to several per cent on these random weights, so the batch-3 run
-      is a report, not a bound -- both runs must sit inside the transformers bound;
+    * the same three images as a batch of 3 through the same model give the same depth (batch
+      invariance, VERDICT r05 item 7: the GroupNorm statistics once tiled each image by batch * hw,
+      and the fp8 roundings amplified the different partial sums to 3-6 % rel L2; every kernel now
+      sums an image's values in an order fixed by that image alone -- bound 1e-3, measured 0);
     * the unprojection of images 0, 31 and 63 bit-exact vs the oracle on the device depth;
     * one coloured binary PLY holding all 67,108,864 points, spot-checked record by record."""
     import os
@@ -256,6 +256,7 @@ def test_c5_batch64_pipeline_fp8_to_coloured_ply(tmp_path):
                 batch3_rel_l2=rel3, batch64_vs_batch3_rel_l2=self_rel)
         assert rel <= bound and mx <= 3e-1, (i, rel, mx, bound)
         assert rel3 <= bound, (i, rel3, bound)
+        assert self_rel <= 1e-3, (i, self_rel)     # batch invariance
     del ref
     for i in picks:
         ep, ec = oref.depth_to_point_cloud(imgs[i], depth[i], density="high", loop=False)

@@ -339,3 +339,49 @@ def test_stagger_bitexact(M, N, K, act, res):
     finally:
         ops.set_tuning("gemm_stagger", 1)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("B,H,W,Co", [(32, 148, 148, 64), (3, 37, 29, 64), (2, 19, 19, 128), (4, 296, 296, 64),
+                                      (1, 5, 70, 64)])
+def test_conv3_halo_bitexact(B, H, W, Co):
+    """The 64-channel 3x3 convs of Depth-Anything-V2-Small's fusion / head on k_conv3_halo (one input
+    halo per 16 x 16 output pixels in LDS; knob conv_halo) equal the implicit-GEMM tile kernel bit for
+    bit -- same K order (tap-major, two 32-k sub-steps) -- for the unit's three epilogues (ReLU-in +
+    bias + ReLU; bias + res + res2; bias + res), image sizes that leave partial tiles and several
+    N-tiles; and torch fp32 within 8e-3."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    C = 64
+    g = torch.Generator(device="cpu").manual_seed(B * 7 + H + Co)
+    x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+    res = _bf(torch.randn(B, H, W, Co, generator=g)).to(dev)
+    res2 = _bf(torch.randn(B, H, W, Co, generator=g)).to(dev)
+    w = (torch.randn(Co, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev)
+    b = (torch.randn(Co, generator=g) * 0.1).to(dev)
+    wp = _pack_conv(w)
+    cases = [dict(relu_in=True, act="relu"), dict(res=res, res2=res2), dict(res=res)]
+    d = ops.GemmDesc()
+    d.a = d.w = d.c = 16
+    d.m, d.n, d.k, d.lda, d.ldw, d.ldc = B * H * W, Co, 9 * C, C, 9 * C, Co
+    d.conv, d.conv_batch, d.conv_h, d.conv_w, d.conv_c = 1, B, H, W, C
+    d.conv_oh, d.conv_ow, d.conv_k, d.conv_stride, d.conv_pad = H, W, 3, 1, 1
+    assert ops.gemm_kernel_label(d).startswith("k_conv3_halo<"), ops.gemm_kernel_label(d)
+    for kw in cases:
+        outs = []
+        try:
+            for on in (3, 0):
+                ops.set_tuning("conv_halo", on)
+                outs.append(ops.conv2d(x, wp, bias=b, **kw).clone())
+        finally:
+            ops.set_tuning("conv_halo", 3)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), (kw.keys(), (outs[0].float() - outs[1].float()).abs().max().item())
+        xin = F.relu(x.float()) if kw.get("relu_in") else x.float()
+        r = F.conv2d(xin.permute(0, 3, 1, 2), _bf(w).float(), b, padding=1).permute(0, 2, 3, 1)
+        if kw.get("act") == "relu":
+            r = F.relu(r)
+        if "res" in kw:
+            r = r + res.float()
+        if "res2" in kw:
+            r = r + res2.float()
+        assert _fro(outs[0], r) <= 8e-3

@@ -311,3 +311,43 @@ def test_bf16_stream_forward_matches_fp32_stream(model):
     from test_dpt_gpu import _report
     _report(f"{model} bf16 stream vs fp32 stream", rel_l2=rel)
     assert rel <= 2e-2, rel
+
+
+@pytest.mark.parametrize("M,N,K,C,shifted,rsh", [(18464, 1024, 1024, 64, True, True), (18464, 1024, 4096, 64, False, True),
+                                                 (18464, 1024, 1024, 32, True, False), (1000, 1024, 1024, 64, True, True),
+                                                 (36928, 768, 768, 64, True, True)])
+def test_bf16_stream_producer_persistent_matches_tile_kernel(M, N, K, C, shifted, rsh):
+    """The bf16-stream producer on the persistent engine (EPI_LNPB: full rounds of 256 x 256 tiles + a
+    160-row remainder launch; knob gemm_lnp_stream, 2 = every K) writes exactly the tile kernel's
+    bytes: the stream in place and the chunk partials."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M * 3 + K + C)
+    a = _rand((M, K), g).to(torch.bfloat16).to(dev)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = _rand((N,), g, 0.1).to(torch.float32).to(dev)
+    r0 = (_rand((M, N), g) + 0.5).to(torch.bfloat16).to(dev)
+    s_in = (_rand((M,), g) * 5).to(torch.float32).to(dev) if rsh else None
+    s_out = (_rand((M,), g) * 5).to(torch.float32).to(dev) if shifted else None
+    outs, labels = [], []
+    try:
+        for mode in (2, 0):
+            ops.set_tuning("gemm_lnp_stream", mode)
+            r = r0.clone()
+            part = torch.full((M, N // C, 2), float("nan"), dtype=torch.float32, device=dev)
+            d = ops.GemmDesc()
+            d.m, d.n, d.k, d.lda, d.ldw, d.ldc, d.ldr, d.res_f32, d.c_f32 = M, N, K, K, K, N, N, 0, 0
+            d.a = d.w = d.c = d.res = d.ln_part = 16
+            d.ln_chunk = C
+            if rsh:
+                d.res_shift = 16
+            labels.append(ops.gemm_kernel_label(d))
+            ops.linear(a, w, bias=b, res=r, res_shift=s_in, out=r, ln_part=part, ln_shift=s_out, ln_chunk=C)
+            torch.cuda.synchronize()
+            outs.append((r, part))
+    finally:
+        ops.set_tuning("gemm_lnp_stream", 0)
+    assert labels[0].startswith("k_gemm_p<") and labels[0].endswith("ln_stream>"), labels
+    assert labels[1].startswith("k_gemm<"), labels
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16)), "the bf16 stream"
+    assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32)), "chunk partials"
