@@ -250,6 +250,9 @@ def test_c2_benchmarked_graph_32x1024():
     def snap():
         return [t.clone() for t in (out.xyz, out.rgb, out.bbox, out.stats, pipe.depth)]
 
+    def bits(t):      # bit identity (stats[:, 3] is NaN for a map without non-finite pixels)
+        return t.view({8: torch.int64, 4: torch.int32, 1: torch.uint8}[t.element_size()])
+
     pipe.replay()
     torch.cuda.synchronize()
     r1 = snap()
@@ -258,13 +261,13 @@ def test_c2_benchmarked_graph_32x1024():
     r2 = snap()
     names = ("xyz", "rgb", "bbox", "stats", "depth")
     for n, a, b in zip(names, r1, r2):
-        assert torch.equal(a, b), f"replay 1 vs replay 2 differ in {n}"
+        assert torch.equal(bits(a), bits(b)), f"replay 1 vs replay 2 differ in {n}"
     st = pipe._ws[:624 * B].view(torch.int32).view(B, 156)[:, 85].cpu()
     assert int((st == 16).sum()) == 0, f"selection from scratch on images {torch.nonzero(st == 16).flatten().tolist()}"
     eo = pipe.run(images)
     torch.cuda.synchronize()
     for n, a, b in zip(names, r1, (eo.xyz, eo.rgb, eo.bbox, eo.stats, pipe.depth)):
-        assert torch.equal(a, b), f"replay vs eager run() differ in {n}"
+        assert torch.equal(bits(a), bits(b)), f"replay vs eager run() differ in {n}"
     depth = r1[4].cpu().numpy()
     assert depth.shape == (B, 384, 384) and np.isfinite(depth).all()
     per_std = depth.reshape(B, -1).std(axis=1)
