@@ -170,9 +170,12 @@ def test_end_to_end_points_vs_fp32_reference():
     # the bulk of the cloud: the normalised-depth error the bf16 network leaves (its depth is within
     # ~1-2 % rel L2 of fp32, test_dpt_forward_matches_transformers_fp32; p98 - p2 spans a fraction of
     # the depth, so the normalised error is a few times that)
-    assert out["interior_share"] >= 0.5, out
-    assert out["interior_abs_p50"] <= 2e-2 and out["interior_abs_p99"] <= 1e-1, out
-    assert out["interior_rel_p50"] <= 5e-2, out
+    # (measured r06: interior 93 % of the points, |dz| / depth_scale p50 0.44 % / p99 1.7 %, relative
+    # p50 0.87 % / p99 6.1 %; far 2.8 % of the points, relative p99 147 %; clip 4.1 %, relative p99 ~24
+    # -- z pinned at 0 by one path's p98 clip)
+    assert out["interior_share"] >= 0.8, out
+    assert out["interior_abs_p50"] <= 1e-2 and out["interior_abs_p99"] <= 5e-2, out
+    assert out["interior_rel_p50"] <= 2e-2, out
 
 
 def test_captured_pipeline_survives_workspace_regrow():
