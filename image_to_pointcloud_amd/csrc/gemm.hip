@@ -141,6 +141,18 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erf_v);
 }
 
+// GELU in the tanh form, x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)) = x / (1 + exp2(x (c1 + c2 x^2))):
+// five VALU and two transcendentals instead of the erf form's ~14 and two (|GELU_tanh - GELU_erf| <=
+// 2.2e-4, a few per cent of a bf16 output ulp).  Activation code 3 (knob "gelu_tanh"); the epilogues of
+// the short-K GEMMs that take GELU (FC1 at K = 384 / 1024) are VALU-bound when every wave of a tile runs
+// its epilogue at once.
+__device__ __forceinline__ float gelu_tanh(float x) {
+  constexpr float c1 = -2.3022082f;                 // -2 sqrt(2/pi) log2(e)
+  constexpr float c2 = -2.3022082f * 0.044715f;
+  const float u = x * __builtin_fmaf(x * x, c2, c1);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+}
+
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_base), 16, 0, 0);
 }
@@ -265,6 +277,9 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       if (p.act == 1) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = gelu_erf(v[t]);
+      } else if (p.act == 3) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = gelu_tanh(v[t]);
       } else if (p.act == 2) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
@@ -434,6 +449,9 @@ __device__ __forceinline__ void epilogue4(const Args& p, int m, int n, float v[4
   if (p.act == 1) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) v[t] = gelu_erf(v[t]);
+  } else if (p.act == 3) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = gelu_tanh(v[t]);
   } else if (p.act == 2) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) v[t] = fmaxf(v[t], 0.f);
@@ -893,6 +911,7 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
 template <int ACT>
 __device__ __forceinline__ float act_f(float x) {
   if constexpr (ACT == 1) return gelu_erf(x);
+  else if constexpr (ACT == 3) return gelu_tanh(x);
   else if constexpr (ACT == 2) return fmaxf(x, 0.f);
   else return x;
 }
@@ -1210,6 +1229,7 @@ __device__ __forceinline__ void epilogue_p(const Args& p, f32x4 (&acc)[RM][RN], 
     });
     };
     if (act == 1) epilogue(std::integral_constant<int, 1>{});
+    else if (act == 3) epilogue(std::integral_constant<int, 3>{});
     else if (act == 2) epilogue(std::integral_constant<int, 2>{});
     else epilogue(std::integral_constant<int, 0>{});
 }
@@ -1930,6 +1950,8 @@ static thread_local int g_halo = [] { const char* e = getenv("I2PC_CONV_HALO"); 
 // Measured r06 in one process (tools/ab_pipeline.py, C2): tile kernel 20.68 ms per step, attention-out on
 // EPI_LNPB 20.81, attention-out and FC2 21.22 -- the producer epilogue's register-direct shuffle tree and
 // the 1 + 0.6-round schedule do not beat the tile kernel's single round, so the default is 0 (bit-identical).
+// GELU in the tanh form (activation 3) for the calls that ask for GELU (I2PC_GELU_TANH / "gelu_tanh")
+static thread_local int g_gelu_tanh = [] { const char* e = getenv("I2PC_GELU_TANH"); return e ? atoi(e) : 0; }();
 static thread_local int g_lnp_stream = [] { const char* e = getenv("I2PC_GEMM_LNP_STREAM"); return e ? atoi(e) : 0; }();
 
 static int64_t max_row(const Args& p) {
@@ -2411,7 +2433,7 @@ static int make_args(const i2pc_gemm_desc* d, gemm::Args& p) {
   p.bias = d->bias;
   p.rbias = d->row_bias; p.rb_g = d->row_bias_group > 0 ? d->row_bias_group : 1;
   p.tbl = d->table; p.tbl_rows = d->table_rows > 0 ? d->table_rows : 1;
-  p.act = d->act;
+  p.act = d->act == 1 && gemm::g_gelu_tanh ? 3 : d->act;
   p.res = d->res; p.res_f32 = d->res_f32; p.ldr = d->ldr;
   p.res2 = static_cast<const gemm::bf16_t*>(d->res2); p.ldr2 = d->ldr2;
   p.C = d->c; p.c_f32 = d->c_f32; p.ldc = d->ldc;
@@ -2559,6 +2581,7 @@ bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_lnp_p") == 0) { i2pc::gemm::g_lnp_p = value; return true; }
   if (std::strcmp(name, "gemm_lnp_stream") == 0) { i2pc::gemm::g_lnp_stream = value; return true; }
   if (std::strcmp(name, "conv_halo") == 0) { i2pc::gemm::g_halo = value; return true; }
+  if (std::strcmp(name, "gelu_tanh") == 0) { i2pc::gemm::g_gelu_tanh = value; return true; }
   if (std::strcmp(name, "gemm_tail160") == 0) { i2pc::gemm::g_tail160 = value; return true; }
   if (std::strcmp(name, "gemm_stagger") == 0) { i2pc::gemm::g_stagger = value; return true; }
   return false;
