@@ -112,7 +112,10 @@ struct Args {
                   // (knob "gemm_stagger")
   int dbg_drop;   // diagnostic (I2PC_GEMM_DROP_STORES=1): the persistent engine's output stores are issued to an
                   // empty buffer range (dropped), to measure what the stores cost the next tile's K-loop
+  int resq;       // tile kernel: residual rows through LDS in the epilogue (knob "gemm_resq")
 };
+
+__device__ __forceinline__ bool g_resq_dev(const Args& p) { return p.resq != 0; }
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
   return g > 0 ? (m / g) * gs + (m % g) + o : m + o;
@@ -205,6 +208,26 @@ __device__ __forceinline__ void epi_passes(F&& f) {
   }
 }
 
+// Residual rows staged through LDS by the tile epilogue (ResQ; the 8-wave 320 x 256 tile kernel with a
+// bf16 residual -- DPT-Large's attention-out / FC2 LayerNorm producers on the bf16 stream).  Read in the
+// epilogue's phase 2 by plain loads, each pass's residual load sat behind the previous iteration's
+// stores: vmcnt retires in issue order, so every iteration waited for a store's round trip (phase 2 of
+// the producer ~57-61 K cycles against ~19-42 K for a plain store epilogue, r04 stamps).  Here pass
+// p + 1's residual rows go to LDS by LDS-DMA, issued once pass p's phase 1 is done and before its
+// stores, and pass p + 1 waits once (vmcnt(0)) instead of once per iteration.  The DMA is inline asm,
+// invisible to the compiler (a builtin LDS-DMA made it wait vmcnt(0) before every later LDS access).
+struct ResQ {
+  int on;
+  uint8_t* buf;          // [2][NW][EP_RM * 16 rows][128 B] (after the phase-1 staging region)
+};
+
+__device__ __forceinline__ void dma16_gemm(__amdgpu_buffer_rsrc_t rs, uint32_t lds_base, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rs), "s"(0u)
+               : "memory", "m0");
+}
+
 // Spatial output tile of the halo convolution (k_conv3_halo): local row r of the tile is pixel
 // (ty0 + r / tw, tx0 + r % tw) of image b; rows outside the output map are skipped.
 struct SpTile {
@@ -214,7 +237,7 @@ struct SpTile {
 
 template <int RM, int RN, int NI, bool SPAT = false>
 __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int mrow0,
-                                              int ncol0, float* lds, SpTile sp = SpTile{}) {
+                                              int ncol0, float* lds, SpTile sp = SpTile{}, ResQ rq = ResQ{}) {
   constexpr int ni = NI;
   constexpr int TN = RN * 16;
   constexpr int U = TN / 4;                 // 16-B units per LDS row
@@ -248,6 +271,25 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       if (p.rsh) pre_rs[it] = __hip_atomic_load(p.rsh + orow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (p.lnsh) pre_sh[it] = __hip_atomic_load(p.lnsh + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+  // residual rows through LDS (ResQ): one 16-B DMA per lane and 8 rows, [row][128 B] per wave and pass
+  constexpr int NPASS = RM / NI;
+  const int pass = i0 / NI;
+  const int wid_q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t rq_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.res), 0, (uint32_t)((int64_t)p.M * p.ldr * 2), 0x00020000);
+  auto res_dma = [&](int ps) {
+    uint8_t* dst = rq.buf + ((ps & 1) * 8 + wid_q) * (NI * 16 * 128);
+#pragma unroll
+    for (int j = 0; j < NI * 2; ++j) {
+      const int r = j * 8 + (lane >> 3);
+      const int m = mrow0 + ps * NI * 16 + r;
+      const uint32_t off = m < p.M ? (uint32_t)((m * p.ldr + ncol0 + (lane & 7) * 8) * 2) : 0x7FFFFFF0u;
+      dma16_gemm(rq_rs, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(dst + j * 1024)), off);
+    }
+  };
+  if constexpr (TN == 64 && !SPAT) {
+    if (rq.on && pass == 0) res_dma(0);
   }
   // bias depends on the column only: load it once, all loads in flight together
   float4 bias4[RN];
@@ -291,6 +333,16 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint8_t* rq_cur = nullptr;
+  if constexpr (TN == 64 && !SPAT) {
+    if (rq.on) {
+      // this pass's rows landed (and the previous pass's stores drained: one wait per pass), then the
+      // next pass's rows start while this pass computes and stores
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (pass + 1 < NPASS) res_dma(pass + 1);
+      rq_cur = rq.buf + ((pass & 1) * 8 + wid_q) * (NI * 16 * 128);
+    }
+  }
   if (i0 == 0) STAMP(4);
   // phase 2
   const int rows = ni * 16;
@@ -336,7 +388,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
         v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
       } else {
-        const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
+        const uint4 x = rq_cur ? *reinterpret_cast<const uint4*>(rq_cur + r * 128 + c8 * 16)
+                               : *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
         if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
           const float rs = PRE_SH && pre ? pre_rs[PRE_SH ? it : 0]
@@ -666,9 +719,18 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   static_assert(EP_RM >= 1 && RM % EP_RM == 0, "epilogue LDS");
   // the passes as a compile-time sequence (a `#pragma unroll` loop over them can exceed the
   // unroller's size limit, and a rolled loop puts acc[][] in scratch)
+  ResQ rq{};
+  if constexpr (NW == 8 && TN == 64 && !CONV) {
+    // residual rows through LDS when the staging region leaves room for two passes of them
+    constexpr int STG = NW * EP_RM * 16 * TN * 4, RQB = 2 * NW * EP_RM * 16 * 128;
+    if (STG + RQB <= 2 * STAGE && g_resq_dev(p) && p.res && !p.res_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0) {
+      rq.on = 1;
+      rq.buf = smem + STG;
+    }
+  }
   epi_passes<RM / EP_RM>([&](int pass) {
     tile_epilogue<RM, RN, EP_RM>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
-                                 reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
+                                 reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN, SpTile{}, rq);
     __builtin_amdgcn_wave_barrier();
   });
   STAMP(3);
@@ -677,6 +739,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
 // 8-wave GEMM kernels (tile and persistent): waves 4-7 issue each next K-stage half-way through the
 // step (I2PC_GEMM_STAGGER / "gemm_stagger"; bit-identical either way)
 static thread_local int g_stagger = [] { const char* e = getenv("I2PC_GEMM_STAGGER"); return e ? atoi(e) : 1; }();
+// tile epilogue: a bf16 residual's rows staged in LDS one pass ahead (ResQ; I2PC_GEMM_RESQ / "gemm_resq")
+static thread_local int g_resq = [] { const char* e = getenv("I2PC_GEMM_RESQ"); return e ? atoi(e) : 1; }();
 
 template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>
 static void launch(const Args& p, hipStream_t s, int splits = 1) {
@@ -685,6 +749,7 @@ static void launch(const Args& p, hipStream_t s, int splits = 1) {
   q.tiles_n = p.N / BN;
   q.group_m = group_m_for(q.tiles_m);
   q.stagger = g_stagger;
+  q.resq = g_resq;
   const int smem = 2 * (BM + BN) * KB * 2;
   auto kern = k_gemm<BM, BN, WM, WN, KB, CONV, RELU_A>;
   static bool attr = false;
@@ -1950,8 +2015,10 @@ static thread_local int g_halo = [] { const char* e = getenv("I2PC_CONV_HALO"); 
 // Measured r06 in one process (tools/ab_pipeline.py, C2): tile kernel 20.68 ms per step, attention-out on
 // EPI_LNPB 20.81, attention-out and FC2 21.22 -- the producer epilogue's register-direct shuffle tree and
 // the 1 + 0.6-round schedule do not beat the tile kernel's single round, so the default is 0 (bit-identical).
-// GELU in the tanh form (activation 3) for the calls that ask for GELU (I2PC_GELU_TANH / "gelu_tanh")
-static thread_local int g_gelu_tanh = [] { const char* e = getenv("I2PC_GELU_TANH"); return e ? atoi(e) : 0; }();
+// GELU in the tanh form (activation 3) for the calls that ask for GELU (I2PC_GELU_TANH / "gelu_tanh").
+// Measured r06 in one process (tools/ab_pipeline.py): C2 20.91 -> 20.46 ms per step (+2.2 %), DA-v2
+// 7.97 -> 7.78 ms (+2.5 %); the networks stay inside their transformers-fp32 bounds.
+static thread_local int g_gelu_tanh = [] { const char* e = getenv("I2PC_GELU_TANH"); return e ? atoi(e) : 1; }();
 static thread_local int g_lnp_stream = [] { const char* e = getenv("I2PC_GEMM_LNP_STREAM"); return e ? atoi(e) : 0; }();
 
 static int64_t max_row(const Args& p) {
@@ -2582,6 +2649,7 @@ bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "gemm_lnp_stream") == 0) { i2pc::gemm::g_lnp_stream = value; return true; }
   if (std::strcmp(name, "conv_halo") == 0) { i2pc::gemm::g_halo = value; return true; }
   if (std::strcmp(name, "gelu_tanh") == 0) { i2pc::gemm::g_gelu_tanh = value; return true; }
+  if (std::strcmp(name, "gemm_resq") == 0) { i2pc::gemm::g_resq = value; return true; }
   if (std::strcmp(name, "gemm_tail160") == 0) { i2pc::gemm::g_tail160 = value; return true; }
   if (std::strcmp(name, "gemm_stagger") == 0) { i2pc::gemm::g_stagger = value; return true; }
   return false;

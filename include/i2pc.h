@@ -401,7 +401,9 @@ int i2pc_gemm_set_engine(int mode);
  *                 pixels / 4 waves, 2 = 16 x 16 / 8 waves, 3 = 8 x 16 / 4 waves (default), 4 = 8 x 32 /
  *                 4 waves; 0 = the implicit GEMM.  Bit-identical (same K order)
  *   "gelu_tanh"   1 = act 1 (GELU) evaluated in the tanh form x * sigmoid(1.5958 (x + 0.044715 x^3))
- *                 (|difference to the erf form| <= 2.2e-4), 0 = the erf form (default)
+ *                 (|difference to the erf form| <= 2.2e-4; default), 0 = the erf form
+ *   "gemm_resq"   1 = the 8-wave 320 x 256 tile kernel stages a bf16 residual's rows in LDS one epilogue
+ *                 pass ahead (LDS-DMA, one wait per pass), 0 = plain loads in the epilogue; bit-identical
  *   "gemm_tail160" 1 = a persistent GEMM's last partial round as 160 x 256 tiles where 256 x 128
  *                 tiles do not fit one round (DPT-Large FC1)
  *   "gemm_stagger" 1 = in the 8-wave GEMM kernels waves 4-7 issue the next K-stage's loads half-way

@@ -351,3 +351,31 @@ def test_bf16_stream_producer_persistent_matches_tile_kernel(M, N, K, C, shifted
     assert labels[1].startswith("k_gemm<"), labels
     assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16)), "the bf16 stream"
     assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32)), "chunk partials"
+
+
+@pytest.mark.parametrize("M,N,K,shifted", [(18464, 1024, 1024, True), (18464, 1024, 4096, False), (1000, 1024, 1024, True)])
+def test_bf16_stream_producer_resq_bitexact(M, N, K, shifted):
+    """The 320 x 256 tile kernel's epilogue with the bf16 residual rows staged in LDS one pass ahead
+    (knob gemm_resq) writes exactly the bytes of the plain-load epilogue: the stream and the partials."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M + 5 * K)
+    a = _rand((M, K), g).to(torch.bfloat16).to(dev)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = _rand((N,), g, 0.1).to(torch.float32).to(dev)
+    r0 = (_rand((M, N), g) + 0.5).to(torch.bfloat16).to(dev)
+    s_in = (_rand((M,), g) * 5).to(torch.float32).to(dev)
+    s_out = (_rand((M,), g) * 5).to(torch.float32).to(dev) if shifted else None
+    outs = []
+    try:
+        for on in (1, 0):
+            ops.set_tuning("gemm_resq", on)
+            r = r0.clone()
+            part = torch.full((M, N // 64, 2), float("nan"), dtype=torch.float32, device=dev)
+            ops.linear(a, w, bias=b, res=r, res_shift=s_in, out=r, ln_part=part, ln_shift=s_out)
+            torch.cuda.synchronize()
+            outs.append((r, part))
+    finally:
+        ops.set_tuning("gemm_resq", 1)
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16)), "the bf16 stream"
+    assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32)), "chunk partials"
