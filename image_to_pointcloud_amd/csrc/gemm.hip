@@ -278,17 +278,21 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   const int wid_q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const __amdgpu_buffer_rsrc_t rq_rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.res), 0, (uint32_t)((int64_t)p.M * p.ldr * 2), 0x00020000);
+  // [NI * 16 rows][TN * 2 B] per wave and pass: element e = 16-B chunk e % LPR of row e / LPR
+  constexpr int RQ_ELEMS = NI * 16 * LPR, RQ_BYTES = NI * 16 * TN * 2;
   auto res_dma = [&](int ps) {
-    uint8_t* dst = rq.buf + ((ps & 1) * 8 + wid_q) * (NI * 16 * 128);
+    uint8_t* dst = rq.buf + ((ps & 1) * 8 + wid_q) * RQ_BYTES;
 #pragma unroll
-    for (int j = 0; j < NI * 2; ++j) {
-      const int r = j * 8 + (lane >> 3);
+    for (int j = 0; j < (RQ_ELEMS + 63) / 64; ++j) {
+      const int e = j * 64 + lane;
+      const int r = e / LPR, ch = e - (e / LPR) * LPR;
       const int m = mrow0 + ps * NI * 16 + r;
-      const uint32_t off = m < p.M ? (uint32_t)((m * p.ldr + ncol0 + (lane & 7) * 8) * 2) : 0x7FFFFFF0u;
+      const uint32_t off = (m < p.M && e < RQ_ELEMS) ? (uint32_t)((m * p.ldr + ncol0 + ch * 8) * 2) : 0x7FFFFFF0u;
       dma16_gemm(rq_rs, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(dst + j * 1024)), off);
     }
   };
-  if constexpr (TN == 64 && !SPAT) {
+  constexpr bool RQ_OK = (TN == 64 || TN == 96) && !SPAT;
+  if constexpr (RQ_OK) {
     if (rq.on && pass == 0) res_dma(0);
   }
   // bias depends on the column only: load it once, all loads in flight together
@@ -334,13 +338,13 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint8_t* rq_cur = nullptr;
-  if constexpr (TN == 64 && !SPAT) {
+  if constexpr (RQ_OK) {
     if (rq.on) {
       // this pass's rows landed (and the previous pass's stores drained: one wait per pass), then the
       // next pass's rows start while this pass computes and stores
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (pass + 1 < NPASS) res_dma(pass + 1);
-      rq_cur = rq.buf + ((pass & 1) * 8 + wid_q) * (NI * 16 * 128);
+      rq_cur = rq.buf + ((pass & 1) * 8 + wid_q) * RQ_BYTES;
     }
   }
   if (i0 == 0) STAMP(4);
@@ -388,7 +392,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
         v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
       } else {
-        const uint4 x = rq_cur ? *reinterpret_cast<const uint4*>(rq_cur + r * 128 + c8 * 16)
+        const uint4 x = rq_cur ? *reinterpret_cast<const uint4*>(rq_cur + (r * LPR + c8) * 16)
                                : *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
         if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
@@ -719,18 +723,31 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   static_assert(EP_RM >= 1 && RM % EP_RM == 0, "epilogue LDS");
   // the passes as a compile-time sequence (a `#pragma unroll` loop over them can exceed the
   // unroller's size limit, and a rolled loop puts acc[][] in scratch)
+  // residual rows through LDS (ResQ): the passes' m-subtiles (EP_RQ, a divisor of RM) sized so the
+  // phase-1 staging and two passes of bf16 residual rows fit the K-loop's LDS
+  constexpr int EP_RQ0 = (2 * STAGE) / (NW * 16 * TN * 8);
+  constexpr int EP_RQ = EP_RQ0 >= 1 ? (RM % EP_RQ0 == 0 ? EP_RQ0 : (EP_RQ0 >= 2 && RM % (EP_RQ0 - 1) == 0) ? EP_RQ0 - 1 : 1) : 0;
   ResQ rq{};
-  if constexpr (NW == 8 && TN == 64 && !CONV) {
-    // residual rows through LDS when the staging region leaves room for two passes of them
-    constexpr int STG = NW * EP_RM * 16 * TN * 4, RQB = 2 * NW * EP_RM * 16 * 128;
-    if (STG + RQB <= 2 * STAGE && g_resq_dev(p) && p.res && !p.res_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0) {
+  if constexpr (NW == 8 && (TN == 64 || TN == 96) && !CONV && EP_RQ >= 1) {
+    if (g_resq_dev(p) && p.res && !p.res_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0) {
       rq.on = 1;
-      rq.buf = smem + STG;
+      rq.buf = smem + NW * EP_RQ * 16 * TN * 4;
+    }
+  }
+  if constexpr (EP_RQ >= 1) {
+    if (rq.on) {
+      epi_passes<RM / EP_RQ>([&](int pass) {
+        tile_epilogue<RM, RN, EP_RQ>(p, acc, pass * EP_RQ, m0 + wm * TM, n0 + wn * TN,
+                                     reinterpret_cast<float*>(smem) + wid * EP_RQ * 16 * TN, SpTile{}, rq);
+        __builtin_amdgcn_wave_barrier();
+      });
+      STAMP(3);
+      return;
     }
   }
   epi_passes<RM / EP_RM>([&](int pass) {
     tile_epilogue<RM, RN, EP_RM>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
-                                 reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN, SpTile{}, rq);
+                                 reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
     __builtin_amdgcn_wave_barrier();
   });
   STAMP(3);

@@ -353,10 +353,13 @@ def test_bf16_stream_producer_persistent_matches_tile_kernel(M, N, K, C, shifted
     assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32)), "chunk partials"
 
 
-@pytest.mark.parametrize("M,N,K,shifted", [(18464, 1024, 1024, True), (18464, 1024, 4096, False), (1000, 1024, 1024, True)])
-def test_bf16_stream_producer_resq_bitexact(M, N, K, shifted):
-    """The 320 x 256 tile kernel's epilogue with the bf16 residual rows staged in LDS one pass ahead
-    (knob gemm_resq) writes exactly the bytes of the plain-load epilogue: the stream and the partials."""
+@pytest.mark.parametrize("M,N,K,shifted,C", [(18464, 1024, 1024, True, 64), (18464, 1024, 4096, False, 64),
+                                             (1000, 1024, 1024, True, 64), (43840, 384, 1536, True, 32),
+                                             (43840, 384, 384, False, 32), (1000, 384, 384, True, 32)])
+def test_bf16_stream_producer_resq_bitexact(M, N, K, shifted, C):
+    """The tile kernel's epilogue (320 x 256 and 384 x 192 tiles) with the bf16 residual rows staged in
+    LDS one pass ahead (knob gemm_resq) writes exactly the bytes of the plain-load epilogue: the stream
+    and the partials."""
     ops = _ops()
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(M + 5 * K)
@@ -371,8 +374,8 @@ def test_bf16_stream_producer_resq_bitexact(M, N, K, shifted):
         for on in (1, 0):
             ops.set_tuning("gemm_resq", on)
             r = r0.clone()
-            part = torch.full((M, N // 64, 2), float("nan"), dtype=torch.float32, device=dev)
-            ops.linear(a, w, bias=b, res=r, res_shift=s_in, out=r, ln_part=part, ln_shift=s_out)
+            part = torch.full((M, N // C, 2), float("nan"), dtype=torch.float32, device=dev)
+            ops.linear(a, w, bias=b, res=r, res_shift=s_in, out=r, ln_part=part, ln_shift=s_out, ln_chunk=C)
             torch.cuda.synchronize()
             outs.append((r, part))
     finally:
