@@ -728,8 +728,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   constexpr int EP_RQ0 = (2 * STAGE) / (NW * 16 * TN * 8);
   constexpr int EP_RQ = EP_RQ0 >= 1 ? (RM % EP_RQ0 == 0 ? EP_RQ0 : (EP_RQ0 >= 2 && RM % (EP_RQ0 - 1) == 0) ? EP_RQ0 - 1 : 1) : 0;
   ResQ rq{};
-  if constexpr (NW == 8 && (TN == 64 || TN == 96) && !CONV && EP_RQ >= 1) {
-    if (g_resq_dev(p) && p.res && !p.res_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0) {
+  if constexpr (NW == 8 && (TN == 64 || TN == 96) && EP_RQ >= 1) {
+    if (g_resq_dev(p) && p.res && !p.res_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && p.kspan == 0) {
       rq.on = 1;
       rq.buf = smem + NW * EP_RQ * 16 * TN * 4;
     }
