@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256, OCC) void k_attention_tr(const bf16_t* __restr
 // k_attention_tr by rounding only (P in bf16 against a different reference point).  (Scaling Q inside
 // the kernel instead -- bf16(q * c) -- would add a rounding of Q whose error grows with the score: 6 %
 // of the largest output on x4 scores against torch fp32, outside the 3 % bound; measured r05.)
-template <int OCC, bool F8OUT = false>
+template <int OCC, bool F8OUT = false, bool RB = false>
 __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __restrict__ qkv, int B, int T, int NH,
                                                              bf16_t* __restrict__ out,
                                                              uint8_t* __restrict__ out8 = nullptr,
@@ -628,11 +628,24 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
         if (k2 == 1 && half) break;
         const int key = 32 * k2 + lq;
         f32x16 st;
+        if constexpr (RB) {
+          // the four K fragment reads in flight together, then the four MFMAs (one LDS round trip per
+          // half instead of four)
+          bf16x8 kf[4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int lchunk = 2 * s + hh;
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ k_swz(key)) << 4));
-          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? nm : st, 0, 0, 0);
+          for (int s = 0; s < 4; ++s)
+            kf[s] = *reinterpret_cast<const bf16x8*>(sK + key * 128 + (((2 * s + hh) ^ k_swz(key)) << 4));
+#pragma unroll
+          for (int s = 0; s < 4; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[s], s == 0 ? nm : st, 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int lchunk = 2 * s + hh;
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + key * 128 + ((lchunk ^ k_swz(key)) << 4));
+            st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], s == 0 ? nm : st, 0, 0, 0);
+          }
         }
         if (nvalid < 32 * k2 + 32) {
 #pragma unroll
@@ -677,6 +690,7 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
           for (int i = 0; i < 16; ++i) nm[i] -= delta;
         }
         l_run += ls;
+        bf16x8 vfs[2][2];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           bf16x8 pf;
@@ -693,8 +707,21 @@ __global__ __launch_bounds__(256, OCC) void k_attention_fast(const bf16_t* __res
             const int r0 = kb + tq, r1 = kb + 8 + tq;
             const v4s lo = tr_read(sV + r0 * 128 + ((lch ^ v_swz(r0)) << 4) + within);
             const v4s hi = tr_read(sV + r1 * 128 + ((lch ^ v_swz(r1)) << 4) + within);
-            const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+            vfs[s][dt] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            if constexpr (!RB) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfs[s][dt], pf, o[dt], 0, 0, 0);
+          }
+          if constexpr (RB) {
+            if (s == 1) {
+              // all eight V^T reads in flight, then the four MFMAs
+              typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+              const bf16x8 p0 = __builtin_bit_cast(bf16x8, u32x4{pk[0], pk[1], pk[2], pk[3]});
+#pragma unroll
+              for (int dt = 0; dt < 2; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfs[0][dt], p0, o[dt], 0, 0, 0);
+#pragma unroll
+              for (int dt = 0; dt < 2; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfs[1][dt], pf, o[dt], 0, 0, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            }
           }
         }
       }
@@ -715,9 +742,16 @@ using namespace i2pc;
 static thread_local int g_lazy = [] { const char* e = getenv("I2PC_ATTN_LAZY"); return e ? atoi(e) : 1; }();
 // scalar exponent FMAs (I2PC_ATTN_SCALAR / "attn_scalar")
 static thread_local int g_scalar = [] { const char* e = getenv("I2PC_ATTN_SCALAR"); return e ? atoi(e) : 1; }();
+// the q2 kernel's LDS fragment reads batched per MFMA group (I2PC_ATTN_RB / "attn_rb"; bit-identical).
+// Measured r06 in one process (tools/attn_ab.py, 5 rounds): C2 shape 64.4 -> 63.5 us, DA-v2
+// 112.2 -> 109.1 us.  Also measured there and not kept: the next block's QK^T and the previous block's
+// P.V issued beside each block's softmax (a software-pipelined form; ~140 VGPRs, so three waves per
+// SIMD): C2 74.4 us, DA-v2 112.0 -- the four-wave form's cross-wave overlap was worth more.
+static thread_local int g_rb = [] { const char* e = getenv("I2PC_ATTN_RB"); return e ? atoi(e) : 1; }();
 bool i2pc_attention_tune(const char* name, int value) {
   if (std::strcmp(name, "attn_lazy") == 0) { g_lazy = value; return true; }
   if (std::strcmp(name, "attn_scalar") == 0) { g_scalar = value; return true; }
+  if (std::strcmp(name, "attn_rb") == 0) { g_rb = value; return true; }
   return false;
 }
 
@@ -778,8 +812,12 @@ extern "C" int i2pc_attention_q2(const void* qkv, int batch, int tokens, int hea
   I2PC_REQUIRE(qkv && out, "NULL pointer");
   I2PC_REQUIRE(batch > 0 && tokens > 0 && heads > 0, "attention_q2: empty shape");
   const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
-  hipLaunchKernelGGL((attn::k_attention_fast<4>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, static_cast<uint16_t*>(out));
+  if (g_rb)
+    hipLaunchKernelGGL((attn::k_attention_fast<4, false, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, static_cast<uint16_t*>(out));
+  else
+    hipLaunchKernelGGL((attn::k_attention_fast<4>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, static_cast<uint16_t*>(out));
   return check_launch("attention_q2");
 }
 
@@ -793,8 +831,13 @@ extern "C" int i2pc_attention_q2_fp8(const void* qkv, int batch, int tokens, int
                    (reinterpret_cast<uintptr_t>(out_scale) % 4) == 0,
                "attention_q2_fp8: scale rows of ldo_scale dwords cover heads * 2 blocks; 16-B aligned data");
   const int qtiles = (tokens + attn::kQ - 1) / attn::kQ;
-  hipLaunchKernelGGL((attn::k_attention_fast<4, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint16_t*>(qkv), batch, tokens, heads, nullptr, static_cast<uint8_t*>(out),
-                     static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
+  if (g_rb)
+    hipLaunchKernelGGL((attn::k_attention_fast<4, true, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, nullptr, static_cast<uint8_t*>(out),
+                       static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
+  else
+    hipLaunchKernelGGL((attn::k_attention_fast<4, true>), dim3(batch * heads * qtiles), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint16_t*>(qkv), batch, tokens, heads, nullptr, static_cast<uint8_t*>(out),
+                       static_cast<uint8_t*>(out_scale), (int)(ldo_scale * 4));
   return check_launch("attention_q2_fp8");
 }

@@ -425,6 +425,9 @@ int i2pc_gemm_set_engine(int mode);
  *                 fallback of a missed window; tests and measurement only), default 0
  *   "attn_lazy"   1 = skip the softmax rescale of a key tile that raised no row's running max
  *   "attn_scalar" 1 = unpacked exponent FMAs and a permlane row max
+ *   "attn_rb"     i2pc_attention_q2 / _q2_fp8: 1 = each 32-key half's K (and V^T) fragment reads issued
+ *                 together ahead of their MFMAs (counted waits), 0 = one read per MFMA; bit-identical,
+ *                 default 1
  *   "ln_f2"       1 = the register-resident LayerNorm for dim 384 (k_layernorm2)
  *   "ln_apply_gs" DIAGNOSTIC reproducer of the r04 nondeterminism: 1 = i2pc_ln_apply as
  *                 the r04 grid-stride kernel (row statistics by vector loads), 2 / 3 / 4 / 5 = the same with an

@@ -228,15 +228,24 @@ def test_attention_q2_threshold_rescale(dev, B, T, H, mode):
     very negative scores (every p far below 1 against tile 0's reference point), and a rising
     sequence (every 64-key tile raises every row's max).  Sequence lengths put the last key tile's valid
     keys below, at and above the 32-key half the kernel works in (T % 64 = 1, 26, 2, 44, 33, 37, 32, 0,
-    31).  The raw-Q kernel on the unscaled operands is held to the same bound against its own reference."""
+    31).  The batched-read form (attn_rb 1, default) equals the one-read-per-MFMA form bit for bit.  The
+    raw-Q kernel on the unscaled operands is held to the same bound against its own reference."""
     ops = _ops()
     qkv, q2 = _q2_inputs(B, T, H, mode, T * 7 + H)
     qkv, q2 = qkv.to(dev), q2.to(dev)
     q, k, v = q2.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = F.scaled_dot_product_attention(q, k, v, scale=math.log(2.0)).permute(0, 2, 1, 3).reshape(B * T, H * 64)
-    got = ops.attention(q2, B, T, H, 0.125, q_log2=True)
+    outs = []
+    try:
+        for rb in (1, 0):
+            ops.set_tuning("attn_rb", rb)
+            outs.append(ops.attention(q2, B, T, H, 0.125, q_log2=True).clone())
+    finally:
+        ops.set_tuning("attn_rb", 1)
+    got = outs[0]
     assert torch.isfinite(got.float()).all()
     _close(got, ref, rel=1.2e-2, mx=3e-2)
+    assert torch.equal(outs[0], outs[1])
     q, k, v = qkv.float().view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).permute(0, 2, 1, 3).reshape(B * T, H * 64)
     _close(ops.attention(qkv, B, T, H, 0.125), ref, rel=1.2e-2, mx=3e-2)
