@@ -115,7 +115,7 @@ struct Args {
   int resq;       // tile kernel: residual rows through LDS in the epilogue (knob "gemm_resq")
 };
 
-__device__ __forceinline__ bool g_resq_dev(const Args& p) { return p.resq != 0; }
+__device__ __forceinline__ int g_resq_dev(const Args& p) { return p.resq; }
 
 __device__ __forceinline__ int remap(int m, int g, int gs, int o) {
   return g > 0 ? (m / g) * gs + (m % g) + o : m + o;
@@ -216,9 +216,17 @@ __device__ __forceinline__ void epi_passes(F&& f) {
 // p + 1's residual rows go to LDS by LDS-DMA, issued once pass p's phase 1 is done and before its
 // stores, and pass p + 1 waits once (vmcnt(0)) instead of once per iteration.  The DMA is inline asm,
 // invisible to the compiler (a builtin LDS-DMA made it wait vmcnt(0) before every later LDS access).
+// On the RQ path (tile_epilogue<..., RQP = true>) nothing else is loaded after the first pass: the bias
+// comes in registers from the caller (b4) and the wave's row shifts (res_shift, ln_shift) go to LDS by
+// one LDS-DMA each before pass 0 (rsl: [rs: TM floats][sh: TM floats]), so a pass's only wait is for its
+// residual rows -- counted past the previous pass's stores (full: the wave's rows are all < M, so each
+// phase-2 iteration issued at least one store) instead of vmcnt(0), which waited for those stores too.
 struct ResQ {
   int on;
   uint8_t* buf;          // [2][NW][EP_RM * 16 rows][128 B] (after the phase-1 staging region)
+  uint8_t* rsl;          // this wave's row shifts in LDS (RQP)
+  const float4* b4;      // this lane's bias columns (RQP)
+  int full;
 };
 
 __device__ __forceinline__ void dma16_gemm(__amdgpu_buffer_rsrc_t rs, uint32_t lds_base, uint32_t voff) {
@@ -226,6 +234,17 @@ __device__ __forceinline__ void dma16_gemm(__amdgpu_buffer_rsrc_t rs, uint32_t l
                :
                : "s"(lds_base), "v"(voff), "s"(rs), "s"(0u)
                : "memory", "m0");
+}
+// the same with sc1 (agent scope: per-call row shifts written by the launch before)
+__device__ __forceinline__ void dma16_gemm_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t lds_base, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen sc1 lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rs), "s"(0u)
+               : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // Spatial output tile of the halo convolution (k_conv3_halo): local row r of the tile is pixel
@@ -235,7 +254,7 @@ struct SpTile {
   int ty0, tx0, tw, oh, ow;
 };
 
-template <int RM, int RN, int NI, bool SPAT = false>
+template <int RM, int RN, int NI, bool SPAT = false, bool RQP = false>
 __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int mrow0,
                                               int ncol0, float* lds, SpTile sp = SpTile{}, ResQ rq = ResQ{}) {
   constexpr int ni = NI;
@@ -257,7 +276,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   // previous one's stores (r04, tools/diag12.sh: O 70 -> 68 us, DA-v2's 384 x 192 producer 100 -> 95 us).
   // Prefetching the residual rows as well was no faster: before phase 1 it pushed the 320 x 256 kernel
   // into scratch, after phase 1 (registers free) it measured 2-3 % slower (tools/diag17.sh).
-  constexpr bool PRE_SH = ITS <= 10;
+  constexpr bool PRE_SH = ITS <= 10 && !RQP;
   const bool pre = p.lnp && p.ct_s == 0;
   float pre_rs[PRE_SH ? ITS : 1], pre_sh[PRE_SH ? ITS : 1];
   if (PRE_SH && pre) {
@@ -292,14 +311,32 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
     }
   };
   constexpr bool RQ_OK = (TN == 64 || TN == 96) && !SPAT;
-  if constexpr (RQ_OK) {
+  constexpr int TMW = RM * 16;              // the wave's rows
+  static_assert(!RQP || (RQ_OK && TMW <= 256), "RQ path");
+  if constexpr (RQP) {
+    if (pass == 0) {
+      // the wave's row shifts, 4 rows per lane, before any store of the epilogue (see ResQ)
+      if (lane < TMW / 4) {
+        const uint32_t off = (uint32_t)((mrow0 + 4 * lane) * 4);
+        const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)rq.rsl;
+        if (p.rsh)
+          dma16_gemm_sc1(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.rsh), 0, (uint32_t)(p.M * 4), 0x00020000),
+                         __builtin_amdgcn_readfirstlane(base), off);
+        if (p.lnsh)
+          dma16_gemm_sc1(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.lnsh), 0, (uint32_t)(p.M * 4), 0x00020000),
+                         __builtin_amdgcn_readfirstlane(base + TMW * 4), off);
+      }
+      res_dma(0);
+    }
+  } else if constexpr (RQ_OK) {
     if (rq.on && pass == 0) res_dma(0);
   }
   // bias depends on the column only: load it once, all loads in flight together
   float4 bias4[RN];
 #pragma unroll
   for (int j = 0; j < RN; ++j)
-    bias4[j] = p.bias ? *reinterpret_cast<const float4*>(p.bias + ncol0 + j * 16 + fq * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bias4[j] = RQP ? rq.b4[j]
+                   : p.bias ? *reinterpret_cast<const float4*>(p.bias + ncol0 + j * 16 + fq * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
   // phase 1
 #pragma unroll
   for (int ii = 0; ii < ni; ++ii) {
@@ -338,7 +375,13 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint8_t* rq_cur = nullptr;
-  if constexpr (RQ_OK) {
+  if constexpr (RQP) {
+    // this pass's rows landed: issued before the previous pass's >= ITS stores, which may stay in flight
+    if (pass > 0 && rq.full) wait_vm<ITS>();
+    else wait_vm<0>();
+    if (pass + 1 < NPASS) res_dma(pass + 1);
+    rq_cur = rq.buf + ((pass & 1) * 8 + wid_q) * RQ_BYTES;
+  } else if constexpr (RQ_OK) {
     if (rq.on) {
       // this pass's rows landed (and the previous pass's stores drained: one wait per pass), then the
       // next pass's rows start while this pass computes and stores
@@ -396,8 +439,9 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
                                : *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
         if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
-          const float rs = PRE_SH && pre ? pre_rs[PRE_SH ? it : 0]
-                                          : __hip_atomic_load(p.rsh + orow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float rs = RQP ? reinterpret_cast<const float*>(rq.rsl)[i0 * 16 + r]
+                           : PRE_SH && pre ? pre_rs[PRE_SH ? it : 0]
+                                           : __hip_atomic_load(p.rsh + orow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             v[2 * t] += __uint_as_float(q[t] << 16) + rs;
@@ -426,8 +470,9 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         if (p.lnp) {
           // LayerNorm producer: the bf16 copy of out - shift[m], and (mean, M2) of each 64-column
           // chunk (= 8 lanes) of it, or of each 32-column chunk (4 lanes; lnc = 32)
-          const float shf = p.lnsh ? (PRE_SH && pre ? pre_sh[PRE_SH ? it : 0]
-                                                   : __hip_atomic_load(p.lnsh + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+          const float shf = p.lnsh ? (RQP ? reinterpret_cast<const float*>(rq.rsl)[TMW + i0 * 16 + r]
+                                      : PRE_SH && pre ? pre_sh[PRE_SH ? it : 0]
+                                                      : __hip_atomic_load(p.lnsh + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                                     : 0.f;
           float u[8];
 #pragma unroll
@@ -728,10 +773,31 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   constexpr int EP_RQ0 = (2 * STAGE) / (NW * 16 * TN * 8);
   constexpr int EP_RQ = EP_RQ0 >= 1 ? (RM % EP_RQ0 == 0 ? EP_RQ0 : (EP_RQ0 >= 2 && RM % (EP_RQ0 - 1) == 0) ? EP_RQ0 - 1 : 1) : 0;
   ResQ rq{};
+  constexpr int RQ_STAGING = NW * EP_RQ * 16 * TN * 4, RQ_ROWS = 2 * NW * EP_RQ * 16 * TN * 2;
+  constexpr bool RQ_SHIFTS = RQ_STAGING + RQ_ROWS + NW * TM * 8 <= 2 * STAGE;   // room for the row shifts
   if constexpr (NW == 8 && (TN == 64 || TN == 96) && EP_RQ >= 1) {
     if (g_resq_dev(p) && p.res && !p.res_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && p.kspan == 0) {
       rq.on = 1;
-      rq.buf = smem + NW * EP_RQ * 16 * TN * 4;
+      rq.buf = smem + RQ_STAGING;
+    }
+  }
+  if constexpr (EP_RQ >= 1 && RQ_SHIFTS && NW == 8 && (TN == 64 || TN == 96)) {
+    if (rq.on && g_resq_dev(p) >= 2) {
+      float4 b4[RN];
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        b4[j] = p.bias ? *reinterpret_cast<const float4*>(p.bias + n0 + wn * TN + j * 16 + ((threadIdx.x & 63) >> 4) * 4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      rq.rsl = smem + RQ_STAGING + RQ_ROWS + wid * TM * 8;
+      rq.b4 = b4;
+      rq.full = m0 + wm * TM + TM <= p.M;
+      epi_passes<RM / EP_RQ>([&](int pass) {
+        tile_epilogue<RM, RN, EP_RQ, false, true>(p, acc, pass * EP_RQ, m0 + wm * TM, n0 + wn * TN,
+                                                  reinterpret_cast<float*>(smem) + wid * EP_RQ * 16 * TN, SpTile{}, rq);
+        __builtin_amdgcn_wave_barrier();
+      });
+      STAMP(3);
+      return;
     }
   }
   if constexpr (EP_RQ >= 1) {
@@ -756,8 +822,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
 // 8-wave GEMM kernels (tile and persistent): waves 4-7 issue each next K-stage half-way through the
 // step (I2PC_GEMM_STAGGER / "gemm_stagger"; bit-identical either way)
 static thread_local int g_stagger = [] { const char* e = getenv("I2PC_GEMM_STAGGER"); return e ? atoi(e) : 1; }();
-// tile epilogue: a bf16 residual's rows staged in LDS one pass ahead (ResQ; I2PC_GEMM_RESQ / "gemm_resq")
-static thread_local int g_resq = [] { const char* e = getenv("I2PC_GEMM_RESQ"); return e ? atoi(e) : 1; }();
+// tile epilogue: a bf16 residual's rows staged in LDS one pass ahead (ResQ; I2PC_GEMM_RESQ / "gemm_resq");
+// 2 = the RQ path (struct ResQ): measured r06 in one process (tools/ab_pipeline.py), C2 19.022 -> 19.014 ms
+// per step, DA-v2 7.173 -> 7.121 ms, bit-identical
+static thread_local int g_resq = [] { const char* e = getenv("I2PC_GEMM_RESQ"); return e ? atoi(e) : 2; }();
 
 template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>
 static void launch(const Args& p, hipStream_t s, int splits = 1) {

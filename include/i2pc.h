@@ -402,8 +402,10 @@ int i2pc_gemm_set_engine(int mode);
  *                 4 waves; 0 = the implicit GEMM.  Bit-identical (same K order)
  *   "gelu_tanh"   1 = act 1 (GELU) evaluated in the tanh form x * sigmoid(1.5958 (x + 0.044715 x^3))
  *                 (|difference to the erf form| <= 2.2e-4; default), 0 = the erf form
- *   "gemm_resq"   1 = the 8-wave 320 x 256 tile kernel stages a bf16 residual's rows in LDS one epilogue
- *                 pass ahead (LDS-DMA, one wait per pass), 0 = plain loads in the epilogue; bit-identical
+ *   "gemm_resq"   1 = the 8-wave 320 x 256 / 384 x 192 tile kernels stage a bf16 residual's rows in LDS
+ *                 one epilogue pass ahead (LDS-DMA, one wait per pass); 2 = also the row shifts in LDS
+ *                 and the bias in registers before the first pass, and each pass's wait counted past the
+ *                 previous pass's stores (default); 0 = plain loads in the epilogue; bit-identical
  *   "gemm_tail160" 1 = a persistent GEMM's last partial round as 160 x 256 tiles where 256 x 128
  *                 tiles do not fit one round (DPT-Large FC1)
  *   "gemm_stagger" 1 = in the 8-wave GEMM kernels waves 4-7 issue the next K-stage's loads half-way

@@ -349,8 +349,9 @@ def test_bf16_stream_producer_persistent_matches_tile_kernel(M, N, K, C, shifted
         ops.set_tuning("gemm_lnp_stream", 0)
     assert labels[0].startswith("k_gemm_p<") and labels[0].endswith("ln_stream>"), labels
     assert labels[1].startswith("k_gemm<"), labels
-    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16)), "the bf16 stream"
-    assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32)), "chunk partials"
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0].view(torch.int16), o[0].view(torch.int16)), "the bf16 stream"
+        assert torch.equal(outs[0][1].view(torch.int32), o[1].view(torch.int32)), "chunk partials"
 
 
 @pytest.mark.parametrize("M,N,K,shifted,C", [(18464, 1024, 1024, True, 64), (18464, 1024, 4096, False, 64),
@@ -358,8 +359,9 @@ def test_bf16_stream_producer_persistent_matches_tile_kernel(M, N, K, C, shifted
                                              (43840, 384, 384, False, 32), (1000, 384, 384, True, 32)])
 def test_bf16_stream_producer_resq_bitexact(M, N, K, shifted, C):
     """The tile kernel's epilogue (320 x 256 and 384 x 192 tiles) with the bf16 residual rows staged in
-    LDS one pass ahead (knob gemm_resq) writes exactly the bytes of the plain-load epilogue: the stream
-    and the partials."""
+    LDS one pass ahead (knob gemm_resq 1; 2: also the row shifts in LDS and the bias in registers before
+    the first pass, each pass waiting only for its residual rows) writes exactly the bytes of the
+    plain-load epilogue: the stream and the partials."""
     ops = _ops()
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(M + 5 * K)
@@ -371,7 +373,7 @@ def test_bf16_stream_producer_resq_bitexact(M, N, K, shifted, C):
     s_out = (_rand((M,), g) * 5).to(torch.float32).to(dev) if shifted else None
     outs = []
     try:
-        for on in (1, 0):
+        for on in (2, 1, 0):
             ops.set_tuning("gemm_resq", on)
             r = r0.clone()
             part = torch.full((M, N // C, 2), float("nan"), dtype=torch.float32, device=dev)
@@ -379,6 +381,31 @@ def test_bf16_stream_producer_resq_bitexact(M, N, K, shifted, C):
             torch.cuda.synchronize()
             outs.append((r, part))
     finally:
-        ops.set_tuning("gemm_resq", 1)
-    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16)), "the bf16 stream"
-    assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32)), "chunk partials"
+        ops.set_tuning("gemm_resq", 2)
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0].view(torch.int16), o[0].view(torch.int16)), "the bf16 stream"
+        assert torch.equal(outs[0][1].view(torch.int32), o[1].view(torch.int32)), "chunk partials"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(18464, 1024, 1024), (2000, 1024, 512), (43840, 384, 384)])
+def test_bf16_residual_resq_modes_bitexact(M, N, K):
+    """A plain bf16-residual GEMM (no LayerNorm producer, separate output) on the 320 x 256 / 384 x 192
+    tile kernels: the three epilogue forms (gemm_resq 2 / 1 / 0) write the same bytes."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M + 3 * K)
+    a = _rand((M, K), g).to(torch.bfloat16).to(dev)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = _rand((N,), g, 0.1).to(torch.float32).to(dev)
+    r = _rand((M, N), g).to(torch.bfloat16).to(dev)
+    outs = []
+    try:
+        for on in (2, 1, 0):
+            ops.set_tuning("gemm_resq", on)
+            outs.append(ops.linear(a, w, bias=b, res=r))
+            torch.cuda.synchronize()
+    finally:
+        ops.set_tuning("gemm_resq", 2)
+    for o in outs[1:]:
+        assert torch.equal(outs[0].view(torch.int16), o.view(torch.int16))
