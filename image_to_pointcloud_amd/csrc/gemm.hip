@@ -349,15 +349,16 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       const int n = ncol0 + j * 16 + fq * 4;
       float v[4] = {acc[i][j][0] + bias4[j].x, acc[i][j][1] + bias4[j].y, acc[i][j][2] + bias4[j].z,
                     acc[i][j][3] + bias4[j].w};
-      if (p.rbias) {
+      if (!RQP && p.rbias) {
         const float4 bb = *reinterpret_cast<const float4*>(p.rbias + (int64_t)(mc / p.rb_g) * p.N + n);
         v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       }
-      if (p.tbl) {
+      if (!RQP && p.tbl) {
         const float4 bb = *reinterpret_cast<const float4*>(p.tbl + (int64_t)(mc % p.tbl_rows) * p.N + n);
         v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       }
-      if (p.act == 1) {
+      if (RQP) {
+      } else if (p.act == 1) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = gelu_erf(v[t]);
       } else if (p.act == 3) {
@@ -377,8 +378,11 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   const uint8_t* rq_cur = nullptr;
   if constexpr (RQP) {
     // this pass's rows landed: issued before the previous pass's >= ITS stores, which may stay in flight
+    if (pass == 1) STAMP(6);
     if (pass > 0 && rq.full) wait_vm<ITS>();
     else wait_vm<0>();
+    if (pass == 1) STAMP(5);
+    if (pass == NPASS - 1) STAMP(7);
     if (pass + 1 < NPASS) res_dma(pass + 1);
     rq_cur = rq.buf + ((pass & 1) * 8 + wid_q) * RQ_BYTES;
   } else if constexpr (RQ_OK) {
@@ -412,7 +416,10 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
     const int n = ncol0 + c8 * 8;
     int64_t off;
     int orow = 0;
-    if (p.ct_s > 0) {
+    if (RQP) {
+      orow = m;
+      off = (int64_t)m * p.ldc + n;
+    } else if (p.ct_s > 0) {
       const int hw = p.ct_h * p.ct_w;
       const int bi = m / hw;
       const int rem = m - bi * hw;
@@ -427,15 +434,15 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       orow = remap(m, p.o_g, p.o_gs, p.o_o);
       off = (int64_t)orow * p.ldc + n;
     }
-    if (p.res) {
+    if (RQP || p.res) {
       const int64_t roff = p.ct_s > 0 ? off : (int64_t)orow * p.ldr + n;
-      if (p.res_f32) {
+      if (!RQP && p.res_f32) {
         const float4 x0 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.res) + roff);
         const float4 x1 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.res) + roff + 4);
         v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
         v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
       } else {
-        const uint4 x = rq_cur ? *reinterpret_cast<const uint4*>(rq_cur + (r * LPR + c8) * 16)
+        const uint4 x = (RQP || rq_cur) ? *reinterpret_cast<const uint4*>(rq_cur + (r * LPR + c8) * 16)
                                : *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
         if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
@@ -453,15 +460,15 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         }
       }
     }
-    if (p.res2) {
+    if (!RQP && p.res2) {
       const int64_t roff = p.ct_s > 0 ? off : (int64_t)orow * p.ldr2 + n;
       const uint4 x = *reinterpret_cast<const uint4*>(p.res2 + roff);
       const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
 #pragma unroll
       for (int t = 0; t < 4; ++t) { v[2 * t] += __uint_as_float(q[t] << 16); v[2 * t + 1] += __uint_as_float(q[t] & 0xffff0000u); }
     }
-    if (p.c_f32 || p.lnp) {
-      if (p.c_f32) {
+    if ((!RQP && p.c_f32) || p.lnp) {
+      if (!RQP && p.c_f32) {
         float* c = static_cast<float*>(p.C) + off;
         *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -782,7 +789,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
     }
   }
   if constexpr (EP_RQ >= 1 && RQ_SHIFTS && NW == 8 && (TN == 64 || TN == 96)) {
-    if (rq.on && g_resq_dev(p) >= 2) {
+    // the RQ path's epilogue is compiled for exactly these calls (tile_epilogue<..., RQP>: no row bias,
+    // table, activation, second residual or fp32 output)
+    if (rq.on && g_resq_dev(p) >= 2 && p.act == 0 && !p.rbias && !p.tbl && !p.res2 && !p.c_f32) {
       float4 b4[RN];
 #pragma unroll
       for (int j = 0; j < RN; ++j)
@@ -823,8 +832,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
 // step (I2PC_GEMM_STAGGER / "gemm_stagger"; bit-identical either way)
 static thread_local int g_stagger = [] { const char* e = getenv("I2PC_GEMM_STAGGER"); return e ? atoi(e) : 1; }();
 // tile epilogue: a bf16 residual's rows staged in LDS one pass ahead (ResQ; I2PC_GEMM_RESQ / "gemm_resq");
-// 2 = the RQ path (struct ResQ): measured r06 in one process (tools/ab_pipeline.py), C2 19.022 -> 19.014 ms
-// per step, DA-v2 7.173 -> 7.121 ms, bit-identical
+// 2 = the RQ path (struct ResQ; its epilogue compiled without the generic one's runtime-skipped features):
+// measured r06 in one process (tools/ab_pipeline.py), C2 18.675 -> 18.347 ms per step, DA-v2 7.074 ->
+// 6.815 ms, bit-identical.  Per call (tools/stamps_tile.py): DPT-Large O 64.8 -> 53.4 us (epilogue phase 2
+// 47 K -> 19 K stamp cycles), FC2 172.5 -> 164.7 us; DA-v2 FC2 87.0 -> 71.7 us, O 46.8 -> 33.5 us
 static thread_local int g_resq = [] { const char* e = getenv("I2PC_GEMM_RESQ"); return e ? atoi(e) : 2; }();
 
 template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>

@@ -20,8 +20,9 @@ if mode == "lnp":
               out_bf16=torch.empty(m, n, dtype=torch.bfloat16, device=dev), ln_shift=torch.zeros(m, device=dev))
 elif mode == "lnpbf":   # the bf16 residual stream: res = out (bf16, in place) + res_shift, bf16 shifted output
     out = torch.randn(m, n, device=dev).to(torch.bfloat16)
-    kw = dict(res=out, res_shift=torch.zeros(m, device=dev), ln_part=torch.empty(m, n // 64, 2, device=dev),
-              ln_shift=torch.zeros(m, device=dev))
+    C = 64 if n % 256 == 0 else 32   # the networks' LayerNorm chunk (DA-v2's 384 columns: 32)
+    kw = dict(res=out, res_shift=torch.zeros(m, device=dev), ln_part=torch.empty(m, n // C, 2, device=dev),
+              ln_shift=torch.zeros(m, device=dev), ln_chunk=C)
 else:
     out = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
     kw = {}
@@ -53,3 +54,6 @@ end = a[:, 3] - t0
 q = lambda v: "/".join(f"{np.percentile(v, p):.0f}" for p in (5, 50, 95))
 print(f"blocks {nb} (cycles, p5/p50/p95): start {q(st)}  first stage {q(pro)}  K-loop {q(loop)} "
       f"(per K-step {np.median(loop) / (k // 64):.0f})  epi phase1 {q(p1)}  phase2 {q(p2)}  end {q(end)}  span {end.max()}")
+if (a[:, 5] > 0).all():
+    print(f"  RQ path: pass-0 phase 2 + pass-1 phase 1 {q(a[:, 6] - a[:, 4])}  pass-1 residual wait {q(a[:, 5] - a[:, 6])}  "
+          f"last pass start -> end {q(a[:, 3] - a[:, 7])}")
