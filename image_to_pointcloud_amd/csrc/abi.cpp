@@ -35,7 +35,7 @@ extern "C" int i2pc_set_tuning(const char* name, int value) {
       i2pc_misc_tune(name, value))
     return I2PC_OK;
   return i2pc::set_error(I2PC_EINVAL,
-                         "unknown tuning knob '%s' (gemm_tail, gemm_bn128, gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_lnp_stream, conv_halo, gelu_tanh, gemm_resq, gemm_tail160, gemm_stagger, "
+                         "unknown tuning knob '%s' (gemm_tail, gemm_bn128, gemm_splitk, gemm_split_tile, gemm_tile192, gemm_lnp_p, gemm_lnp_stream, conv_halo, gelu_tanh, gemm_resq, gemm_simple_epi, gemm_tail160, gemm_stagger, "
                          "unp_rows, unp_nt, unp_rpt, sel_windows, sel_parts, sel_rows, sel_lband, sel_scratch, attn_lazy, attn_scalar, attn_rb, "
                          "ln_f2, ln_apply_gs, resize_rows: include/i2pc.h)",
                          name);

@@ -113,6 +113,7 @@ struct Args {
   int dbg_drop;   // diagnostic (I2PC_GEMM_DROP_STORES=1): the persistent engine's output stores are issued to an
                   // empty buffer range (dropped), to measure what the stores cost the next tile's K-loop
   int resq;       // tile kernel: residual rows through LDS in the epilogue (knob "gemm_resq")
+  int simple;     // tile / halo kernels: the compiled-down epilogues where they apply (knob "gemm_simple_epi")
 };
 
 __device__ __forceinline__ int g_resq_dev(const Args& p) { return p.resq; }
@@ -254,9 +255,24 @@ struct SpTile {
   int ty0, tx0, tw, oh, ow;
 };
 
-template <int RM, int RN, int NI, bool SPAT = false, bool RQP = false>
+// RQP: the RQ path (struct ResQ).  SIMPLE 1 / 2: bias (+ activation: 2) (+ a bf16 residual) -> bf16 only
+// (simple_epilogue).  Both compile out the generic epilogue's other features: the code a call runs
+// through is then a fraction of the generic one's, whose runtime-skipped branches made a plain bf16
+// store epilogue of the 320 x 256 tile as slow as the LayerNorm producer's (tools/stamps_tile.py).
+// which compiled-down epilogue a call can use: 1 / 2 = tile_epilogue<..., SIMPLE> without / with an
+// activation, 0 = the generic one
+__device__ __forceinline__ int simple_kind(const Args& p) {
+  const bool s = !p.rbias && !p.tbl && !p.res2 && !p.c_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && !p.lnp &&
+                 !p.rsh && !(p.res && p.res_f32);
+  return s && p.simple ? (p.act == 0 ? 1 : 2) : 0;
+}
+
+template <int RM, int RN, int NI, bool SPAT = false, bool RQP = false, int SIMPLE = 0>
 __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int mrow0,
                                               int ncol0, float* lds, SpTile sp = SpTile{}, ResQ rq = ResQ{}) {
+  constexpr bool NO_EXTRA = RQP || SIMPLE != 0;     // no row bias, table, res2, fp32 out, scatter, row map
+  constexpr bool NO_ACT = RQP || SIMPLE == 1;
+  constexpr bool NO_LNP = SIMPLE != 0;
   constexpr int ni = NI;
   constexpr int TN = RN * 16;
   constexpr int U = TN / 4;                 // 16-B units per LDS row
@@ -276,7 +292,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
   // previous one's stores (r04, tools/diag12.sh: O 70 -> 68 us, DA-v2's 384 x 192 producer 100 -> 95 us).
   // Prefetching the residual rows as well was no faster: before phase 1 it pushed the 320 x 256 kernel
   // into scratch, after phase 1 (registers free) it measured 2-3 % slower (tools/diag17.sh).
-  constexpr bool PRE_SH = ITS <= 10 && !RQP;
+  constexpr bool PRE_SH = ITS <= 10 && !RQP && SIMPLE == 0;
   const bool pre = p.lnp && p.ct_s == 0;
   float pre_rs[PRE_SH ? ITS : 1], pre_sh[PRE_SH ? ITS : 1];
   if (PRE_SH && pre) {
@@ -349,15 +365,15 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       const int n = ncol0 + j * 16 + fq * 4;
       float v[4] = {acc[i][j][0] + bias4[j].x, acc[i][j][1] + bias4[j].y, acc[i][j][2] + bias4[j].z,
                     acc[i][j][3] + bias4[j].w};
-      if (!RQP && p.rbias) {
+      if (!NO_EXTRA && p.rbias) {
         const float4 bb = *reinterpret_cast<const float4*>(p.rbias + (int64_t)(mc / p.rb_g) * p.N + n);
         v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       }
-      if (!RQP && p.tbl) {
+      if (!NO_EXTRA && p.tbl) {
         const float4 bb = *reinterpret_cast<const float4*>(p.tbl + (int64_t)(mc % p.tbl_rows) * p.N + n);
         v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       }
-      if (RQP) {
+      if (NO_ACT) {
       } else if (p.act == 1) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = gelu_erf(v[t]);
@@ -416,7 +432,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
     const int n = ncol0 + c8 * 8;
     int64_t off;
     int orow = 0;
-    if (RQP) {
+    if (NO_EXTRA) {
       orow = m;
       off = (int64_t)m * p.ldc + n;
     } else if (p.ct_s > 0) {
@@ -435,8 +451,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       off = (int64_t)orow * p.ldc + n;
     }
     if (RQP || p.res) {
-      const int64_t roff = p.ct_s > 0 ? off : (int64_t)orow * p.ldr + n;
-      if (!RQP && p.res_f32) {
+      const int64_t roff = (!NO_EXTRA && p.ct_s > 0) ? off : (int64_t)orow * p.ldr + n;
+      if (!NO_EXTRA && p.res_f32) {
         const float4 x0 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.res) + roff);
         const float4 x1 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.res) + roff + 4);
         v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
@@ -445,7 +461,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         const uint4 x = (RQP || rq_cur) ? *reinterpret_cast<const uint4*>(rq_cur + (r * LPR + c8) * 16)
                                : *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.res) + roff);
         const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
-        if (p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
+        if (SIMPLE == 0 && p.rsh) {   // shifted bf16 residual stream: value = stored + its row's shift
           const float rs = RQP ? reinterpret_cast<const float*>(rq.rsl)[i0 * 16 + r]
                            : PRE_SH && pre ? pre_rs[PRE_SH ? it : 0]
                                            : __hip_atomic_load(p.rsh + orow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -460,20 +476,20 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         }
       }
     }
-    if (!RQP && p.res2) {
+    if (!NO_EXTRA && p.res2) {
       const int64_t roff = p.ct_s > 0 ? off : (int64_t)orow * p.ldr2 + n;
       const uint4 x = *reinterpret_cast<const uint4*>(p.res2 + roff);
       const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
 #pragma unroll
       for (int t = 0; t < 4; ++t) { v[2 * t] += __uint_as_float(q[t] << 16); v[2 * t + 1] += __uint_as_float(q[t] & 0xffff0000u); }
     }
-    if ((!RQP && p.c_f32) || p.lnp) {
-      if (!RQP && p.c_f32) {
+    if ((!NO_EXTRA && p.c_f32) || (!NO_LNP && p.lnp)) {
+      if (!NO_EXTRA && p.c_f32) {
         float* c = static_cast<float*>(p.C) + off;
         *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
       }
-      if constexpr (LPR % 4 == 0) {
+      if constexpr (LPR % 4 == 0 && !NO_LNP) {
         if (p.lnp) {
           // LayerNorm producer: the bf16 copy of out - shift[m], and (mean, M2) of each 64-column
           // chunk (= 8 lanes) of it, or of each 32-column chunk (4 lanes; lnc = 32)
@@ -820,11 +836,26 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
       return;
     }
   }
-  epi_passes<RM / EP_RM>([&](int pass) {
-    tile_epilogue<RM, RN, EP_RM>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
-                                 reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
-    __builtin_amdgcn_wave_barrier();
-  });
+  const int sk = simple_kind(p);
+  if (sk == 1) {
+    epi_passes<RM / EP_RM>([&](int pass) {
+      tile_epilogue<RM, RN, EP_RM, false, false, 1>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
+                                                    reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
+      __builtin_amdgcn_wave_barrier();
+    });
+  } else if (sk == 2) {
+    epi_passes<RM / EP_RM>([&](int pass) {
+      tile_epilogue<RM, RN, EP_RM, false, false, 2>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
+                                                    reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
+      __builtin_amdgcn_wave_barrier();
+    });
+  } else {
+    epi_passes<RM / EP_RM>([&](int pass) {
+      tile_epilogue<RM, RN, EP_RM>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
+                                   reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
+      __builtin_amdgcn_wave_barrier();
+    });
+  }
   STAMP(3);
 }
 
@@ -837,6 +868,9 @@ static thread_local int g_stagger = [] { const char* e = getenv("I2PC_GEMM_STAGG
 // 6.815 ms, bit-identical.  Per call (tools/stamps_tile.py): DPT-Large O 64.8 -> 53.4 us (epilogue phase 2
 // 47 K -> 19 K stamp cycles), FC2 172.5 -> 164.7 us; DA-v2 FC2 87.0 -> 71.7 us, O 46.8 -> 33.5 us
 static thread_local int g_resq = [] { const char* e = getenv("I2PC_GEMM_RESQ"); return e ? atoi(e) : 2; }();
+// tile / halo kernel epilogues compiled without the generic one's features for calls that use none of them
+// (bias, activation, bf16 residual, bf16 out; I2PC_GEMM_SIMPLE_EPI / "gemm_simple_epi"; bit-identical)
+static thread_local int g_simple = [] { const char* e = getenv("I2PC_GEMM_SIMPLE_EPI"); return e ? atoi(e) : 1; }();
 
 template <int BM, int BN, int WM, int WN, int KB, bool CONV, bool RELU_A>
 static void launch(const Args& p, hipStream_t s, int splits = 1) {
@@ -846,6 +880,7 @@ static void launch(const Args& p, hipStream_t s, int splits = 1) {
   q.group_m = group_m_for(q.tiles_m);
   q.stagger = g_stagger;
   q.resq = g_resq;
+  q.simple = g_simple;
   const int smem = 2 * (BM + BN) * KB * 2;
   auto kern = k_gemm<BM, BN, WM, WN, KB, CONV, RELU_A>;
   static bool attr = false;
@@ -991,11 +1026,26 @@ __global__ __launch_bounds__(64 * WM * WN) void k_conv3_halo(Args p) {
   constexpr int EP_RM = RM % EP_RM1 == 0 ? EP_RM1 : RM % (EP_RM1 - 1) == 0 ? EP_RM1 - 1 : 1;
   static_assert(EP_RM >= 1 && RM % EP_RM == 0, "epilogue LDS");
   const SpTile sp{b * p.coh * p.cow, y0, x0, TW, p.coh, p.cow};
-  epi_passes<RM / EP_RM>([&](int pass) {
-    tile_epilogue<RM, RN, EP_RM, true>(p, acc, pass * EP_RM, wm * TM, n0 + wn * TN,
-                                       reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN, sp);
-    __builtin_amdgcn_wave_barrier();
-  });
+  const int sk = simple_kind(p);
+  if (sk == 1) {
+    epi_passes<RM / EP_RM>([&](int pass) {
+      tile_epilogue<RM, RN, EP_RM, true, false, 1>(p, acc, pass * EP_RM, wm * TM, n0 + wn * TN,
+                                                   reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN, sp);
+      __builtin_amdgcn_wave_barrier();
+    });
+  } else if (sk == 2) {
+    epi_passes<RM / EP_RM>([&](int pass) {
+      tile_epilogue<RM, RN, EP_RM, true, false, 2>(p, acc, pass * EP_RM, wm * TM, n0 + wn * TN,
+                                                   reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN, sp);
+      __builtin_amdgcn_wave_barrier();
+    });
+  } else {
+    epi_passes<RM / EP_RM>([&](int pass) {
+      tile_epilogue<RM, RN, EP_RM, true>(p, acc, pass * EP_RM, wm * TM, n0 + wn * TN,
+                                         reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN, sp);
+      __builtin_amdgcn_wave_barrier();
+    });
+  }
 }
 
 template <int TH, int TW, int BN, int WM, int WN, bool RELU_A>
@@ -1009,7 +1059,9 @@ static void launch_halo(const Args& p, hipStream_t s) {
     attr = true;
   }
   const int tiles = p.cb * ((p.coh + TH - 1) / TH) * ((p.cow + TW - 1) / TW);
-  hipLaunchKernelGGL(kern, dim3(tiles, p.N / BN), dim3(64 * WM * WN), smem, s, p);
+  Args q = p;
+  q.simple = g_simple;
+  hipLaunchKernelGGL(kern, dim3(tiles, p.N / BN), dim3(64 * WM * WN), smem, s, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -2746,6 +2798,7 @@ bool i2pc_gemm_tune(const char* name, int value) {
   if (std::strcmp(name, "conv_halo") == 0) { i2pc::gemm::g_halo = value; return true; }
   if (std::strcmp(name, "gelu_tanh") == 0) { i2pc::gemm::g_gelu_tanh = value; return true; }
   if (std::strcmp(name, "gemm_resq") == 0) { i2pc::gemm::g_resq = value; return true; }
+  if (std::strcmp(name, "gemm_simple_epi") == 0) { i2pc::gemm::g_simple = value; return true; }
   if (std::strcmp(name, "gemm_tail160") == 0) { i2pc::gemm::g_tail160 = value; return true; }
   if (std::strcmp(name, "gemm_stagger") == 0) { i2pc::gemm::g_stagger = value; return true; }
   return false;

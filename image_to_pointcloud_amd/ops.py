@@ -137,7 +137,7 @@ def gemm_kernel_label(desc: GemmDesc) -> str:
 
 
 # every knob i2pc_set_tuning accepts (include/i2pc.h), checked by tests/test_abi.py
-TUNING_KNOBS = ("gemm_tail", "gemm_bn128", "gemm_splitk", "gemm_split_tile", "gemm_tile192", "gemm_lnp_p", "gemm_lnp_stream", "conv_halo", "gelu_tanh", "gemm_resq", "gemm_tail160",
+TUNING_KNOBS = ("gemm_tail", "gemm_bn128", "gemm_splitk", "gemm_split_tile", "gemm_tile192", "gemm_lnp_p", "gemm_lnp_stream", "conv_halo", "gelu_tanh", "gemm_resq", "gemm_simple_epi", "gemm_tail160",
                 "gemm_stagger", "unp_rows",
                 "unp_nt", "unp_rpt", "sel_windows", "sel_parts", "sel_rows", "sel_lband", "sel_scratch", "attn_lazy", "attn_scalar",
                 "attn_rb", "ln_f2", "ln_apply_gs", "resize_rows")

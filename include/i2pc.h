@@ -406,6 +406,9 @@ int i2pc_gemm_set_engine(int mode);
  *                 one epilogue pass ahead (LDS-DMA, one wait per pass); 2 = also the row shifts in LDS
  *                 and the bias in registers before the first pass, and each pass's wait counted past the
  *                 previous pass's stores (default); 0 = plain loads in the epilogue; bit-identical
+ *   "gemm_simple_epi" 1 = tile / halo-conv kernel calls whose epilogue is bias (+ activation) (+ a bf16
+ *                 residual) -> bf16 run an epilogue compiled without the generic one's other features
+ *                 (default), 0 = the generic epilogue; bit-identical
  *   "gemm_tail160" 1 = a persistent GEMM's last partial round as 160 x 256 tiles where 256 x 128
  *                 tiles do not fit one round (DPT-Large FC1)
  *   "gemm_stagger" 1 = in the 8-wave GEMM kernels waves 4-7 issue the next K-stage's loads half-way

@@ -103,7 +103,7 @@ def test_tuning_knob_names():
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libi2pc.so not built")
     from image_to_pointcloud_amd import ops
-    defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "gemm_split_tile": 0, "gemm_tile192": 1, "gemm_lnp_p": 0, "gemm_lnp_stream": 0, "conv_halo": 3, "gelu_tanh": 1, "gemm_resq": 2, "gemm_tail160": 1,
+    defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "gemm_split_tile": 0, "gemm_tile192": 1, "gemm_lnp_p": 0, "gemm_lnp_stream": 0, "conv_halo": 3, "gelu_tanh": 1, "gemm_resq": 2, "gemm_simple_epi": 1, "gemm_tail160": 1,
                 "gemm_stagger": 1,
                 "unp_rows": 1, "unp_nt": 1, "unp_rpt": 8, "sel_windows": 1, "sel_parts": 0, "sel_rows": 16,
                 "sel_lband": -1, "sel_scratch": 0, "attn_lazy": 1, "attn_scalar": 1, "attn_rb": 1, "ln_f2": 1, "ln_apply_gs": 0, "resize_rows": 1}

@@ -385,3 +385,45 @@ def test_conv3_halo_bitexact(B, H, W, Co):
         if "res2" in kw:
             r = r + res2.float()
         assert _fro(outs[0], r) <= 8e-3
+
+
+@pytest.mark.parametrize("case", ["linear", "linear_384", "conv", "halo"])
+def test_simple_epilogue_bitexact(case):
+    """The tile / halo-conv kernels' compiled-down epilogues (gemm_simple_epi 1: bias, activation, a bf16
+    residual, bf16 out) write the bytes of the generic epilogue (gemm_simple_epi 0) for every combination
+    they take; calls they do not take (a second residual) run the generic one either way."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(len(case))
+    calls = []
+    if case in ("linear", "linear_384"):
+        M, N, K = (2000, 1024, 512) if case == "linear" else (43840, 384, 384)
+        a = _bf(torch.randn(M, K, generator=g)).to(dev)
+        w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+        b = (torch.randn(N, generator=g) * 0.1).to(dev)
+        r = _bf(torch.randn(M, N, generator=g)).to(dev)
+        for act in (None, "relu", "gelu"):
+            for res in (None, r):
+                calls.append(lambda act=act, res=res: ops.linear(a, w, bias=b, act=act, res=res))
+    else:
+        B, H, W, C, Co = (4, 48, 40, 256, 256) if case == "conv" else (3, 37, 29, 64, 64)
+        x = _bf(torch.randn(B, H, W, C, generator=g)).to(dev)
+        res = _bf(torch.randn(B, H, W, Co, generator=g)).to(dev)
+        res2 = _bf(torch.randn(B, H, W, Co, generator=g)).to(dev)
+        wp = _pack_conv((torch.randn(Co, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(dev))
+        b = (torch.randn(Co, generator=g) * 0.1).to(dev)
+        for kw in (dict(relu_in=True, act="relu"), dict(res=res), dict(res=res, res2=res2), dict()):
+            calls.append(lambda kw=kw: ops.conv2d(x, wp, bias=b, **kw))
+    try:
+        if case != "halo":
+            ops.set_gemm_engine(1)          # the tile kernel
+        for fn in calls:
+            outs = []
+            for on in (1, 0):
+                ops.set_tuning("gemm_simple_epi", on)
+                outs.append(fn().clone())
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1])
+    finally:
+        ops.set_tuning("gemm_simple_epi", 1)
+        ops.set_gemm_engine(0)

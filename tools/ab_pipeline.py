@@ -34,7 +34,7 @@ for v in a.variant or ["base:"]:
     name, _, kv = v.partition(":")
     knobs = dict((k, int(x)) for k, x in (p.split("=") for p in kv.split(",") if p))
     variants.append((name, knobs))
-defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "gemm_split_tile": 0, "gemm_tile192": 1, "gemm_lnp_p": 0, "gemm_lnp_stream": 0, "conv_halo": 3, "gelu_tanh": 1, "gemm_resq": 2, "gemm_tail160": 1, "gemm_stagger": 1, "unp_rows": 1, "unp_nt": 1, "unp_rpt": 8, "attn_lazy": 1, "attn_scalar": 1, "attn_rb": 1, "ln_f2": 1, "resize_rows": 1, "engine": 0}
+defaults = {"gemm_tail": 1, "gemm_bn128": 1, "gemm_splitk": 1, "gemm_split_tile": 0, "gemm_tile192": 1, "gemm_lnp_p": 0, "gemm_lnp_stream": 0, "conv_halo": 3, "gelu_tanh": 1, "gemm_resq": 2, "gemm_simple_epi": 1, "gemm_tail160": 1, "gemm_stagger": 1, "unp_rows": 1, "unp_nt": 1, "unp_rpt": 8, "attn_lazy": 1, "attn_scalar": 1, "attn_rb": 1, "ln_f2": 1, "resize_rows": 1, "engine": 0}
 
 
 def apply(knobs):
