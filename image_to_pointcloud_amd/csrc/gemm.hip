@@ -260,18 +260,20 @@ struct SpTile {
 // through is then a fraction of the generic one's, whose runtime-skipped branches made a plain bf16
 // store epilogue of the 320 x 256 tile as slow as the LayerNorm producer's (tools/stamps_tile.py).
 // which compiled-down epilogue a call can use: 1 / 2 = tile_epilogue<..., SIMPLE> without / with an
-// activation, 0 = the generic one
+// activation, 3 = raw fp32 rows (split-K partial sums: no bias, activation or residual), 0 = the generic one
 __device__ __forceinline__ int simple_kind(const Args& p) {
-  const bool s = !p.rbias && !p.tbl && !p.res2 && !p.c_f32 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && !p.lnp &&
-                 !p.rsh && !(p.res && p.res_f32);
-  return s && p.simple ? (p.act == 0 ? 1 : 2) : 0;
+  if (!p.simple) return 0;
+  const bool s = !p.rbias && !p.tbl && !p.res2 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && !p.lnp && !p.rsh;
+  if (s && p.c_f32) return !p.res && !p.bias && p.act == 0 ? 3 : 0;
+  return s && !(p.res && p.res_f32) ? (p.act == 0 ? 1 : 2) : 0;
 }
 
 template <int RM, int RN, int NI, bool SPAT = false, bool RQP = false, int SIMPLE = 0>
 __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN], int i0, int mrow0,
                                               int ncol0, float* lds, SpTile sp = SpTile{}, ResQ rq = ResQ{}) {
   constexpr bool NO_EXTRA = RQP || SIMPLE != 0;     // no row bias, table, res2, fp32 out, scatter, row map
-  constexpr bool NO_ACT = RQP || SIMPLE == 1;
+  constexpr bool NO_ACT = RQP || SIMPLE == 1 || SIMPLE == 3;
+  constexpr bool F32_ONLY = SIMPLE == 3;            // raw fp32 rows
   constexpr bool NO_LNP = SIMPLE != 0;
   constexpr int ni = NI;
   constexpr int TN = RN * 16;
@@ -450,7 +452,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       orow = remap(m, p.o_g, p.o_gs, p.o_o);
       off = (int64_t)orow * p.ldc + n;
     }
-    if (RQP || p.res) {
+    if (!F32_ONLY && (RQP || p.res)) {
       const int64_t roff = (!NO_EXTRA && p.ct_s > 0) ? off : (int64_t)orow * p.ldr + n;
       if (!NO_EXTRA && p.res_f32) {
         const float4 x0 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.res) + roff);
@@ -483,8 +485,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
 #pragma unroll
       for (int t = 0; t < 4; ++t) { v[2 * t] += __uint_as_float(q[t] << 16); v[2 * t + 1] += __uint_as_float(q[t] & 0xffff0000u); }
     }
-    if ((!NO_EXTRA && p.c_f32) || (!NO_LNP && p.lnp)) {
-      if (!NO_EXTRA && p.c_f32) {
+    if (F32_ONLY || (!NO_EXTRA && p.c_f32) || (!NO_LNP && p.lnp)) {
+      if (F32_ONLY || (!NO_EXTRA && p.c_f32)) {
         float* c = static_cast<float*>(p.C) + off;
         *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -840,6 +842,12 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm(Args p) {
   if (sk == 1) {
     epi_passes<RM / EP_RM>([&](int pass) {
       tile_epilogue<RM, RN, EP_RM, false, false, 1>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
+                                                    reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
+      __builtin_amdgcn_wave_barrier();
+    });
+  } else if (sk == 3) {
+    epi_passes<RM / EP_RM>([&](int pass) {
+      tile_epilogue<RM, RN, EP_RM, false, false, 3>(p, acc, pass * EP_RM, m0 + wm * TM, n0 + wn * TN,
                                                     reinterpret_cast<float*>(smem) + wid * EP_RM * 16 * TN);
       __builtin_amdgcn_wave_barrier();
     });

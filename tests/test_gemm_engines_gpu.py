@@ -387,16 +387,26 @@ def test_conv3_halo_bitexact(B, H, W, Co):
         assert _fro(outs[0], r) <= 8e-3
 
 
-@pytest.mark.parametrize("case", ["linear", "linear_384", "conv", "halo"])
+@pytest.mark.parametrize("case", ["linear", "linear_384", "conv", "halo", "splitk"])
 def test_simple_epilogue_bitexact(case):
     """The tile / halo-conv kernels' compiled-down epilogues (gemm_simple_epi 1: bias, activation, a bf16
     residual, bf16 out) write the bytes of the generic epilogue (gemm_simple_epi 0) for every combination
-    they take; calls they do not take (a second residual) run the generic one either way."""
+    they take, and the raw fp32 one of split-K's partial sums; calls they do not take (a second residual)
+    run the generic one either way."""
     ops = _ops()
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(len(case))
     calls = []
-    if case in ("linear", "linear_384"):
+    if case == "splitk":
+        M, N, K = 300, 256, 4096
+        a = _bf(torch.randn(M, K, generator=g)).to(dev)
+        w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+        b = (torch.randn(N, generator=g) * 0.1).to(dev)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        assert "split-K" in ops.gemm_kernel_label(_desc_of(ops, a, w, b, out))
+        for act in (None, "gelu"):
+            calls.append(lambda act=act: ops.linear(a, w, bias=b, act=act))
+    elif case in ("linear", "linear_384"):
         M, N, K = (2000, 1024, 512) if case == "linear" else (43840, 384, 384)
         a = _bf(torch.randn(M, K, generator=g)).to(dev)
         w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
@@ -415,7 +425,7 @@ def test_simple_epilogue_bitexact(case):
         for kw in (dict(relu_in=True, act="relu"), dict(res=res), dict(res=res, res2=res2), dict()):
             calls.append(lambda kw=kw: ops.conv2d(x, wp, bias=b, **kw))
     try:
-        if case != "halo":
+        if case not in ("halo", "splitk"):
             ops.set_gemm_engine(1)          # the tile kernel
         for fn in calls:
             outs = []
