@@ -255,7 +255,7 @@ struct SpTile {
   int ty0, tx0, tw, oh, ow;
 };
 
-// RQP: the RQ path (struct ResQ).  SIMPLE 1 / 2: bias (+ activation: 2) (+ a bf16 residual) -> bf16 only
+// RQP: the RQ path (struct ResQ).  SIMPLE 1 / 2: bias (+ activation: 2) (+ bf16 residuals) -> bf16 only
 // (simple_epilogue).  Both compile out the generic epilogue's other features: the code a call runs
 // through is then a fraction of the generic one's, whose runtime-skipped branches made a plain bf16
 // store epilogue of the 320 x 256 tile as slow as the LayerNorm producer's (tools/stamps_tile.py).
@@ -263,8 +263,8 @@ struct SpTile {
 // activation, 3 = raw fp32 rows (split-K partial sums: no bias, activation or residual), 0 = the generic one
 __device__ __forceinline__ int simple_kind(const Args& p) {
   if (!p.simple) return 0;
-  const bool s = !p.rbias && !p.tbl && !p.res2 && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && !p.lnp && !p.rsh;
-  if (s && p.c_f32) return !p.res && !p.bias && p.act == 0 ? 3 : 0;
+  const bool s = !p.rbias && !p.tbl && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && !p.lnp && !p.rsh;
+  if (s && p.c_f32) return !p.res && !p.res2 && !p.bias && p.act == 0 ? 3 : 0;
   return s && !(p.res && p.res_f32) ? (p.act == 0 ? 1 : 2) : 0;
 }
 
@@ -478,8 +478,8 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
         }
       }
     }
-    if (!NO_EXTRA && p.res2) {
-      const int64_t roff = p.ct_s > 0 ? off : (int64_t)orow * p.ldr2 + n;
+    if ((!NO_EXTRA || SIMPLE == 1 || SIMPLE == 2) && p.res2) {
+      const int64_t roff = (!NO_EXTRA && p.ct_s > 0) ? off : (int64_t)orow * p.ldr2 + n;
       const uint4 x = *reinterpret_cast<const uint4*>(p.res2 + roff);
       const uint32_t* q = reinterpret_cast<const uint32_t*>(&x);
 #pragma unroll

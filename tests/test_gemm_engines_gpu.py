@@ -391,8 +391,7 @@ def test_conv3_halo_bitexact(B, H, W, Co):
 def test_simple_epilogue_bitexact(case):
     """The tile / halo-conv kernels' compiled-down epilogues (gemm_simple_epi 1: bias, activation, a bf16
     residual, bf16 out) write the bytes of the generic epilogue (gemm_simple_epi 0) for every combination
-    they take, and the raw fp32 one of split-K's partial sums; calls they do not take (a second residual)
-    run the generic one either way."""
+    they take (a second bf16 residual included), and the raw fp32 one of split-K's partial sums."""
     ops = _ops()
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(len(case))
