@@ -260,11 +260,12 @@ struct SpTile {
 // through is then a fraction of the generic one's, whose runtime-skipped branches made a plain bf16
 // store epilogue of the 320 x 256 tile as slow as the LayerNorm producer's (tools/stamps_tile.py).
 // which compiled-down epilogue a call can use: 1 / 2 = tile_epilogue<..., SIMPLE> without / with an
-// activation, 3 = raw fp32 rows (split-K partial sums: no bias, activation or residual), 0 = the generic one
+// activation, 3 = fp32 rows (+ bias) (+ an fp32 residual), no activation (split-K partial sums, the fp32
+// residual stream's attention-out / FC2 of DPT-Hybrid), 0 = the generic one
 __device__ __forceinline__ int simple_kind(const Args& p) {
   if (!p.simple) return 0;
   const bool s = !p.rbias && !p.tbl && p.ct_s == 0 && p.o_g == 0 && p.o_o == 0 && !p.lnp && !p.rsh;
-  if (s && p.c_f32) return !p.res && !p.res2 && !p.bias && p.act == 0 ? 3 : 0;
+  if (s && p.c_f32) return (!p.res || p.res_f32) && !p.res2 && p.act == 0 ? 3 : 0;
   return s && !(p.res && p.res_f32) ? (p.act == 0 ? 1 : 2) : 0;
 }
 
@@ -273,7 +274,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
                                               int ncol0, float* lds, SpTile sp = SpTile{}, ResQ rq = ResQ{}) {
   constexpr bool NO_EXTRA = RQP || SIMPLE != 0;     // no row bias, table, res2, fp32 out, scatter, row map
   constexpr bool NO_ACT = RQP || SIMPLE == 1 || SIMPLE == 3;
-  constexpr bool F32_ONLY = SIMPLE == 3;            // raw fp32 rows
+  constexpr bool F32_ONLY = SIMPLE == 3;            // fp32 rows (+ an fp32 residual)
   constexpr bool NO_LNP = SIMPLE != 0;
   constexpr int ni = NI;
   constexpr int TN = RN * 16;
@@ -452,9 +453,9 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       orow = remap(m, p.o_g, p.o_gs, p.o_o);
       off = (int64_t)orow * p.ldc + n;
     }
-    if (!F32_ONLY && (RQP || p.res)) {
+    if (RQP || p.res) {
       const int64_t roff = (!NO_EXTRA && p.ct_s > 0) ? off : (int64_t)orow * p.ldr + n;
-      if (!NO_EXTRA && p.res_f32) {
+      if (F32_ONLY || (!NO_EXTRA && p.res_f32)) {
         const float4 x0 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.res) + roff);
         const float4 x1 = *reinterpret_cast<const float4*>(static_cast<const float*>(p.res) + roff + 4);
         v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;

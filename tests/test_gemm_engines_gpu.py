@@ -387,16 +387,28 @@ def test_conv3_halo_bitexact(B, H, W, Co):
         assert _fro(outs[0], r) <= 8e-3
 
 
-@pytest.mark.parametrize("case", ["linear", "linear_384", "conv", "halo", "splitk"])
+@pytest.mark.parametrize("case", ["linear", "linear_384", "conv", "halo", "splitk", "f32res"])
 def test_simple_epilogue_bitexact(case):
     """The tile / halo-conv kernels' compiled-down epilogues (gemm_simple_epi 1: bias, activation, a bf16
     residual, bf16 out) write the bytes of the generic epilogue (gemm_simple_epi 0) for every combination
-    they take (a second bf16 residual included), and the raw fp32 one of split-K's partial sums."""
+    they take (a second bf16 residual included), and the fp32 one (split-K's partial sums; bias + an fp32
+    residual stream in place, DPT-Hybrid's bf16 FC2)."""
     ops = _ops()
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(len(case))
     calls = []
-    if case == "splitk":
+    if case == "f32res":
+        M, N, K = 3000, 768, 1024
+        a = _bf(torch.randn(M, K, generator=g)).to(dev)
+        w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
+        b = (torch.randn(N, generator=g) * 0.1).to(dev)
+        x0 = torch.randn(M, N, generator=g).to(dev)
+
+        def inplace():
+            x = x0.clone()
+            return ops.linear(a, w, bias=b, res=x, out=x)
+        calls.append(inplace)
+    elif case == "splitk":
         M, N, K = 300, 256, 4096
         a = _bf(torch.randn(M, K, generator=g)).to(dev)
         w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(dev)
@@ -424,7 +436,7 @@ def test_simple_epilogue_bitexact(case):
         for kw in (dict(relu_in=True, act="relu"), dict(res=res), dict(res=res, res2=res2), dict()):
             calls.append(lambda kw=kw: ops.conv2d(x, wp, bias=b, **kw))
     try:
-        if case not in ("halo", "splitk"):
+        if case not in ("halo", "splitk", "f32res"):
             ops.set_gemm_engine(1)          # the tile kernel
         for fn in calls:
             outs = []
