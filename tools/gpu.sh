@@ -8,6 +8,8 @@
 #                              pmc_traffic.json,bench.json}, copied to gpurun_out/ (copy them back to profiles/)
 #   sq <tag> [bench args]      SQ counters (two passes of 8) of one eager step for attention and the persistent GEMM
 #   full                       check + profile of C2 (dpt-large-bf16) and C5 (dpt-hybrid-fp8, batch 64)
+#   final1 / final2            the round's record: check (+ profiles/<round>_bench_check.json) and the C2 high /
+#                              medium profiles; the DA-v2 and C5 profiles
 #   bench                      the default bench line (with the CPU baseline), as the driver runs it
 #   ab-pipe [args]             tools/ab_pipeline.py: kernel-selection knobs A/B on the bench pipeline, one process
 #   census [args]              tools/gemm_census.py: every network launch with shape, kernel and rate
@@ -92,6 +94,9 @@ case "$TASK" in
   profile) profile "$@" ;;
   sq) sq "$@" ;;
   full) check && profile dpt-large-bf16 && profile dpt-hybrid-fp8 --model dpt-hybrid --batch 64 ;;
+  final1) check && cp gpurun_out/bench.json profiles/${R}_bench_check.json && cp gpurun_out/bench.json gpurun_out/${R}_bench_check.json \
+          && profile dpt-large-bf16 && profile dpt-large-bf16-medium --density medium ;;
+  final2) profile depth-anything-v2-small-bf16 --model depth-anything-v2 && profile dpt-hybrid-fp8 --model dpt-hybrid --batch 64 ;;
   bench)
     timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err
     rc=$?; cut -c1-400 gpurun_out/bench_default.json; exit $rc ;;
