@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void k_stem_im2col(const float* __restrict__ x
             v[h] = x[(((int64_t)b * 3 + c) * H + iy) * W + ix];
         }
       }
-      w[e / 2] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      w[e / 2] = pk2bf(v[0], v[1]);
     }
     *reinterpret_cast<uint4*>(out + (int64_t)m * kp + k0) = make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -271,10 +271,10 @@ __global__ __launch_bounds__(256) void k_gn_apply(GnOperand a, GnOperand r, int 
         for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       }
       uint4 o;
-      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-      o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      o.x = pk2bf(v[0], v[1]);
+      o.y = pk2bf(v[2], v[3]);
+      o.z = pk2bf(v[4], v[5]);
+      o.w = pk2bf(v[6], v[7]);
       *reinterpret_cast<uint4*>(y + base + (int64_t)p * C) = o;
     }
   }
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256) void k_stem_im2col_lds(const float* __restrict
     for (int e = 0; e < 8; e += 2) {
       const float v0 = off[e] >= 0 ? win[off[e] + 2 * ml] : 0.f;
       const float v1 = off[e + 1] >= 0 ? win[off[e + 1] + 2 * ml] : 0.f;
-      w[e / 2] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+      w[e / 2] = pk2bf(v0, v1);
     }
     *reinterpret_cast<uint4*>(ob + (int64_t)ml * kp) = make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -383,10 +383,10 @@ __global__ __launch_bounds__(256) void k_maxpool(const bf16_t* __restrict__ x, i
       for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], 0.f);
     }
     uint4 o;
-    o.x = (uint32_t)f2bf(m[0]) | ((uint32_t)f2bf(m[1]) << 16);
-    o.y = (uint32_t)f2bf(m[2]) | ((uint32_t)f2bf(m[3]) << 16);
-    o.z = (uint32_t)f2bf(m[4]) | ((uint32_t)f2bf(m[5]) << 16);
-    o.w = (uint32_t)f2bf(m[6]) | ((uint32_t)f2bf(m[7]) << 16);
+    o.x = pk2bf(m[0], m[1]);
+    o.y = pk2bf(m[2], m[3]);
+    o.z = pk2bf(m[4], m[5]);
+    o.w = pk2bf(m[6], m[7]);
     *reinterpret_cast<uint4*>(y + (int64_t)pix * C + c0) = o;
   }
 }

@@ -25,6 +25,14 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// two floats -> packed bf16 pair (low = a) in one v_cvt_pk_bf16_f32 (RNE, the same bits as two scalar
+// (__bf16) conversions; the scalar pair costs a convert each plus a shift and an or)
+__device__ __forceinline__ uint32_t pk2bf(float a, float b) {
+  typedef float pk2bf_f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 pk2bf_b2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(pk2bf_f2{a, b}, pk2bf_b2));
+}
+
 constexpr int kWave = 64;
 
 }  // namespace i2pc

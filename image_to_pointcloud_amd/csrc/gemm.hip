@@ -504,10 +504,10 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
 #pragma unroll
           for (int t = 0; t < 8; ++t) u[t] = v[t] - shf;
           uint4 o;
-          o.x = (uint32_t)f2bf(u[0]) | ((uint32_t)f2bf(u[1]) << 16);
-          o.y = (uint32_t)f2bf(u[2]) | ((uint32_t)f2bf(u[3]) << 16);
-          o.z = (uint32_t)f2bf(u[4]) | ((uint32_t)f2bf(u[5]) << 16);
-          o.w = (uint32_t)f2bf(u[6]) | ((uint32_t)f2bf(u[7]) << 16);
+          o.x = pk2bf(u[0], u[1]);
+          o.y = pk2bf(u[2], u[3]);
+          o.z = pk2bf(u[4], u[5]);
+          o.w = pk2bf(u[6], u[7]);
           *reinterpret_cast<uint4*>(p.cbf + (int64_t)m * p.ldcb + n) = o;
           // chunk sums across the row's lanes by DPP (one VALU each) instead of ds_bpermute round trips:
           // lane ^ 1, lane ^ 2 inside a quad, then the mirrored lane of the 8-lane group (7 - lane: the
@@ -532,10 +532,10 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, f32x4 (&acc)[RM][RN
       }
     } else {
       uint4 o;
-      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-      o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      o.x = pk2bf(v[0], v[1]);
+      o.y = pk2bf(v[2], v[3]);
+      o.z = pk2bf(v[4], v[5]);
+      o.w = pk2bf(v[6], v[7]);
       *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + off) = o;
     }
   }
@@ -605,8 +605,8 @@ __device__ __forceinline__ void epilogue4(const Args& p, int m, int n, float v[4
     *reinterpret_cast<float4*>(static_cast<float*>(p.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
   } else {
     uint2 o;
-    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.x = pk2bf(v[0], v[1]);
+    o.y = pk2bf(v[2], v[3]);
     *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + off) = o;
   }
 }
@@ -1127,7 +1127,7 @@ __device__ __forceinline__ void grouped(const Args& p, int tile, int& tm, int& t
 }
 
 __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return pk2bf(a, b);
 }
 
 template <int ACT>

@@ -20,7 +20,7 @@ __device__ __forceinline__ bf16_t f2bf(float x) {
   __bf16 b = (__bf16)x;
   return *reinterpret_cast<bf16_t*>(&b);
 }
-__device__ __forceinline__ uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) { return pk2bf(a, b); }
 
 __device__ __forceinline__ float wave_sum(float x) {
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256) void k_ln_apply(const uint4* __restrict__ x, i
     for (int t = 0; t < 4; ++t) {
       const float lo = __builtin_fmaf(g[2 * t], __builtin_fmaf(__uint_as_float(q[t] << 16), s.x, s.y), b[2 * t]);
       const float hi = __builtin_fmaf(g[2 * t + 1], __builtin_fmaf(__uint_as_float(q[t] & 0xffff0000u), s.x, s.y), b[2 * t + 1]);
-      o[t] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+      o[t] = pk2bf(lo, hi);
     }
     y[r * ldy8 + c] = make_uint4(o[0], o[1], o[2], o[3]);
   }
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256) void k_ln_apply_gs(const uint4* __restrict__ x
     for (int t = 0; t < 4; ++t) {
       const float lo = __builtin_fmaf(g[2 * t], __builtin_fmaf(__uint_as_float(q[t] << 16), s.x, s.y), b[2 * t]);
       const float hi = __builtin_fmaf(g[2 * t + 1], __builtin_fmaf(__uint_as_float(q[t] & 0xffff0000u), s.x, s.y), b[2 * t + 1]);
-      o[t] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+      o[t] = pk2bf(lo, hi);
     }
     y[r * ldy8 + c] = make_uint4(o[0], o[1], o[2], o[3]);
   }
