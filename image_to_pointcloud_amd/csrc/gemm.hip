@@ -1683,8 +1683,10 @@ __global__ __launch_bounds__(512) void k_gemm_p(Args p) {
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_a)::"memory");
 #endif
       // stage g landed: everything issued after it (the previous epilogue) may stay in flight
-      if (kt == 0 && after_epi) {
+      if (kt == 0 && after_epi && !(EPI == EPI_LNF && BN == 128)) {
         // any count <= E_ALL is safe (in-order completion); use the largest available
+        // (not on the LN-fold consumer's 256 x 128 tiles: its column sums read back wrong at one
+        // within-wave column of some tiles, run to run, with the counted wait -- r06, tools/probes/det_lnf2.py)
         if constexpr (E_ALL >= 63) I2PC_WAIT_VM(63);
         else if constexpr (E_ALL >= 48) I2PC_WAIT_VM(48);
         else if constexpr (E_ALL >= 40) I2PC_WAIT_VM(40);
@@ -2098,9 +2100,13 @@ static void launch_p(const Args& p, hipStream_t s) {
   }
   static const int drop = [] { const char* e = getenv("I2PC_GEMM_DROP_STORES"); return e ? atoi(e) : 0; }();
   q.dbg_drop = drop;
-  q.stagger = g_stagger;
+  // (the LN-fold consumer on 256 x 128 tiles -- DA-v2's QKV, N = 1152 -- returned run-to-run different
+  // values with the stagger at one within-wave column (12: j 0, fq 3, e 0) of some tiles: r06,
+  // tools/probes/det_lnf.py; the stagger off there made every call identical; root cause not found)
+  q.stagger = g_stagger && !(EPI == pers::EPI_LNF && BN == 128);
   const int tiles = q.tiles_m * q.tiles_n;
-  const int grid = std::min(tiles, num_cus());
+  // (the 256 x 128 LN-fold instance: one tile per workgroup, see run_persistent)
+  const int grid = EPI == pers::EPI_LNF && BN == 128 ? tiles : std::min(tiles, num_cus());
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), smem, s, q);
 }
 
@@ -2396,7 +2402,28 @@ static int run_persistent(const Plan& pl, const Args& p, hipStream_t s) {
   if (pl.bn == 128) {   // plan: EPI_PLAIN (or EPI_LNF), no ReLU on A
     if constexpr (!RELU_A) {
       if constexpr (!CONV) {
-        if (pl.epi == EPI_LNF) { launch_p<256, false, false, EPI_LNF, 128>(p, s); return check_launch("gemm"); }
+        if (pl.epi == EPI_LNF) {
+          // N = 256 k + 128 (DA-v2's QKV, 1152): the 256-multiple part on 256 x 256 tiles, the last 128
+          // columns on 256 x 128 tiles, one tile per workgroup (launch_p).  r06: the 256 x 128 LN-fold
+          // instance returned run-to-run different column-sum terms at one within-wave column of some
+          // tiles once a workgroup walked more than one tile (tools/probes/det_lnf.py, det_lnf2.py);
+          // with one tile per workgroup every call is identical.  Same per-output arithmetic either way.
+          if (p.N > 128) {
+            const int nb = p.N - 128;
+            Args pa = p, pb = p;
+            pa.N = nb;
+            pb.N = 128;
+            pb.W = p.W + (int64_t)nb * p.ldw;
+            pb.C = static_cast<bf16_t*>(p.C) + nb;
+            pb.bias = p.bias ? p.bias + nb : nullptr;
+            pb.csum = p.csum + nb;
+            launch_p<256, false, false, EPI_LNF>(pa, s);
+            launch_p<256, false, false, EPI_LNF, 128>(pb, s);
+            return check_launch("gemm (LN fold, N = 256 k + 128)");
+          }
+          launch_p<256, false, false, EPI_LNF, 128>(p, s);
+          return check_launch("gemm");
+        }
       }
       launch_p<256, CONV, false, EPI_PLAIN, 128>(p, s);
       return check_launch("gemm");

@@ -88,3 +88,25 @@ def test_resize_bilinear_matches_torch(B, h, w, c, oh, ow, ac):
                                           align_corners=ac).permute(0, 2, 3, 1) + add.float()
     err = (got - ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("B", [4, 32])
+def test_depth_anything_pipeline_run_to_run(B):
+    """Depth-Anything-V2-Small through the bench pipeline (1024^2, seeded weights) returns the same depth,
+    points and bounds on every run in one process (r06: the LN-fold QKV on 256 x 128 tiles did not;
+    tools/probes/det_da.py)."""
+    import bench
+    from image_to_pointcloud_amd.pipeline import PointCloudPipeline
+    dev = torch.device("cuda")
+    pipe = PointCloudPipeline(B, 1024, 1024, spec=bench._spec("depth-anything-v2"), density="high", device=dev, seed=0)
+    images = bench._images(B, 1024, 0, dev)
+    ref = None
+    for _ in range(3):
+        out = pipe.run(images)
+        torch.cuda.synchronize()
+        got = (pipe.depth.clone(), out.xyz.clone(), out.bbox.clone())
+        if ref is None:
+            ref = got
+            continue
+        for a, b in zip(ref, got):
+            assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))

@@ -409,3 +409,28 @@ def test_bf16_residual_resq_modes_bitexact(M, N, K):
         ops.set_tuning("gemm_resq", 2)
     for o in outs[1:]:
         assert torch.equal(outs[0].view(torch.int16), o.view(torch.int16))
+
+
+@pytest.mark.parametrize("M,N,K,act", [(5480, 1152, 384, None), (43840, 1152, 384, None), (5480, 1536, 384, "gelu"),
+                                       (2308, 3072, 1024, None)])
+def test_ln_fold_consumer_run_to_run(M, N, K, act):
+    """The LayerNorm-fold consumer returns the same bytes on every call with the same inputs (r06: the
+    256 x 128-tile instance -- DA-v2's QKV, N = 1152 -- did not once a workgroup walked more than one
+    tile; N = 256 k + 128 now runs as a 256 x 256 part plus a one-tile-per-workgroup 256 x 128 part,
+    tools/probes/det_lnf.py)."""
+    ops = _ops()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M + N)
+    x = (_rand((M, K), g) * 2).to(torch.bfloat16).to(dev)
+    w = (_rand((N, K), g) / math.sqrt(K)).to(torch.bfloat16).to(dev)
+    b = _rand((N,), g).to(torch.float32).to(dev)
+    rs = torch.stack([torch.rand(M, generator=g, dtype=torch.float64) + 0.5, _rand((M,), g)], 1).to(torch.float32).to(dev).contiguous()
+    cs = _rand((N,), g).to(torch.float32).to(dev)
+    outs = []
+    for _ in range(8):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        ops.linear(x, w, bias=b, ln_rows=rs, col_sum=cs, act=act, out=out)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(outs[0].view(torch.int16), o.view(torch.int16))
