@@ -15,6 +15,14 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "two_process: two processes share the one GPU (run last)")
+
+
+def pytest_collection_modifyitems(config, items):
+    # two processes on one GPU are outside the deployment rule (one process per GPU) and their
+    # run-to-run determinism is a known open item ("two-process nondeterminism"):
+    # run them after every single-process test, so that under -x a failure there cannot hide the rest
+    items.sort(key=lambda it: it.get_closest_marker("two_process") is not None)
 
 
 @pytest.fixture(scope="session")

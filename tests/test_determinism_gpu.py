@@ -10,7 +10,7 @@ import sys
 import pytest
 
 torch = pytest.importorskip("torch")
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.two_process]
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 

@@ -44,20 +44,30 @@ def _worker(rank, ws, port, q):
         images = bench._images(B, S, rank, dev)
         pipe.capture(images)
         pipe2.capture(images)
-        og = D.OverlappedGather([pipe.replay, pipe2.replay], ws, B, pipe.points_per_image, dev)
+        last = {}
+
+        def run(k, fn):
+            def r():
+                last[k] = fn()
+                return last[k]
+            return r
+        og = D.OverlappedGather([run(0, pipe.replay), run(1, pipe2.replay)], ws, B, pipe.points_per_image, dev)
         for _ in range(3):
             slot = og.step()
         og.finish()
         gx, gr = og.gathered(slot)
-        # this rank's own images, unprojected by a separate eager call on the same depth
-        pipe.infer_depth(images)
-        mine = geometry.unproject_batch(pipe.depth, images, density="medium")
+        # the point buffers this rank's step handed to the gather (not rewritten since: the other
+        # pipeline ran in between).  Not a second eager forward: with two processes on the card the
+        # network is not guaranteed bit-identical run to run (the two-process
+        # nondeterminism); graph replay against eager in one process: test_dpt_gpu.py
+        mine = last[slot]
         torch.cuda.synchronize()
         q.put((rank, gx.cpu().numpy(), gr.cpu().numpy(), mine.xyz.cpu().numpy(), mine.rgb.cpu().numpy()))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.two_process
 def test_overlapped_gather_two_ranks_on_device_bit_identical():
     import torch.multiprocessing as mp
     ws, port = 2, _free_port()
@@ -76,7 +86,7 @@ def test_overlapped_gather_two_ranks_on_device_bit_identical():
     B = out[0][3].shape[0]
     for rank, gx, gr, _, _ in out:
         assert gx.shape[0] == ws * B
-        for src, _, _, mx, mr in out:         # rank src's images sit at [src*B, (src+1)*B)
+        for src, _, _, mx, mr in out:      # rank src's images sit at [src*B, (src+1)*B)
             assert gx[src * B:(src + 1) * B].tobytes() == mx.tobytes(), (rank, src)
             assert gr[src * B:(src + 1) * B].tobytes() == mr.tobytes(), (rank, src)
     assert out[0][3].tobytes() != out[1][3].tobytes()     # the ranks really had different images
