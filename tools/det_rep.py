@@ -13,7 +13,8 @@ Environment knobs (r05 root-cause of the r04 nondeterminism):
                  output at the call, and the hidden state at the end of the forward match run 1
   DET_PROBE=2    as 1, and each ln_apply runs twice on the same inputs (first into a scratch buffer);
                  reports per call whether the two outputs of the same run differ
-  DET_SYNC=1     with DET_PROBE, a host synchronise right after each ln_apply"""
+  DET_SYNC=1     with DET_PROBE, a host synchronise right after each ln_apply
+  DET_KNOBS=a=1,b=0  tuning knobs (i2pc_set_tuning) set in every process before the pipeline is built"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -25,6 +26,9 @@ def worker(rank, q, model, reps, graph):
     from image_to_pointcloud_amd.pipeline import PointCloudPipeline
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    for kv in filter(None, os.environ.get("DET_KNOBS", "").split(",")):   # name=value tuning knobs
+        k, v = kv.split("=")
+        _lib.call("i2pc_set_tuning", k.encode(), int(v))
     if os.environ.get("DET_GS"):
         _lib.call("i2pc_set_tuning", b"ln_apply_gs", int(os.environ["DET_GS"]))
     probe = os.environ.get("DET_PROBE") in ("1", "2")
